@@ -1,0 +1,66 @@
+"""Pin the CPU oracle against the golden vectors produced by the reference itself.
+
+CPU only (no GPU marker).  The oracle is a from-scratch restatement; these fixtures came
+from importing the reference's models/unet3d.py + utils/losses.py (make_golden.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet3d_cpu as ref
+from tests import golden_util as gu
+
+SHA0 = "30bd43350217be6678086943ef7d085e4c31cd929ca6fda2d4c56ba40fec9416"
+
+
+def test_init_hash_matches_reference_survey():
+    torch.manual_seed(0)
+    sd = ref.init_params(5, 1)
+    assert len(sd) == 136
+    assert gu.sd_hash(sd) == SHA0
+    assert sum(v.numel() for k, v in sd.items() if k in ref.param_keys(sd)) == 90311361
+
+
+@pytest.mark.parametrize("name", list(gu.CASES))
+def test_oracle_matches_golden(name):
+    g = gu.load(name)
+    ncls, n, spatial, lab, loss_kind, lr = gu.CASES[name]
+    torch.manual_seed(0)
+    sd = ref.init_params(5, ncls)
+    assert gu.sd_hash(sd) == str(g["sd_sha256"])
+    x, y = gu.batch(name, 0)
+    assert abs(float(x.double().sum()) - float(g["input_sum"])) < 1e-6
+    assert abs(float(y.double().sum()) - float(g["label_sum"])) < 1e-6
+    step = ref.RefStep(sd, lr=lr, loss=loss_kind)
+    loss0, logits = step.forward_backward(x, y)
+    np.testing.assert_allclose(logits.numpy(), g["logits_train"], rtol=0, atol=2e-5)
+    assert abs(float(loss0) - float(g["loss0"])) < 1e-5
+    for k in step.keys:
+        got = gu.sampled(sd[k].grad, g["g_stride__" + k])
+        exp = g["g__" + k]
+        scale = max(float(np.abs(exp).max()), 1e-12)
+        if k.endswith("conv.0.bias") or k.endswith("conv.3.bias"):
+            # pre-BN conv biases: exact gradient is 0, value is rounding noise
+            assert np.abs(got).max() < 1e-4
+            continue
+        np.testing.assert_allclose(got, exp, rtol=0, atol=1e-4 * scale + 1e-7, err_msg=k)
+    step.opt.step()
+    for k in step.keys:
+        if k.endswith("conv.0.bias") or k.endswith("conv.3.bias"):
+            continue  # H5: Adam normalises the bias noise into lr-sized updates
+        got = gu.sampled(sd[k].detach(), g["p_stride__" + k])
+        np.testing.assert_allclose(got, g["p__" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+    for k in sd:
+        if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+            np.testing.assert_allclose(sd[k].numpy(), g["b__" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+    with torch.no_grad():
+        le = ref.forward(sd, x, training=False)
+    np.testing.assert_allclose(le.numpy(), g["logits_eval"], rtol=0, atol=2e-4)
+    x1, y1 = gu.batch(name, 1)
+    loss1 = step.step(x1, y1)
+    assert abs(loss1 - float(g["loss1"])) < 1e-4
+
+
+def test_dice_shape_mismatch_raises():
+    with pytest.raises(ValueError):
+        ref.dice_loss(torch.zeros(1, 1, 2, 2, 2), torch.zeros(1, 2, 2, 2, 2))
