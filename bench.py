@@ -1,0 +1,185 @@
+"""Benchmark: train volumes/s of the 5-channel 3D U-Net (128x128x64, batch 2 per GPU,
+BCEDiceLoss, Adam) on MI355X — SURVEY.md §8(d), BASELINE.json config 2 (N=1) / config 3
+(N=8, launched by torch.distributed.run, one process per GPU, RCCL all-reduce).
+
+One "step" = Trainer.step on resident synthetic inputs: forward + loss + backward +
+(all-reduce) + Adam.  Prints ONE JSON line (rank 0) with the roofline of the stem conv
+(forward + weight-gradient kernels, HBM-bound, 578.9 MB algorithmic at N=2) measured with
+HIP events, and the CPU oracle timed on the host cores (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK = 2.5e15    # dense bf16 FLOP/s
+FLOP_PER_VOL = 5.72e12     # conv fwd+dgrad+wgrad per 5x128x128x64 volume
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=2, help="volumes per GPU")
+    ap.add_argument("--size", type=str, default="128,128,64")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--kernel-reps", type=int, default=30)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--zero-fill", action="store_true", help="config 4: 1-2 modalities zeroed")
+    return ap.parse_args()
+
+
+def stem_roofline(tr, N, spatial, reps):
+    """Time the stem conv (5->64, k3) forward and weight-gradient launches with HIP events
+    on the launch stream, rotating 3 buffer sets (> 256 MiB Infinity Cache)."""
+    from pcms_amd import _lib as L
+    eng = tr.model.engine()
+    code = eng.code
+    D, H, W = spatial
+    nvox = N * D * H * W
+    cs = eng.convs[0]
+    T = eng.tdtype
+    sets = []
+    for i in range(3):
+        xin = torch.rand(nvox * eng.cp, device="cuda").to(T)
+        y = torch.empty(nvox * 64, dtype=T, device="cuda")
+        dy = torch.randn(nvox * 64, device="cuda").to(T)
+        sets.append((xin, y, dy))
+    rows = L.query("pcms_conv3_mblocks", N, D, H, W)
+    stats = torch.empty(rows * 64 * 2, device="cuda")
+    dw = torch.zeros(64 * 5 * 27, device="cuda")
+    dwt = torch.empty(27 * 64 * eng.cp, device="cuda")
+
+    def fwd(s):
+        L.call("pcms_conv3_fwd", code, s[0], eng.cp, None, 0, cs.fwd, cs.mod.bias, s[1], None, 64, None, stats,
+               0, N, D, H, W, 64, 1)
+
+    def wgrad(s):
+        L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 512)
+
+    res = {}
+    for name, fn in (("fwd", fwd), ("wgrad", wgrad)):
+        for i in range(3):
+            fn(sets[i % 3])
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for i in range(reps):
+            fn(sets[i % 3])
+        ev1.record()
+        ev1.synchronize()
+        res[name] = ev0.elapsed_time(ev1) / reps * 1e-3  # s per launch
+    es = 2 if code == 1 else 4
+    # algorithmic bytes: X (5 ch) + W + Y  /  X + dY + dW
+    xb = nvox * 5 * es
+    yb = nvox * 64 * es
+    fwd_bytes = xb + 64 * 5 * 27 * es + yb
+    wg_bytes = xb + yb + 64 * 5 * 27 * 4
+    t = res["fwd"] + res["wgrad"]
+    achieved = (fwd_bytes + wg_bytes) / t
+    return {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+            "kernel": "stem conv3d 5->64 fwd + wgrad (conv3_fwd_kernel + conv3_wgrad_kernel)",
+            "algorithmic_bytes": fwd_bytes + wg_bytes, "t_fwd_us": round(res["fwd"] * 1e6, 1),
+            "t_wgrad_us": round(res["wgrad"] * 1e6, 1)}
+
+
+def cpu_baseline(spatial):
+    """The CPU oracle (a restatement of utils/trainer.py:179-195 on torch CPU fp32) timed on
+    this host: one BCEDice train step of ONE volume (bounded sample, ~10-30 s)."""
+    from oracle import unet3d_cpu as ref
+    from pcms_amd.synthetic import make_batch
+    cores = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    torch.set_num_threads(cores)
+    torch.manual_seed(0)
+    sd = ref.init_params(5, 1)
+    step = ref.RefStep(sd, lr=1e-4, loss="bce_dice")
+    b = make_batch(1, spatial, seed=1234)
+    t0 = time.perf_counter()
+    step.step(b["image"], b["label"])
+    dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 4), "unit": "volumes/s", "cores": cores, "kind": "port",
+            "sample": f"1 train step (fwd+BCEDice+bwd+Adam), batch 1 x 5x{'x'.join(map(str, spatial))}, "
+                      f"torch CPU fp32, {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import pcms_amd
+    from pcms_amd.synthetic import make_batch, step_seed
+    from pcms_amd.utils.trainer import Trainer
+
+    spatial = tuple(int(v) for v in a.size.split(","))
+    torch.manual_seed(0)
+    cfg = {"device": f"cuda:{local}", "learning_rate": 1e-4, "batch_size": a.batch, "num_epochs": 1,
+           "loss": "bce_dice", "precision": a.precision}
+    tr = Trainer(cfg)
+    batches = []
+    for i in range(2):
+        b = make_batch(a.batch, spatial, seed=step_seed(rank, i), zero_fill=a.zero_fill)
+        batches.append({"image": b["image"].cuda(), "label": b["label"].cuda()})
+    for i in range(a.warmup):
+        tr.step_async(batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for i in range(a.steps):
+        last = tr.step_async(batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    loss = float(last) if last is not None else float("nan")
+    dtt = torch.tensor([dt], device="cuda", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(dtt, op=dist.ReduceOp.MAX)
+    dt = float(dtt)
+    vols = world * a.batch * a.steps
+    value = vols / dt
+    roof = stem_roofline(tr, a.batch, spatial, a.kernel_reps) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(spatial)
+    if rank == 0:
+        vox = spatial[0] * spatial[1] * spatial[2]
+        flops = FLOP_PER_VOL * vox / (128 * 128 * 64) * vols
+        out = {
+            "metric": "train volumes/sec (5ch 128x128x64)", "value": round(value, 3), "unit": "volumes/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.precision,
+            "data": "synthetic (U[0,1) images, ellipsoid labels; random-init weights, seed 0)",
+            "config": {"workload": f"UNet3D 5->1, {a.batch} x 5x{'x'.join(map(str, spatial))} per GPU, "
+                                   f"BCEDiceLoss, Adam(1e-4, wd 1e-5){', zero_fill' if a.zero_fill else ''}",
+                       "global_batch": world * a.batch, "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "mfma_util_step": round(flops / dt / MFMA_BF16_PEAK, 4), "final_loss": round(loss, 5),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+/*
+ * pcms_hip.h — C ABI of libpcms_hip.so, the MI355X (gfx950) kernels behind the drop-in
+ * UNet3D / DiceLoss / BCEDiceLoss / Trainer.step of
+ * qwertyhgb/Prostate-Cancer-Multimodal-Segmentation.
+ *
+ * The reference has no FFI: its hot path is PyTorch aten called from Python.  Each entry
+ * point below replaces the aten op(s) named in its comment (paths relative to the
+ * reference repo root).  The Python host layer (pcms_amd) binds these through ctypes.
+ *
+ * Conventions
+ *   - dtype: 0 = fp32 storage (parity build), 1 = bf16 storage (performance build).
+ *     Accumulation is always fp32; statistics are combined in fp64.
+ *   - Activations are NDHWC, contiguous, channel pitch = channel count.
+ *   - Pointers are device pointers; the caller owns every buffer (no allocation inside,
+ *     except workspace passed in).  `s` is a hipStream_t; every call is stream-ordered and
+ *     returns 0 on success, a hipError_t code, or a negative code for a bad argument.
+ */
+#ifndef PCMS_HIP_H
+#define PCMS_HIP_H
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- layout ---------------------------------------------------------------------- */
+/* batch['image'] (N, Cin, D, H, W) fp32 NCDHW -> NDHWC, channels zero-padded to Cp.
+ * Replaces the implicit layout of images.to(device) (utils/trainer.py:179).          */
+int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long V, int Cp, hipStream_t s);
+
+/* ---- Conv3d(k=3, padding=1): models/unet3d.py:29,35 ------------------------------- */
+int pcms_conv3_chunk(int dtype);                  /* input channels per K-chunk        */
+int pcms_conv3_mblocks(int N, int D, int H, int W);/* rows of the BN partial buffer     */
+/* master W [Cout][Cin][3][3][3] fp32 -> kernel pack; flip=1 builds the dgrad pack      */
+int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s);
+/* Y = conv(X) + bias, X = channel-concat(x0[:, :c0], x1[:, :c1]) (Up3D cat, :156),
+ * output channels [0, cy0) -> y0, [cy0, Cout) -> y1 (dgrad concat split).
+ * stats: [mblocks][Cout][2] fp32 BN partials (sum, sumsq) or NULL.  splits > 1: fp32
+ * atomic accumulation into the zeroed yacc [Nvox][Cout]; finish with
+ * pcms_split_epilogue.  Also used for dgrad with the flip pack.                      */
+int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
+                   const void* wpack, const float* bias, void* y0, void* y1, int cy0,
+                   float* yacc, float* stats, int accumulate,
+                   int N, int D, int H, int W, int Cout, int splits, hipStream_t s);
+/* dw [Cout][Cin][27] fp32 += sum_v dy[v, co] * x[v + tap, ci];  dwt = 27*Cout*Cin fp32 ws */
+int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
+                     float* dw, float* dwt, int N, int D, int H, int W, int Cout, int target_wgs,
+                     hipStream_t s);
+int pcms_split_epilogue_rows(long nvox);
+int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0,
+                        float* stats, int C, long nvox, hipStream_t s);
+
+/* ---- BatchNorm3d (train / eval) + ReLU(inplace): models/unet3d.py:31-39 ----------- */
+int pcms_bn_finalize(const float* part, int rows, int C, double count, const float* gamma,
+                     const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                     float eps, float* scale, float* shift, float* mean, float* invstd, hipStream_t s);
+int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                        float eps, int C, float* scale, float* shift, hipStream_t s);
+int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const float* shift, int C,
+                 long nvox, hipStream_t s);
+int pcms_bn_bwd_rows(int dtype, int C, long nvox);
+/* dy = BN+ReLU backward(da); dgamma/dbeta += ; part: rows*C*2 fp32; coef: 3*C fp32   */
+int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scale, const float* shift,
+                     const float* mean, const float* invstd, const float* gamma, float* part, float* coef,
+                     float* dgamma, float* dbeta, void* dy, int C, long nvox, hipStream_t s);
+
+/* ---- MaxPool3d(2): models/unet3d.py:80 ------------------------------------------- */
+int pcms_maxpool_fwd(int dtype, const void* a, void* p, int N, int D, int H, int W, int C, hipStream_t s);
+/* da[argmax] += dp (first max in d,h,w scan order wins, as PyTorch)                  */
+int pcms_maxpool_bwd(int dtype, const void* a, const void* dp, void* da, int N, int D, int H, int W,
+                     int C, hipStream_t s);
+
+/* ---- ConvTranspose3d(k=2, s=2) + F.pad: models/unet3d.py:120,139-151 --------------- */
+int pcms_convt_pack(int dtype, const float* w, void* out, int Cin, int Cout, int dgrad, hipStream_t s);
+int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bias, void* out,
+                   int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
+int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
+                     int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
+int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
+                     int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
+                     int target_wgs, hipStream_t s);
+/* out[c] += sum over the sub-box of x (ConvTranspose3d bias gradient)                  */
+int pcms_box_channel_sum(int dtype, const void* x, float* out, int N, int D, int H, int W, int C,
+                         int z0, int y0, int x0, int bd, int bh, int bw, hipStream_t s);
+
+/* ---- outc Conv3d(64, ncls, 1): models/unet3d.py:222,295 ---------------------------- */
+int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* logits,
+                  long nvox_per_n, int N, int ncls, hipStream_t s);
+int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w, void* da, float* dw,
+                  float* db, long nvox_per_n, int N, int ncls, hipStream_t s);
+
+/* ---- DiceLoss / BCEDiceLoss: utils/losses.py:44-92, 124-152 ------------------------ */
+int pcms_loss_rows(long M);
+int pcms_loss_fwd(const float* x, const float* t, long M, float smooth, float wb, float wd, float* part,
+                  double* sums, float* loss, hipStream_t s);
+int pcms_loss_bwd(const float* x, const float* t, long M, const double* sums, float smooth, float wb,
+                  float wd, const float* gout, float* dx, hipStream_t s);
+
+/* ---- torch.optim.Adam(lr, weight_decay=1e-5): utils/trainer.py:113-117 ------------- */
+/* g_eff = gscale * g + wd * p (gscale = 1/world for the data-parallel mean)           */
+int pcms_adam(float* p, const float* g, float* m, float* v, long n, float step_size, float b1, float b2,
+              float eps, float wd, float bc2_sqrt, float gscale, hipStream_t s);
+
+/* ---- misc -------------------------------------------------------------------------- */
+int pcms_add(int dtype, void* dst, const void* src, long n, hipStream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCMS_HIP_H */

@@ -1,0 +1,112 @@
+"""ctypes binding of libpcms_hip.so (the C ABI declared in include/pcms_hip.h).
+
+There is no fallback: if the library is missing or a call fails, this raises.  Tensors are
+passed as raw device pointers; every call is enqueued on the current torch stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpcms_hip.so")
+
+F32, BF16 = 0, 1
+
+# name -> argument codes: i int32, l int64, d double, f float, p pointer, s hipStream_t
+SIGNATURES = {
+    "pcms_pack_input": "ippiilis",
+    "pcms_conv3_chunk": "i",
+    "pcms_conv3_mblocks": "iiii",
+    "pcms_conv3_pack": "ippiiis",
+    "pcms_conv3_fwd": "ipipippppippiiiiiiis",
+    "pcms_conv3_wgrad": "ipipipppiiiiiis",
+    "pcms_split_epilogue_rows": "l",
+    "pcms_split_epilogue": "ippppipils",
+    "pcms_bn_finalize": "piidpppppffpppps",
+    "pcms_bn_eval_coeffs": "ppppfipps",
+    "pcms_bn_relu": "ippppils",
+    "pcms_bn_bwd_rows": "iil",
+    "pcms_bn_relu_bwd": "i" + "p" * 12 + "ils",
+    "pcms_maxpool_fwd": "ippiiiiis",
+    "pcms_maxpool_bwd": "ipppiiiiis",
+    "pcms_convt_pack": "ippiiis",
+    "pcms_convt_fwd": "ippppiiiiiiiiis",
+    "pcms_convt_dgrad": "ipppiiiiiiiiis",
+    "pcms_convt_wgrad": "ippppiiiiiiiiiis",
+    "pcms_box_channel_sum": "ippiiiiiiiiiiis",
+    "pcms_head_fwd": "ippppliis",
+    "pcms_head_bwd": "ippppppliis",
+    "pcms_loss_rows": "l",
+    "pcms_loss_fwd": "pplfffppps",
+    "pcms_loss_bwd": "pplpfffpps",
+    "pcms_adam": "pppplfffffffs",
+    "pcms_add": "ippls",
+}
+
+_CT = {"i": ctypes.c_int, "l": ctypes.c_long, "d": ctypes.c_double, "f": ctypes.c_float,
+       "p": ctypes.c_void_p, "s": ctypes.c_void_p}
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library; raises (never falls back) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). pcms_amd has no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, sig in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = [_CT[c] for c in sig]
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name: str, *args):
+    """Call ``name`` with tensors/None/ints/floats; appends the current stream."""
+    lib = load()
+    conv = []
+    sig = SIGNATURES[name]
+    for code, a in zip(sig, args):
+        if code == "p":
+            conv.append(ptr(a))
+        else:
+            conv.append(a)
+    if sig.endswith("s"):
+        conv.append(stream())
+    rc = getattr(lib, name)(*conv)
+    if rc != 0 and sig.endswith("s"):
+        raise HipError(f"{name} failed with status {rc}")
+    return rc
+
+
+def query(name: str, *args) -> int:
+    """Host-only helpers (no stream): sizes / counts."""
+    return getattr(load(), name)(*args)

@@ -1,0 +1,79 @@
+// Shared device helpers for the gfx950 (CDNA4) U-Net kernels.
+//
+// Storage types: activations are NDHWC in either fp32 (parity build) or bf16
+// (performance build, raw bits in uint16_t).  All accumulation is fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;  // raw bf16 bits (same bytes as torch.bfloat16)
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+
+#define LDS_AS __attribute__((address_space(3)))
+
+enum { PCMS_F32 = 0, PCMS_BF16 = 1 };
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  // round-to-nearest-even via the hardware convert (v_cvt_pk_bf16_f32 on gfx950)
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+  static __device__ __forceinline__ float cvt(float v) { return v; }
+  static constexpr int kVec = 4;  // elements per 16-byte vector
+};
+template <> struct Elem<bf16_t> {
+  static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+  static __device__ __forceinline__ bf16_t cvt(float v) { return f2bf(v); }
+  static constexpr int kVec = 8;
+};
+
+// 16-byte vector load/store of kVec elements as floats.
+template <typename T> __device__ __forceinline__ void load16(const T* p, float* out);
+template <> __device__ __forceinline__ void load16<float>(const float* p, float* out) {
+  f32x4_t v = *reinterpret_cast<const f32x4_t*>(p);
+  out[0] = v[0]; out[1] = v[1]; out[2] = v[2]; out[3] = v[3];
+}
+template <> __device__ __forceinline__ void load16<bf16_t>(const bf16_t* p, float* out) {
+  u32x4_t v = *reinterpret_cast<const u32x4_t*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    out[2 * i] = __uint_as_float(v[i] << 16);
+    out[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+template <typename T> __device__ __forceinline__ void store16(T* p, const float* in);
+template <> __device__ __forceinline__ void store16<float>(float* p, const float* in) {
+  f32x4_t v = {in[0], in[1], in[2], in[3]};
+  *reinterpret_cast<f32x4_t*>(p) = v;
+}
+template <> __device__ __forceinline__ void store16<bf16_t>(bf16_t* p, const float* in) {
+  u32x4_t v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = (uint32_t)f2bf(in[2 * i]) | ((uint32_t)f2bf(in[2 * i + 1]) << 16);
+  *reinterpret_cast<u32x4_t*>(p) = v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+#define PCMS_CHECK_LAUNCH() return (int)hipGetLastError()
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,632 @@
+// 3x3x3 / stride 1 / pad 1 convolution for the U-Net DoubleConv blocks, NDHWC, gfx950.
+//
+// Replaces nn.Conv3d(k=3, padding=1) of models/unet3d.py:29,35 (forward, and the two
+// autograd backward products of aten::convolution_backward).
+//
+//   conv3_fwd   implicit GEMM  Y[v, co] = sum_{tap, ci} X[v + tap, ci] * W[co, ci, tap]
+//               M = voxels (a spatial box of <= 512 voxels per workgroup), N = 64 output
+//               channels per workgroup, K = 27 * Cin walked as (ci-chunk, tap).  The
+//               chunk's (box + halo) input tile is staged once in LDS and re-read for all
+//               27 taps through an LDS row offset; weights stream from L2 into registers.
+//               Epilogue: + bias, store, per-workgroup BatchNorm partial sums (sum, sumsq).
+//               Also serves dgrad (dX = conv(dY, W flipped + transposed)), with
+//               `accumulate` and a two-pointer output for the concat split of Up3D.
+//   conv3_wgrad dW[tap, co, ci] += sum_v dY[v, co] * X[v + tap, ci]   (K = voxels)
+//               Both MFMA operands need the voxel index contiguous: they are read from
+//               natural NDHWC LDS tiles with ds_read_b64_tr_b16 (hardware transpose).
+//
+// bf16 path: v_mfma_f32_32x32x16_bf16; fp32 path (parity build): v_mfma_f32_32x32x2_f32.
+#include "common.h"
+#include "pcms_hip.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kRowBytes = 64;      // one halo row = one LDS row of the current ci-chunk
+constexpr int kHaloMax = 1152;     // halo voxels per workgroup (72 KiB LDS, 2 WG / CU)
+
+template <typename T> struct Traits;
+template <> struct Traits<bf16_t> {
+  static constexpr int CK = 32;    // channels per chunk (64 B rows)
+  static constexpr int KS = 2;     // MFMA k-steps per chunk and tap (K = 16 each)
+  static constexpr int VEC = 8;    // elements per 16-byte piece
+  typedef s16x8_t Frag;
+};
+template <> struct Traits<float> {
+  static constexpr int CK = 16;
+  static constexpr int KS = 8;     // K = 2 each
+  static constexpr int VEC = 4;
+  typedef float Frag;
+};
+
+__device__ __forceinline__ f32x16_t mfma(s16x8_t a, s16x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16_t mfma(float a, float b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// 16-byte slot swizzle inside a 64-byte halo row (spreads ds_read_b128 lane groups).
+__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+
+// A fragment from the halo tile. ks = k-step inside the chunk, h = lane >> 5.
+__device__ __forceinline__ s16x8_t lds_a(const char* lds, int row, int ks, int h, bf16_t*) {
+  int slot = (ks * 2 + h) ^ swz(row);
+  return *reinterpret_cast<const s16x8_t*>(lds + row * kRowBytes + slot * 16);
+}
+__device__ __forceinline__ float lds_a(const char* lds, int row, int ks, int h, float*) {
+  int c = ks * 2 + h;  // channel in chunk (0..15)
+  int slot = (c >> 2) ^ swz(row);
+  return *reinterpret_cast<const float*>(lds + row * kRowBytes + slot * 16 + (c & 3) * 4);
+}
+// B fragment (weights) straight from global: packed [chunk][27][Cout][CK].
+__device__ __forceinline__ s16x8_t gl_b(const bf16_t* wrow, int ks, int h) {
+  return *reinterpret_cast<const s16x8_t*>(wrow + ks * 16 + h * 8);
+}
+__device__ __forceinline__ float gl_b(const float* wrow, int ks, int h) { return wrow[ks * 2 + h]; }
+
+struct Conv3Params {
+  const void* x0; const void* x1; int c0; int c1;
+  const void* w; const float* bias;
+  void* y0; void* y1; int cy0;
+  float* yacc; float* stats;
+  int accumulate;
+  int N, D, H, W, Cin, Cout;
+  int nchunk, chunks_per_split;
+  int lbd, lbh, lbw, nbd, nbh, nbw;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads, 2) conv3_fwd_kernel(Conv3Params p) {
+  typedef Traits<T> Tr;
+  typedef typename Tr::Frag Frag;
+  __shared__ __attribute__((aligned(16))) char lds[kHaloMax * kRowBytes];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r_lane = lane & 31, hsel = lane >> 5;
+  int mb = blockIdx.x;
+  const int bwi = mb % p.nbw; mb /= p.nbw;
+  const int bhi = mb % p.nbh; mb /= p.nbh;
+  const int bdi = mb % p.nbd;
+  const int n = mb / p.nbd;
+  const int co_base = blockIdx.y * 64;
+  const int cbeg = blockIdx.z * p.chunks_per_split;
+  const int cend = min(p.nchunk, cbeg + p.chunks_per_split);
+  const int bd = 1 << p.lbd, bh = 1 << p.lbh, bw = 1 << p.lbw;
+  const int boxvol = bd * bh * bw;
+  const int d0 = bdi * bd, h0 = bhi * bh, w0 = bwi * bw;
+  const int HH = bh + 2, HW = bw + 2;
+  const int HV = (bd + 2) * HH * HW;
+
+  int hb[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    int r = wave * 128 + mt * 32 + r_lane;
+    if (r >= boxvol) r = 0;
+    int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+    hb[mt] = (rd * HH + rh) * HW + rw;
+  }
+  const bool wave_active = wave * 128 < boxvol;
+
+  f32x16_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const T* x0 = (const T*)p.x0;
+  const T* x1 = (const T*)p.x1;
+  const T* wp = (const T*)p.w;
+  const long plane = (long)p.H * p.W;
+
+  for (int chunk = cbeg; chunk < cend; ++chunk) {
+    __syncthreads();
+    // ---- stage the halo tile of this chunk: HV rows x 4 pieces of 16 B ----
+    for (int pc = tid; pc < HV * 4; pc += kThreads) {
+      const int hv = pc >> 2, q = pc & 3;
+      const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+      const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+      const int c = chunk * Tr::CK + q * Tr::VEC;
+      u32x4_t v = {0u, 0u, 0u, 0u};
+      if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
+        const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+        const T* src = (c < p.c0) ? x0 + vox * p.c0 + c : x1 + vox * p.c1 + (c - p.c0);
+        v = *reinterpret_cast<const u32x4_t*>(src);
+      }
+      *reinterpret_cast<u32x4_t*>(lds + hv * kRowBytes + ((q ^ swz(hv)) * 16)) = v;
+    }
+    __syncthreads();
+    if (!wave_active) continue;
+
+    const T* wchunk = wp + (long)chunk * 27 * p.Cout * Tr::CK;
+    Frag bcur[2][Tr::KS], bnxt[2][Tr::KS];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < Tr::KS; ++ks)
+        bnxt[nt][ks] = gl_b(wchunk + (long)(co_base + nt * 32 + r_lane) * Tr::CK, ks, hsel);
+
+    for (int tap = 0; tap < 27; ++tap) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < Tr::KS; ++ks) bcur[nt][ks] = bnxt[nt][ks];
+      if (tap + 1 < 27) {
+        const T* wt = wchunk + ((long)(tap + 1) * p.Cout + co_base + r_lane) * Tr::CK;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int ks = 0; ks < Tr::KS; ++ks) bnxt[nt][ks] = gl_b(wt + nt * 32 * Tr::CK, ks, hsel);
+      }
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      const int off = (kd * HH + kh) * HW + kw;
+#pragma unroll
+      for (int ks = 0; ks < Tr::KS; ++ks) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          Frag a = lds_a(lds, hb[mt] + off, ks, hsel, (T*)nullptr);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a, bcur[nt][ks], acc[mt][nt]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue ----
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  if (wave_active) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = wave * 128 + mt * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+        if (r >= boxvol) continue;
+        const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+        const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+        if (gd >= p.D || gh >= p.H || gw >= p.W) continue;
+        const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int co = co_base + nt * 32 + r_lane;
+          float v = acc[mt][nt][e];
+          if (p.yacc) {
+            atomicAdd(p.yacc + vox * p.Cout + co, v);
+            continue;
+          }
+          if (p.bias) v += p.bias[co];
+          T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co
+                                : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
+          if (p.accumulate) v += Elem<T>::ld(dst);
+          Elem<T>::st(dst, v);
+          s1[nt] += v;
+          s2[nt] += v * v;
+        }
+      }
+    }
+  }
+  if (p.stats && !p.yacc) {
+    __syncthreads();  // halo no longer read: reuse LDS for the cross-wave reduction
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      s1[nt] += __shfl_xor(s1[nt], 32, 64);
+      s2[nt] += __shfl_xor(s2[nt], 32, 64);
+      if (hsel == 0) {
+        red[(wave * 64 + nt * 32 + r_lane) * 2 + 0] = s1[nt];
+        red[(wave * 64 + nt * 32 + r_lane) * 2 + 1] = s2[nt];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        a += red[(w * 64 + tid) * 2 + 0];
+        b += red[(w * 64 + tid) * 2 + 1];
+      }
+      float* st = p.stats + ((long)blockIdx.x * p.Cout + co_base + tid) * 2;
+      st[0] = a;
+      st[1] = b;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// weight-gradient kernel
+// ------------------------------------------------------------------------------------
+constexpr int kWThreads = 512;          // 8 waves: wave = (co-tile, tap-group)
+constexpr int kWHaloMax = 720;          // halo rows (box <= 256 voxels)
+
+template <typename T> struct WTraits;
+template <> struct WTraits<bf16_t> {
+  static constexpr int BV = 256;        // voxels per staged box
+  static constexpr int KV = 16;         // voxels per MFMA
+  static constexpr int NBUF = 2;
+  static constexpr int DYROW = 128;     // 64 co x 2 B
+  static constexpr int XROW = 64;       // 32 ci x 2 B
+  static constexpr int VEC = 8;
+  typedef s16x8_t Frag;
+};
+template <> struct WTraits<float> {
+  static constexpr int BV = 128;
+  static constexpr int KV = 2;
+  static constexpr int NBUF = 1;
+  static constexpr int DYROW = 256;     // 64 co x 4 B
+  static constexpr int XROW = 128;      // 32 ci x 4 B
+  static constexpr int VEC = 4;
+  typedef float Frag;
+};
+
+struct WgradParams {
+  const void* x0; const void* x1; int c0; int c1;
+  const void* dy;
+  float* dwt;            // fp32 workspace [27][Cout][Cin] (atomic accumulate)
+  int N, D, H, W, Cin, Cout;
+  int lbd, lbh, lbw, nbd, nbh, nbw;
+  int nbox, boxes_per_split;
+};
+
+// dy tile: 128-B (bf16) rows, 64-B halves swizzled by row bit 1 (conflict-free tr reads).
+__device__ __forceinline__ int dy_off_bf16(int v, int co) {  // co in 0..63 (element)
+  int half = (co >> 5) ^ ((v >> 1) & 1);
+  return v * 128 + half * 64 + (co & 31) * 2;
+}
+
+__device__ __forceinline__ s16x4_t tr_read(const char* lds, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + byte_off));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p) {
+  typedef WTraits<T> Tr;
+  typedef typename Tr::Frag Frag;
+  constexpr int DYBYTES = Tr::BV * Tr::DYROW;
+  constexpr int XBYTES = kWHaloMax * Tr::XROW;
+  constexpr int BUFBYTES = DYBYTES + XBYTES;
+  extern __shared__ __attribute__((aligned(16))) char wlds[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hsel = lane >> 5;
+  const int cot = wave & 1;           // co tile (32 rows of the 64-wide dy tile)
+  const int tg = wave >> 1;           // taps tg, tg+4, ...
+  const int ntap = (tg == 3) ? 6 : 7;
+  const int co_base = blockIdx.y * 64;
+  const int ci_base = blockIdx.z * 32;
+  const int bd = 1 << p.lbd, bh = 1 << p.lbh, bw = 1 << p.lbw;
+  const int HH = bh + 2, HW = bw + 2;
+  const int HV = (bd + 2) * HH * HW;
+  const int boxvol = bd * bh * bw;
+  const long plane = (long)p.H * p.W;
+  const T* x0 = (const T*)p.x0;
+  const T* x1 = (const T*)p.x1;
+  const T* dy = (const T*)p.dy;
+
+  const int b_beg = blockIdx.x * p.boxes_per_split;
+  const int b_end = min(p.nbox, b_beg + p.boxes_per_split);
+
+  f32x16_t acc[7];
+#pragma unroll
+  for (int t = 0; t < 7; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+
+  // register staging: pieces of 16 B
+  constexpr int DYP = Tr::BV * Tr::DYROW / 16;
+  const int XP = HV * Tr::XROW / 16;
+  constexpr int MAXP = (DYP + kWHaloMax * Tr::XROW / 16 + kWThreads - 1) / kWThreads;
+  u32x4_t stg[MAXP];
+
+  auto box_origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    int bwi = b % p.nbw; b /= p.nbw;
+    int bhi = b % p.nbh; b /= p.nbh;
+    int bdi = b % p.nbd;
+    n = b / p.nbd;
+    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
+  };
+  auto stage_load = [&](int b) {
+    int n, d0, h0, w0;
+    box_origin(b, n, d0, h0, w0);
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int pc = tid + i * kWThreads;
+      u32x4_t v = {0u, 0u, 0u, 0u};
+      if (pc < DYP) {
+        const int r = pc / (Tr::DYROW / 16), q = pc % (Tr::DYROW / 16);
+        if (r < boxvol) {
+          const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+          const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+          if (gd < p.D && gh < p.H && gw < p.W) {
+            const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+            v = *reinterpret_cast<const u32x4_t*>(dy + vox * p.Cout + co_base + q * Tr::VEC);
+          }
+        }
+      } else if (pc < DYP + XP) {
+        const int hp = pc - DYP;
+        const int hv = hp / (Tr::XROW / 16), q = hp % (Tr::XROW / 16);
+        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+        const int c = ci_base + q * Tr::VEC;
+        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
+          const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+          const T* src = (c < p.c0) ? x0 + vox * p.c0 + c : x1 + vox * p.c1 + (c - p.c0);
+          v = *reinterpret_cast<const u32x4_t*>(src);
+        }
+      }
+      stg[i] = v;
+    }
+  };
+  auto stage_store = [&](char* buf) {
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int pc = tid + i * kWThreads;
+      if (pc < DYP) {
+        const int r = pc / (Tr::DYROW / 16), q = pc % (Tr::DYROW / 16);
+        int off;
+        if (sizeof(T) == 2) off = dy_off_bf16(r, q * 8);
+        else off = r * Tr::DYROW + q * 16;
+        *reinterpret_cast<u32x4_t*>(buf + off) = stg[i];
+      } else if (pc < DYP + XP) {
+        const int hp = pc - DYP;
+        *reinterpret_cast<u32x4_t*>(buf + DYBYTES + hp * 16) = stg[i];
+      }
+    }
+  };
+
+  // per-lane voxel-row helpers for the k index (voxel inside the box)
+  auto halo_row = [&](int r) {
+    const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+    return (rd * HH + rh) * HW + rw;
+  };
+
+  auto compute = [&](const char* buf) {
+    const char* xb = buf + DYBYTES;
+    for (int k0 = 0; k0 < boxvol; k0 += Tr::KV) {
+      Frag a;
+      Frag bf[7];
+      if constexpr (sizeof(T) == 2) {
+        // lane 4q+p of each 16-lane group: row q, cols 4p..4p+3 of a 4x16 block
+        const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+        const int v_a = k0 + 8 * hsel + qq;          // rows for elements 0..3; +4 for 4..7
+        const int co = cot * 32 + g * 16 + pp * 4;
+        s16x4_t lo = tr_read(buf, dy_off_bf16(v_a, co));
+        s16x4_t hi = tr_read(buf, dy_off_bf16(v_a + 4, co));
+        a = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const int hr0 = halo_row(v_a), hr1 = halo_row(v_a + 4);
+        const int ci = g * 16 + pp * 4;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          if (j < ntap) {
+            const int tap = tg + 4 * j;
+            const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+            const int off = (kd * HH + kh) * HW + kw;
+            s16x4_t l2 = tr_read(xb, (hr0 + off) * Tr::XROW + ci * 2);
+            s16x4_t h2 = tr_read(xb, (hr1 + off) * Tr::XROW + ci * 2);
+            bf[j] = (s16x8_t){l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
+          }
+        }
+      } else {
+        const int v = k0 + hsel;
+        a = *reinterpret_cast<const float*>(buf + v * Tr::DYROW + (cot * 32 + (lane & 31)) * 4);
+        const int hr = halo_row(v);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          if (j < ntap) {
+            const int tap = tg + 4 * j;
+            const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+            const int off = (kd * HH + kh) * HW + kw;
+            bf[j] = *reinterpret_cast<const float*>(xb + (hr + off) * Tr::XROW + (lane & 31) * 4);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+        if (j < ntap) acc[j] = mfma(a, bf[j], acc[j]);
+    }
+  };
+
+  if (b_beg < b_end) {
+    if constexpr (Tr::NBUF == 2) {
+      stage_load(b_beg);
+      stage_store(wlds);
+      __syncthreads();
+      for (int b = b_beg; b < b_end; ++b) {
+        const int cur = (b - b_beg) & 1;
+        if (b + 1 < b_end) stage_load(b + 1);
+        compute(wlds + cur * BUFBYTES);
+        if (b + 1 < b_end) stage_store(wlds + (cur ^ 1) * BUFBYTES);
+        __syncthreads();
+      }
+    } else {
+      for (int b = b_beg; b < b_end; ++b) {
+        stage_load(b);
+        __syncthreads();
+        stage_store(wlds);
+        __syncthreads();
+        compute(wlds);
+      }
+    }
+  }
+
+  // flush: C[row = co][col = ci] of tap -> dwt[tap][co][ci] (coalesced along ci)
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    if (j >= ntap) continue;
+    const int tap = tg + 4 * j;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int co = co_base + cot * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+      const int ci = ci_base + (lane & 31);
+      if (co < p.Cout && ci < p.Cin)
+        atomicAdd(p.dwt + ((long)tap * p.Cout + co) * p.Cin + ci, acc[j][e]);
+    }
+  }
+}
+
+// dwt [27][Cout][Cin] (fp32 workspace) -> dw [Cout][Cin][27] (+=), torch OIDHW layout
+__global__ void wgrad_permute_kernel(const float* dwt, float* dw, int Cout, int Cin) {
+  const long total = (long)Cout * Cin * 27;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int t = i % 27;
+    const long oc = i / 27;
+    const int ci = oc % Cin, co = oc / Cin;
+    dw[i] += dwt[((long)t * Cout + co) * Cin + ci];
+  }
+}
+
+// master fp32 W[Cout][Cin][27] -> packed T [chunk][27][J][CK]
+//   fwd  (flip=0): J = Cout, k-index = ci
+//   dgrad(flip=1): J = Cin,  k-index = co, tap mirrored (26 - t)
+template <typename T, int CK>
+__global__ void pack_conv3_kernel(const float* w, T* out, int Cout, int Cin, int flip, int nchunk) {
+  const int J = flip ? Cin : Cout;
+  const int Kdim = flip ? Cout : Cin;
+  const long total = (long)nchunk * 27 * J * CK;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int k = i % CK;
+    long r = i / CK;
+    const int j = r % J; r /= J;
+    const int t = r % 27;
+    const int chunk = r / 27;
+    const int kk = chunk * CK + k;
+    float v = 0.f;
+    if (kk < Kdim) v = flip ? w[((long)kk * Cin + j) * 27 + (26 - t)] : w[((long)j * Cin + kk) * 27 + t];
+    out[i] = Elem<T>::cvt(v);
+  }
+}
+
+struct Box { int lbd, lbh, lbw; };
+
+int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
+
+// Pick a power-of-two box (<= maxvol voxels, halo <= maxhalo rows) minimising padded
+// volume (then maximising box size) for a D x H x W grid.
+Box choose_box(int D, int H, int W, int maxvol, int maxhalo, int minw, int minvol) {
+  Box best{0, 0, 0};
+  double best_cost = 1e30;
+  for (int a = 0; a <= 4; ++a)
+    for (int b = 0; b <= 5; ++b)
+      for (int c = 0; c <= 6; ++c) {
+        const int bd = 1 << a, bh = 1 << b, bw = 1 << c;
+        if (bd * bh * bw > maxvol || bd * bh * bw < minvol) continue;
+        if ((bd + 2) * (bh + 2) * (bw + 2) > maxhalo) continue;
+        if (bw < minw && bw < W) continue;
+        if (bd > 2 * D && bd > 1) continue;
+        if (bh > 2 * H && bh > 1) continue;
+        if (bw > 2 * W && bw > 1) continue;
+        const double padded = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh * cdiv(W, bw) * bw;
+        const double halo = (double)cdiv(D, bd) * cdiv(H, bh) * cdiv(W, bw) * (bd + 2) * (bh + 2) * (bw + 2);
+        const double cost = padded + 0.15 * halo;
+        if (cost < best_cost - 1e-9) { best_cost = cost; best = Box{a, b, c}; }
+      }
+  return best;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Returns the m-block count (workgroups along M) the fwd launch will use for a grid;
+// callers size the BatchNorm partial buffer [mblocks][Cout][2] from it.
+int pcms_conv3_mblocks(int N, int D, int H, int W) {
+  Box b = choose_box(D, H, W, 512, kHaloMax, 4, 32);
+  return N * cdiv(D, 1 << b.lbd) * cdiv(H, 1 << b.lbh) * cdiv(W, 1 << b.lbw);
+}
+
+int pcms_conv3_chunk(int dtype) { return dtype == PCMS_BF16 ? Traits<bf16_t>::CK : Traits<float>::CK; }
+
+int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s) {
+  const int CK = pcms_conv3_chunk(dtype);
+  const int Kdim = flip ? Cout : Cin;
+  const int nchunk = cdiv(Kdim, CK);
+  const long total = (long)nchunk * 27 * (flip ? Cin : Cout) * CK;
+  const int grid = (int)std::min<long>(4096, (total + 255) / 256);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((pack_conv3_kernel<bf16_t, 32>), dim3(grid), dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip, nchunk);
+  else
+    hipLaunchKernelGGL((pack_conv3_kernel<float, 16>), dim3(grid), dim3(256), 0, s, w, (float*)out, Cout, Cin, flip, nchunk);
+  PCMS_CHECK_LAUNCH();
+}
+
+// Forward (or dgrad) 3x3x3 conv. See Conv3Params.  splits > 1: fp32 atomic accumulate
+// into yacc (caller zeroes it; bias/stats/conversion then done by pcms_conv3_split_epilogue).
+int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
+                   const void* wpack, const float* bias, void* y0, void* y1, int cy0,
+                   float* yacc, float* stats, int accumulate,
+                   int N, int D, int H, int W, int Cout, int splits, hipStream_t s) {
+  const int Cin = c0 + c1;
+  const int CK = pcms_conv3_chunk(dtype);
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0 || (c1 > 0 && x1 == nullptr)) return -1;
+  if (y1 == nullptr) cy0 = Cout;
+  if (cy0 % 64 != 0 && cy0 != Cout) return -2;
+  Box b = choose_box(D, H, W, 512, kHaloMax, 4, 32);
+  Conv3Params p;
+  p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1;
+  p.w = wpack; p.bias = bias; p.y0 = y0; p.y1 = y1; p.cy0 = cy0;
+  p.yacc = splits > 1 ? yacc : nullptr;
+  p.stats = stats; p.accumulate = accumulate;
+  p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
+  p.nchunk = cdiv(Cin, CK);
+  if (splits < 1) splits = 1;
+  if (splits > p.nchunk) splits = p.nchunk;
+  p.chunks_per_split = cdiv(p.nchunk, splits);
+  splits = cdiv(p.nchunk, p.chunks_per_split);
+  if (splits > 1 && yacc == nullptr) return -3;
+  p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
+  p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
+  if (splits > 1) p.yacc = yacc;
+  dim3 grid(N * p.nbd * p.nbh * p.nbw, Cout / 64, splits);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(conv3_fwd_kernel<bf16_t>, grid, dim3(kThreads), 0, s, p);
+  else
+    hipLaunchKernelGGL(conv3_fwd_kernel<float>, grid, dim3(kThreads), 0, s, p);
+  PCMS_CHECK_LAUNCH();
+}
+
+// Weight gradient: dw (torch layout [Cout][Cin][27], fp32) += sum_v dy (x) x.
+// dwt: fp32 workspace of 27*Cout*Cin floats (zeroed here).
+int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
+                     float* dw, float* dwt, int N, int D, int H, int W, int Cout, int target_wgs,
+                     hipStream_t s) {
+  const int Cin = c0 + c1;
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0) return -1;
+  const int bv = dtype == PCMS_BF16 ? WTraits<bf16_t>::BV : WTraits<float>::BV;
+  Box b = choose_box(D, H, W, bv, kWHaloMax, 4, 16);
+  WgradParams p;
+  p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1; p.dy = dy; p.dwt = dwt;
+  p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
+  p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
+  p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
+  p.nbox = N * p.nbd * p.nbh * p.nbw;
+  const int tiles = (Cout / 64) * cdiv(Cin, 32);
+  if (target_wgs <= 0) target_wgs = 512;
+  int splits = std::max(1, std::min(p.nbox, cdiv(target_wgs, tiles)));
+  p.boxes_per_split = cdiv(p.nbox, splits);
+  splits = cdiv(p.nbox, p.boxes_per_split);
+  hipError_t e = hipMemsetAsync(dwt, 0, sizeof(float) * 27L * Cout * Cin, s);
+  if (e != hipSuccess) return (int)e;
+  dim3 grid(splits, Cout / 64, cdiv(Cin, 32));
+  size_t lds;
+  if (dtype == PCMS_BF16) {
+    lds = (size_t)WTraits<bf16_t>::NBUF * (WTraits<bf16_t>::BV * WTraits<bf16_t>::DYROW + kWHaloMax * WTraits<bf16_t>::XROW);
+    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(conv3_wgrad_kernel<bf16_t>, grid, dim3(kWThreads), lds, s, p);
+  } else {
+    lds = (size_t)WTraits<float>::NBUF * (WTraits<float>::BV * WTraits<float>::DYROW + kWHaloMax * WTraits<float>::XROW);
+    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(conv3_wgrad_kernel<float>, grid, dim3(kWThreads), lds, s, p);
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const long total = 27L * Cout * Cin;
+  hipLaunchKernelGGL(wgrad_permute_kernel, dim3((int)std::min<long>(4096, (total + 255) / 256)), dim3(256), 0, s,
+                     (const float*)dwt, dw, Cout, Cin);
+  PCMS_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -1,0 +1,294 @@
+// ConvTranspose3d(k=2, s=2) of Up3D (models/unet3d.py:120), NDHWC, gfx950.
+//
+// Every output voxel receives exactly one input voxel through one of the 8 taps, so the
+// three products are plain GEMMs with a scattered/gathered voxel index:
+//   fwd   out[child(v,t), co] = b[co] + sum_ci x[v, ci] * W[ci, co, t]
+//         M = input voxels, N = 8*Cout (t-major), K = Cin        (K-contiguous operands)
+//   dgrad dx[v, ci] = sum_{t, co} dout[child(v,t), co] * W[ci, co, t]
+//         M = input voxels, N = Cin, K = 8*Cout                  (K-contiguous operands)
+//   wgrad dW[ci, t, co] += sum_v x[v, ci] * dout[child(v,t), co]
+//         K = voxels: LDS tiles read with ds_read_b64_tr_b16 (bf16) like conv3_wgrad.
+// child(v, t) = (n, 2d+i+pz, 2h+j+py, 2w+k+px) on the skip-sized grid: the symmetric
+// F.pad of models/unet3d.py:143-151 is folded into the offsets (pz, py, px).
+#include "common.h"
+#include "pcms_hip.h"
+#include <algorithm>
+
+namespace {
+
+__device__ __forceinline__ f32x16_t mfma(s16x8_t a, s16x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16_t mfma(float a, float b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <typename T> struct GT;
+template <> struct GT<bf16_t> { static constexpr int KS = 16; typedef s16x8_t Frag; };
+template <> struct GT<float> { static constexpr int KS = 2; typedef float Frag; };
+
+__device__ __forceinline__ s16x8_t ldfrag(const bf16_t* p, int h) { return *reinterpret_cast<const s16x8_t*>(p + 8 * h); }
+__device__ __forceinline__ float ldfrag(const float* p, int h) { return p[h]; }
+
+struct UpGeom {
+  int N, Din, Hin, Win;     // input grid
+  int Do, Ho, Wo;           // output (skip-sized) grid
+  int pz, py, px;           // pad-lo offsets
+};
+
+__device__ __forceinline__ long child_vox(const UpGeom& g, long m, int t) {
+  const int w = m % g.Win; long r = m / g.Win;
+  const int h = r % g.Hin; r /= g.Hin;
+  const int d = r % g.Din; const int n = r / g.Din;
+  const int od = 2 * d + (t >> 2) + g.pz, oh = 2 * h + ((t >> 1) & 1) + g.py, ow = 2 * w + (t & 1) + g.px;
+  return (((long)n * g.Do + od) * g.Ho + oh) * g.Wo + ow;
+}
+
+// wave tile 32 (M) x 64 (N); workgroup 4 waves stacked along M -> 128 x 64.
+template <typename T>
+__global__ void __launch_bounds__(256) convt_fwd_kernel(const T* x, const T* wt, const float* bias, T* out,
+                                                        UpGeom g, int Cin, int Cout) {
+  typedef typename GT<T>::Frag Frag;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  const long m0 = (long)blockIdx.x * 128 + wave * 32;
+  const int q0 = blockIdx.y * 64;
+  if (m0 >= M) return;
+  const long ma = std::min<long>(m0 + r, M - 1);
+  const T* arow = x + ma * Cin;
+  const T* b0 = wt + (long)(q0 + r) * Cin;
+  const T* b1 = wt + (long)(q0 + 32 + r) * Cin;
+  f32x16_t acc0, acc1;
+  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  for (int k = 0; k < Cin; k += GT<T>::KS) {
+    Frag a = ldfrag(arow + k, h);
+    acc0 = mfma(a, ldfrag(b0 + k, h), acc0);
+    acc1 = mfma(a, ldfrag(b1 + k, h), acc1);
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = q0 + j * 32 + r;
+      const int t = q / Cout, co = q % Cout;
+      const float v = (j ? acc1[e] : acc0[e]) + bias[co];
+      Elem<T>::st(out + child_vox(g, m, t) * Cout + co, v);
+    }
+  }
+}
+
+// dx[m, ci] = sum_{t,co} dout[child(m,t), co] * Wd[ci][t][co]
+template <typename T>
+__global__ void __launch_bounds__(256) convt_dgrad_kernel(const T* dout, const T* wd, T* dx, UpGeom g,
+                                                          int Cin, int Cout) {
+  typedef typename GT<T>::Frag Frag;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  const long m0 = (long)blockIdx.x * 128 + wave * 32;
+  const int q0 = blockIdx.y * 64;
+  if (m0 >= M) return;
+  const long ma = std::min<long>(m0 + r, M - 1);
+  const int K = 8 * Cout;
+  const T* b0 = wd + (long)(q0 + r) * K;
+  const T* b1 = wd + (long)(q0 + 32 + r) * K;
+  f32x16_t acc0, acc1;
+  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  for (int t = 0; t < 8; ++t) {
+    const T* arow = dout + child_vox(g, ma, t) * Cout;
+    for (int k = 0; k < Cout; k += GT<T>::KS) {
+      Frag a = ldfrag(arow + k, h);
+      acc0 = mfma(a, ldfrag(b0 + t * Cout + k, h), acc0);
+      acc1 = mfma(a, ldfrag(b1 + t * Cout + k, h), acc1);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (m >= M) continue;
+    Elem<T>::st(dx + m * Cin + q0 + r, acc0[e]);
+    Elem<T>::st(dx + m * Cin + q0 + 32 + r, acc1[e]);
+  }
+}
+
+// ---- weight gradient: C[p = ci][q = (t, co)] over K = input voxels ----
+constexpr int kVB = 64;  // voxels per staged block
+
+__device__ __forceinline__ int half_swz(int v, int c) {  // 128-B rows (64 bf16), c element
+  return v * 128 + (((c >> 5) ^ ((v >> 1) & 1)) * 64) + (c & 31) * 2;
+}
+__device__ __forceinline__ s16x4_t tr_read(const char* lds, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + off));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) convt_wgrad_kernel(const T* x, const T* dout, float* ws, UpGeom g,
+                                                          int Cin, int Cout, int vox_per_split) {
+  constexpr int ROW = 64 * (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) char lds[2 * kVB * ROW];
+  char* P = lds;
+  char* Q = lds + kVB * ROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int wp = wave & 1, wq = wave >> 1;
+  const int p0 = blockIdx.z * 64;     // ci tile
+  const int qt = blockIdx.y;          // (t, co) tile: q = t*Cout + co
+  const int t = (qt * 64) / Cout, co0 = (qt * 64) % Cout;
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  const long vbeg = (long)blockIdx.x * vox_per_split;
+  const long vend = std::min<long>(M, vbeg + vox_per_split);
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int PPR = 64 / VEC;       // pieces per row
+  f32x16_t acc;
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  for (long vb = vbeg; vb < vend; vb += kVB) {
+    __syncthreads();
+    for (int pc = tid; pc < 2 * kVB * PPR; pc += 256) {
+      const int which = pc / (kVB * PPR), rem = pc % (kVB * PPR);
+      const int v = rem / PPR, q = rem % PPR;
+      const long m = vb + v;
+      u32x4_t val = {0u, 0u, 0u, 0u};
+      if (m < vend) {
+        const T* src = which == 0 ? x + m * Cin + p0 + q * VEC : dout + child_vox(g, m, t) * Cout + co0 + q * VEC;
+        val = *reinterpret_cast<const u32x4_t*>(src);
+      }
+      char* base = which == 0 ? P : Q;
+      const int off = sizeof(T) == 2 ? half_swz(v, q * VEC) : v * ROW + q * 16;
+      *reinterpret_cast<u32x4_t*>(base + off) = val;
+    }
+    __syncthreads();
+    if constexpr (sizeof(T) == 2) {
+      const int gg = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+      for (int k0 = 0; k0 < kVB; k0 += 16) {
+        const int v = k0 + 8 * h + qq;
+        const int ca = wp * 32 + gg * 16 + pp * 4, cb = wq * 32 + gg * 16 + pp * 4;
+        s16x4_t a0 = tr_read(P, half_swz(v, ca)), a1 = tr_read(P, half_swz(v + 4, ca));
+        s16x4_t b0 = tr_read(Q, half_swz(v, cb)), b1 = tr_read(Q, half_swz(v + 4, cb));
+        s16x8_t a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        s16x8_t b = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        acc = mfma(a, b, acc);
+      }
+    } else {
+      for (int k0 = 0; k0 < kVB; k0 += 2) {
+        const int v = k0 + h;
+        float a = *reinterpret_cast<const float*>(P + v * ROW + (wp * 32 + (lane & 31)) * 4);
+        float b = *reinterpret_cast<const float*>(Q + v * ROW + (wq * 32 + (lane & 31)) * 4);
+        acc = mfma(a, b, acc);
+      }
+    }
+  }
+  // C[row = ci][col = co]; ws layout [Cin][8][Cout]
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int ci = p0 + wp * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const int co = co0 + wq * 32 + (lane & 31);
+    atomicAdd(ws + ((long)ci * 8 + t) * Cout + co, acc[e]);
+  }
+}
+
+// ws [Cin][8][Cout] -> dw [Cin][Cout][8] (+=), torch ConvTranspose3d layout
+__global__ void convt_wgrad_permute(const float* ws, float* dw, int Cin, int Cout) {
+  const long total = (long)Cin * Cout * 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int t = i & 7;
+    const long r = i >> 3;
+    const int co = r % Cout, ci = r / Cout;
+    dw[i] += ws[((long)ci * 8 + t) * Cout + co];
+  }
+}
+
+// master W[Cin][Cout][8] fp32 ->  fwd pack [8][Cout][Cin]  /  dgrad pack [Cin][8][Cout]
+template <typename T>
+__global__ void convt_pack_kernel(const float* w, T* out, int Cin, int Cout, int dgrad) {
+  const long total = (long)Cin * Cout * 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int t, co, ci;
+    if (!dgrad) { ci = i % Cin; long r = i / Cin; co = r % Cout; t = r / Cout; }
+    else { co = i % Cout; long r = i / Cout; t = r % 8; ci = r / 8; }
+    out[i] = Elem<T>::cvt(w[((long)ci * Cout + co) * 8 + t]);
+  }
+}
+
+UpGeom make_geom(int N, int Din, int Hin, int Win, int Do, int Ho, int Wo) {
+  UpGeom g;
+  g.N = N; g.Din = Din; g.Hin = Hin; g.Win = Win; g.Do = Do; g.Ho = Ho; g.Wo = Wo;
+  g.pz = (Do - 2 * Din) / 2; g.py = (Ho - 2 * Hin) / 2; g.px = (Wo - 2 * Win) / 2;
+  return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pcms_convt_pack(int dtype, const float* w, void* out, int Cin, int Cout, int dgrad, hipStream_t s) {
+  const long total = (long)Cin * Cout * 8;
+  const int grid = (int)std::min<long>(4096, (total + 255) / 256);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(convt_pack_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, w, (bf16_t*)out, Cin, Cout, dgrad);
+  else
+    hipLaunchKernelGGL(convt_pack_kernel<float>, dim3(grid), dim3(256), 0, s, w, (float*)out, Cin, Cout, dgrad);
+  PCMS_CHECK_LAUNCH();
+}
+
+// out: skip-sized (N, Do, Ho, Wo, Cout). If the grid is larger than 2x the input the pad
+// ring is zero-filled here (F.pad semantics).
+int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bias, void* out,
+                   int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
+  if (Cin % 16 || Cout % 64) return -1;
+  UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
+  const size_t es = dtype == PCMS_BF16 ? 2 : 4;
+  if (Do != 2 * Din || Ho != 2 * Hin || Wo != 2 * Win) {
+    hipError_t e = hipMemsetAsync(out, 0, es * N * (size_t)Do * Ho * Wo * Cout, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  const long M = (long)N * Din * Hin * Win;
+  dim3 grid(cdiv(M, 128), 8 * Cout / 64);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(convt_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
+  else
+    hipLaunchKernelGGL(convt_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (const float*)wpack, bias, (float*)out, g, Cin, Cout);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
+                     int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
+  if (Cin % 64 || Cout % 16) return -1;
+  UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
+  const long M = (long)N * Din * Hin * Win;
+  dim3 grid(cdiv(M, 128), Cin / 64);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(convt_dgrad_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, (const bf16_t*)wpack_d, (bf16_t*)dx, g, Cin, Cout);
+  else
+    hipLaunchKernelGGL(convt_dgrad_kernel<float>, grid, dim3(256), 0, s, (const float*)dout, (const float*)wpack_d, (float*)dx, g, Cin, Cout);
+  PCMS_CHECK_LAUNCH();
+}
+
+// dw (torch layout [Cin][Cout][2][2][2], fp32) += ...; ws: Cin*8*Cout floats (zeroed here)
+int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
+                     int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
+                     int target_wgs, hipStream_t s) {
+  if (Cin % 64 || Cout % 64) return -1;
+  UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
+  const long M = (long)N * Din * Hin * Win;
+  hipError_t e = hipMemsetAsync(ws, 0, sizeof(float) * 8L * Cin * Cout, s);
+  if (e != hipSuccess) return (int)e;
+  const int tiles = (8 * Cout / 64) * (Cin / 64);
+  if (target_wgs <= 0) target_wgs = 1024;
+  const long nvb = (M + kVB - 1) / kVB;
+  int splits = (int)std::max<long>(1, std::min<long>(nvb, cdiv(target_wgs, tiles)));
+  const int vps = (int)(cdiv(nvb, splits) * kVB);
+  splits = (int)((M + vps - 1) / vps);
+  dim3 grid(splits, 8 * Cout / 64, Cin / 64);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(convt_wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g, Cin, Cout, vps);
+  else
+    hipLaunchKernelGGL(convt_wgrad_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (const float*)dout, ws, g, Cin, Cout, vps);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const long total = 8L * Cin * Cout;
+  hipLaunchKernelGGL(convt_wgrad_permute, dim3((int)std::min<long>(4096, (total + 255) / 256)), dim3(256), 0, s, (const float*)ws, dw, Cin, Cout);
+  PCMS_CHECK_LAUNCH();
+}
+
+}  // extern "C"

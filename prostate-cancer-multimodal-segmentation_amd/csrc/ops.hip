@@ -1,0 +1,635 @@
+// Bandwidth-bound kernels of the U-Net step (NDHWC, gfx950): input layout pack,
+// BatchNorm3d (train/eval) + ReLU forward/backward, MaxPool3d(2) forward/backward,
+// the 1x1x1 output conv, DiceLoss / BCEDiceLoss forward/backward, flat Adam.
+//
+// Reference ops replaced (paths relative to the reference repo):
+//   BatchNorm3d + ReLU(inplace)   models/unet3d.py:31-39
+//   MaxPool3d(2)                  models/unet3d.py:80
+//   outc Conv3d(64, ncls, 1)      models/unet3d.py:222
+//   DiceLoss / BCEDiceLoss        utils/losses.py:44-92, 124-152
+//   optim.Adam(wd=1e-5, coupled)  utils/trainer.py:113-117
+// Every per-channel statistic is a two-level reduction: fp32 per-block partials written
+// to a [rows][C][2] buffer, combined in fp64 in a fixed order (run-to-run reproducible).
+#include "common.h"
+#include "pcms_hip.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int TPB = 256;
+
+inline int grid_for(long work, int per_block, int cap = 8192) {
+  return (int)std::max<long>(1, std::min<long>(cap, (work + per_block - 1) / per_block));
+}
+
+// ---------------- input: NCDHW fp32 (N, Cin, V) -> NDHWC T (N, V, Cp) ----------------
+template <typename T>
+__global__ void pack_input_kernel(const float* in, T* out, int N, int Cin, long V, int Cp) {
+  const long total = (long)N * V;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / V, v = i % V;
+    for (int c = 0; c < Cp; ++c) {
+      const float x = c < Cin ? in[(n * Cin + c) * V + v] : 0.f;
+      Elem<T>::st(out + i * Cp + c, x);
+    }
+  }
+}
+
+// ---------------- BatchNorm statistics ----------------
+// partial rows -> mean/invstd/scale/shift (+ running stats when training)
+// block: 1024 threads = 16 row-groups x 64 channels
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(
+    const float* part, int rows, int C, double count, const float* gamma, const float* beta,
+    float* rmean, float* rvar, long long* nbt, float momentum, float eps,
+    float* scale, float* shift, float* mean_out, float* invstd_out) {
+  __shared__ double red[16][64][2];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (int r = rg; r < rows; r += 16) {
+      s1 += (double)part[((long)r * C + c) * 2];
+      s2 += (double)part[((long)r * C + c) * 2 + 1];
+    }
+  red[rg][cl][0] = s1;
+  red[rg][cl][1] = s2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int g = 1; g < 16; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
+    const double mean = s1 / count;
+    double var = s2 / count - mean * mean;
+    if (var < 0) var = 0;
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    const float sc = (float)((double)gamma[c] * inv);
+    scale[c] = sc;
+    shift[c] = (float)((double)beta[c] - mean * (double)gamma[c] * inv);
+    mean_out[c] = (float)mean;
+    invstd_out[c] = (float)inv;
+    if (rmean) {
+      const double unb = count > 1 ? var * count / (count - 1) : var;
+      rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+    }
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+__global__ void bn_eval_coeffs_kernel(const float* gamma, const float* beta, const float* rmean,
+                                      const float* rvar, float eps, int C, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double inv = 1.0 / sqrt((double)rvar[c] + (double)eps);
+  scale[c] = (float)((double)gamma[c] * inv);
+  shift[c] = (float)((double)beta[c] - (double)rmean[c] * (double)gamma[c] * inv);
+}
+
+// a = relu(y * scale[c] + shift[c]); 16-byte vectors
+template <typename T>
+__global__ void bn_relu_kernel(const T* y, T* a, const float* scale, const float* shift, int C, long nvec) {
+  constexpr int VEC = Elem<T>::kVec;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * VEC) % C);
+    float v[VEC];
+    load16<T>(y + i * VEC, v);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) v[j] = fmaxf(v[j] * scale[c0 + j] + shift[c0 + j], 0.f);
+    store16<T>(a + i * VEC, v);
+  }
+}
+
+// BN+ReLU backward, pass 1: per-block partial sums of g and g*xhat, g = da * [a > 0].
+// Block: 256 threads = (256 / C8) voxel lanes x C8 channel groups of VEC channels.
+template <typename T>
+__global__ void __launch_bounds__(TPB) bn_relu_bwd_reduce_kernel(
+    const T* da, const T* y, const float* scale, const float* shift, const float* mean,
+    const float* invstd, float* part, int C, long nvox) {
+  constexpr int VEC = Elem<T>::kVec;
+  __shared__ float red[TPB * VEC * 2];
+  const int CG = C / VEC;
+  const int cg = threadIdx.x % CG, vl = threadIdx.x / CG, VL = TPB / CG;
+  const int c0 = cg * VEC;
+  float sc[VEC], sh[VEC], mu[VEC], is[VEC], sg[VEC], sgx[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j];
+    sg[j] = 0.f; sgx[j] = 0.f;
+  }
+  for (long v = (long)blockIdx.x * VL + vl; v < nvox; v += (long)gridDim.x * VL) {
+    float dv[VEC], yv[VEC];
+    load16<T>(da + v * C + c0, dv);
+    load16<T>(y + v * C + c0, yv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float g = (yv[j] * sc[j] + sh[j] > 0.f) ? dv[j] : 0.f;
+      sg[j] += g;
+      sgx[j] += g * ((yv[j] - mu[j]) * is[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    red[(vl * C + c0 + j) * 2] = sg[j];
+    red[(vl * C + c0 + j) * 2 + 1] = sgx[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += TPB) {
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < VL; ++l) { a += red[(l * C + c) * 2]; b += red[(l * C + c) * 2 + 1]; }
+    part[((long)blockIdx.x * C + c) * 2] = a;
+    part[((long)blockIdx.x * C + c) * 2 + 1] = b;
+  }
+}
+
+// pass 2: reduce partials; dgamma/dbeta (+=) and the apply coefficients
+//   dy = k1*g + k2*xhat + k3, k1 = gamma*invstd, k2 = -k1*sum(g xhat)/M, k3 = -k1*sum(g)/M
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(
+    const float* part, int rows, int C, double count, const float* gamma, const float* invstd,
+    float* dgamma, float* dbeta, float* coef) {
+  __shared__ double red[16][64][2];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (int r = rg; r < rows; r += 16) {
+      s1 += (double)part[((long)r * C + c) * 2];
+      s2 += (double)part[((long)r * C + c) * 2 + 1];
+    }
+  red[rg][cl][0] = s1;
+  red[rg][cl][1] = s2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int g = 1; g < 16; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
+    dbeta[c] += (float)s1;
+    dgamma[c] += (float)s2;
+    const double k1 = (double)gamma[c] * (double)invstd[c];
+    coef[c * 3 + 0] = (float)k1;
+    coef[c * 3 + 1] = (float)(-k1 * s2 / count);
+    coef[c * 3 + 2] = (float)(-k1 * s1 / count);
+  }
+}
+
+template <typename T>
+__global__ void bn_relu_bwd_apply_kernel(const T* da, const T* y, const float* scale, const float* shift,
+                                         const float* mean, const float* invstd, const float* coef,
+                                         T* dy, int C, long nvec) {
+  constexpr int VEC = Elem<T>::kVec;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * VEC) % C);
+    float dv[VEC], yv[VEC], o[VEC];
+    load16<T>(da + i * VEC, dv);
+    load16<T>(y + i * VEC, yv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const int c = c0 + j;
+      const float g = (yv[j] * scale[c] + shift[c] > 0.f) ? dv[j] : 0.f;
+      const float xh = (yv[j] - mean[c]) * invstd[c];
+      o[j] = coef[c * 3] * g + coef[c * 3 + 1] * xh + coef[c * 3 + 2];
+    }
+    store16<T>(dy + i * VEC, o);
+  }
+}
+
+// ---------------- MaxPool3d(2), floor mode; first max wins (PyTorch scan order) -------
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* a, T* p, int N, int D, int H, int W, int C) {
+  constexpr int VEC = Elem<T>::kVec;
+  const int Do = D / 2, Ho = H / 2, Wo = W / 2, CV = C / VEC;
+  const long total = (long)N * Do * Ho * Wo * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cv = i % CV; long r = i / CV;
+    const int wo = r % Wo; r /= Wo;
+    const int ho = r % Ho; r /= Ho;
+    const int d_o = r % Do; const long n = r / Do;
+    float m[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) m[j] = -INFINITY;
+    for (int k = 0; k < 8; ++k) {
+      const long vin = ((n * D + 2 * d_o + (k >> 2)) * H + 2 * ho + ((k >> 1) & 1)) * W + 2 * wo + (k & 1);
+      float v[VEC];
+      load16<T>(a + vin * C + cv * VEC, v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (v[j] > m[j] || v[j] != v[j]) m[j] = v[j];
+    }
+    store16<T>(p + i * VEC, m);
+  }
+}
+
+// da[argmax] += dp (da already holds the skip-path gradient)
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* a, const T* dp, T* da, int N, int D, int H, int W, int C) {
+  constexpr int VEC = Elem<T>::kVec;
+  const int Do = D / 2, Ho = H / 2, Wo = W / 2, CV = C / VEC;
+  const long total = (long)N * Do * Ho * Wo * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cv = i % CV; long r = i / CV;
+    const int wo = r % Wo; r /= Wo;
+    const int ho = r % Ho; r /= Ho;
+    const int d_o = r % Do; const long n = r / Do;
+    float m[VEC];
+    int arg[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; arg[j] = 0; }
+    long vin[8];
+    for (int k = 0; k < 8; ++k) {
+      vin[k] = ((n * D + 2 * d_o + (k >> 2)) * H + 2 * ho + ((k >> 1) & 1)) * W + 2 * wo + (k & 1);
+      float v[VEC];
+      load16<T>(a + vin[k] * C + cv * VEC, v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (v[j] > m[j] || (v[j] != v[j] && m[j] == m[j])) { m[j] = v[j]; arg[j] = k; }
+    }
+    float g[VEC];
+    load16<T>(dp + i * VEC, g);
+    for (int k = 0; k < 8; ++k) {
+      float o[VEC];
+      load16<T>(da + vin[k] * C + cv * VEC, o);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] += (arg[j] == k) ? g[j] : 0.f;
+      store16<T>(da + vin[k] * C + cv * VEC, o);
+    }
+  }
+}
+
+// ---------------- sum over a sub-box of an NDHWC tensor (ConvT bias grad) ----------
+template <typename T>
+__global__ void box_channel_sum_kernel(const T* x, float* out, int N, int D, int H, int W, int C,
+                                       int z0, int y0, int x0, int bd, int bh, int bw) {
+  // one voxel per block iteration, threads over channels (loop for C > 256)
+  const long nv = (long)N * bd * bh * bw;
+  for (int cb = 0; cb < C; cb += TPB) {
+    const int c = cb + threadIdx.x;
+    float s = 0.f;
+    if (c < C)
+      for (long i = blockIdx.x; i < nv; i += gridDim.x) {
+        const int w = i % bw; long r = i / bw;
+        const int h = r % bh; r /= bh;
+        const int d = r % bd; const long n = r / bd;
+        s += Elem<T>::ld(x + (((n * D + z0 + d) * H + y0 + h) * W + x0 + w) * C + c);
+      }
+    if (c < C) atomicAdd(out + c, s);
+  }
+}
+
+// ---------------- output head: logits (NCDHW fp32) = b + a . w ----------------
+// 8 lanes per voxel, 8 channels each (Cin = 64)
+template <typename T>
+__global__ void head_fwd_kernel(const T* a, const float* w, const float* b, float* logits,
+                                long nvox_per_n, int N, int ncls) {
+  const long total = (long)N * nvox_per_n;
+  const int sub = threadIdx.x & 7;
+  for (long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3; v < total;
+       v += ((long)gridDim.x * blockDim.x) >> 3) {
+    float x[8];
+    if constexpr (sizeof(T) == 2) {
+      load16<T>(a + v * 64 + sub * 8, x);
+    } else {
+      load16<T>(a + v * 64 + sub * 8, x);
+      load16<T>(a + v * 64 + sub * 8 + 4, x + 4);
+    }
+    const long n = v / nvox_per_n, vv = v % nvox_per_n;
+    for (int k = 0; k < ncls; ++k) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += x[j] * w[k * 64 + sub * 8 + j];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      if (sub == 0) logits[(n * ncls + k) * nvox_per_n + vv] = s + b[k];
+    }
+  }
+}
+
+// da[v, c] = sum_k dl[k, v] w[k, c]  (written);  dw[k, c] += sum_v dl a;  db[k] += sum_v dl
+template <typename T>
+__global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* dlogits, const float* w,
+                                                       T* da, float* dw, float* db, long nvox_per_n,
+                                                       int N, int ncls) {
+  __shared__ float red[TPB / 64][4][65];
+  const long total = (long)N * nvox_per_n;
+  const int sub = threadIdx.x & 7, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float accw[4][8], accb[4];
+  for (int k = 0; k < 4; ++k) { accb[k] = 0.f; for (int j = 0; j < 8; ++j) accw[k][j] = 0.f; }
+  for (long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3; v < total;
+       v += ((long)gridDim.x * blockDim.x) >> 3) {
+    float x[8], o[8];
+    load16<T>(a + v * 64 + sub * 8, x);
+    if constexpr (sizeof(T) == 4) load16<T>(a + v * 64 + sub * 8 + 4, x + 4);
+    const long n = v / nvox_per_n, vv = v % nvox_per_n;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = 0.f;
+    for (int k = 0; k < ncls && k < 4; ++k) {
+      const float g = dlogits[(n * ncls + k) * nvox_per_n + vv];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] += g * w[k * 64 + sub * 8 + j];
+        accw[k][j] += g * x[j];
+      }
+      if (sub == 0) accb[k] += g;
+    }
+    store16<T>(da + v * 64 + sub * 8, o);
+    if constexpr (sizeof(T) == 4) store16<T>(da + v * 64 + sub * 8 + 4, o + 4);
+  }
+  // reduce accw over the 8 voxel-lanes of each wave that share `sub`
+  for (int k = 0; k < ncls && k < 4; ++k) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = accw[k][j];
+      s += __shfl_xor(s, 8, 64);
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 8) red[wave][k][sub * 8 + j] = s;
+    }
+    float sb = wave_sum(accb[k]);
+    if (lane == 0) red[wave][k][64] = sb;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < ncls * 65 && idx < 4 * 65; idx += TPB) {
+    const int k = idx / 65, c = idx % 65;
+    float s = 0.f;
+    for (int wv = 0; wv < TPB / 64; ++wv) s += red[wv][k][c];
+    if (c < 64) atomicAdd(dw + k * 64 + c, s);
+    else atomicAdd(db + k, s);
+  }
+}
+
+// ---------------- losses ----------------
+// partial rows: [block][4] = (sum p*t, sum p, sum t, sum bce)
+__global__ void __launch_bounds__(TPB) loss_partial_kernel(const float* x, const float* t, long M, float* part) {
+  __shared__ float red[4][TPB / 64];
+  float a = 0.f, b = 0.f, c = 0.f, d = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < M; i += (long)gridDim.x * blockDim.x) {
+    const float xv = x[i], tv = t[i];
+    const float p = 1.f / (1.f + expf(-xv));
+    a += p * tv; b += p; c += tv;
+    d += fmaxf(xv, 0.f) - xv * tv + log1pf(expf(-fabsf(xv)));
+  }
+  a = wave_sum(a); b = wave_sum(b); c = wave_sum(c); d = wave_sum(d);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wave] = a; red[1][wave] = b; red[2][wave] = c; red[3][wave] = d; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float s = 0.f;
+    for (int w = 0; w < TPB / 64; ++w) s += red[threadIdx.x][w];
+    part[blockIdx.x * 4 + threadIdx.x] = s;
+  }
+}
+
+// sums[0..3] (double) from partials; loss = wb*bce/M + wd*(1 - dice)
+__global__ void loss_finalize_kernel(const float* part, int rows, long M, float smooth, float wb, float wd,
+                                     double* sums, float* loss) {
+  __shared__ double red[4][64];
+  const int t = threadIdx.x;  // 256 threads: 4 sums x 64 lanes
+  const int k = t >> 6, l = t & 63;
+  double s = 0.0;
+  for (int r = l; r < rows; r += 64) s += (double)part[r * 4 + k];
+  red[k][l] = s;
+  __syncthreads();
+  if (t < 4) {
+    double acc = 0.0;
+    for (int i = 0; i < 64; ++i) acc += red[t][i];
+    sums[t] = acc;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const double I = sums[0], P = sums[1], Tt = sums[2], B = sums[3];
+    const double dice = (2.0 * I + smooth) / (P + Tt + smooth);
+    loss[0] = (float)(wb * (B / (double)M) + wd * (1.0 - dice));
+  }
+}
+
+// dL/dx_i = gout * (wb*(p - t)/M + wd * -(2 t (P+T+s) - (2I+s)) / (P+T+s)^2 * p(1-p))
+__global__ void loss_bwd_kernel(const float* x, const float* t, long M, const double* sums, float smooth,
+                                float wb, float wd, const float* gout, float* dx) {
+  const double I = sums[0], P = sums[1], Tt = sums[2];
+  const double den = P + Tt + smooth, num = 2.0 * I + smooth;
+  const float inv_den2 = (float)(1.0 / (den * den));
+  const float fden = (float)den, fnum = (float)num;
+  const float g = gout ? gout[0] : 1.f;
+  const float invM = (float)(1.0 / (double)M);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < M; i += (long)gridDim.x * blockDim.x) {
+    const float xv = x[i], tv = t[i];
+    const float p = 1.f / (1.f + expf(-xv));
+    const float ddice_dp = -(2.f * tv * fden - fnum) * inv_den2;
+    dx[i] = g * (wb * (p - tv) * invM + wd * ddice_dp * p * (1.f - p));
+  }
+}
+
+// ---------------- Adam (torch.optim.Adam, foreach, coupled weight decay) ----------
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n, float step_size, float b1,
+                            float b2, float eps, float wd, float bc2_sqrt, float gscale) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    if (gscale != 1.f) gi *= gscale;   // data-parallel mean of summed gradients
+    const float pi = p[i];
+    if (wd != 0.f) gi = gi + wd * pi;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);               // exp_avg.lerp_(grad, 1 - beta1)
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;    // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - step_size * (mi / denom);
+  }
+}
+
+// fp32 split-K accumulator -> + bias, store T, BN partial sums; 64 voxels per block row
+template <typename T>
+__global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, const float* bias, T* y0, T* y1,
+                                                             int cy0, float* stats, int C, long nvox) {
+  __shared__ float red[TPB / 64][64][2];
+  const int cl = threadIdx.x & 63, vl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const long v0 = (long)blockIdx.x * 64;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = vl; k < 64; k += TPB / 64) {
+    const long v = v0 + k;
+    if (v >= nvox) break;
+    float x = acc[v * C + c] + (bias ? bias[c] : 0.f);
+    T* dst = c < cy0 ? y0 + v * cy0 + c : y1 + v * (C - cy0) + (c - cy0);
+    Elem<T>::st(dst, x);
+    s1 += x; s2 += x * x;
+  }
+  red[vl][cl][0] = s1;
+  red[vl][cl][1] = s2;
+  __syncthreads();
+  if (vl == 0 && stats) {
+    for (int k = 1; k < TPB / 64; ++k) { s1 += red[k][cl][0]; s2 += red[k][cl][1]; }
+    stats[((long)blockIdx.x * C + c) * 2] = s1;
+    stats[((long)blockIdx.x * C + c) * 2 + 1] = s2;
+  }
+}
+
+template <typename T>
+__global__ void add_kernel(T* dst, const T* src, long nvec) {
+  constexpr int VEC = Elem<T>::kVec;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    float a[VEC], b[VEC];
+    load16<T>(dst + i * VEC, a);
+    load16<T>(src + i * VEC, b);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) a[j] += b[j];
+    store16<T>(dst + i * VEC, a);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long V, int Cp, hipStream_t s) {
+  const int grid = grid_for((long)N * V, TPB);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(pack_input_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, in, (bf16_t*)out, N, Cin, V, Cp);
+  else hipLaunchKernelGGL(pack_input_kernel<float>, dim3(grid), dim3(TPB), 0, s, in, (float*)out, N, Cin, V, Cp);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_bn_finalize(const float* part, int rows, int C, double count, const float* gamma, const float* beta,
+                     float* rmean, float* rvar, long long* nbt, float momentum, float eps,
+                     float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, s, part, rows, C, count, gamma, beta,
+                     rmean, rvar, nbt, momentum, eps, scale, shift, mean, invstd);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                        int C, float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, gamma, beta, rmean, rvar, eps, C, scale, shift);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const float* shift, int C, long nvox,
+                 hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC) return -1;
+  const long nvec = nvox * C / VEC;
+  const int grid = grid_for(nvec, TPB);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(bn_relu_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, (bf16_t*)a, scale, shift, C, nvec);
+  else hipLaunchKernelGGL(bn_relu_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)y, (float*)a, scale, shift, C, nvec);
+  PCMS_CHECK_LAUNCH();
+}
+
+// number of partial rows pcms_bn_relu_bwd_reduce writes (caller sizes `part`)
+int pcms_bn_bwd_rows(int dtype, int C, long nvox) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  const int VL = TPB / (C / VEC);
+  return grid_for(nvox, VL * 16, 2048);
+}
+
+int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scale, const float* shift,
+                     const float* mean, const float* invstd, const float* gamma, float* part, float* coef,
+                     float* dgamma, float* dbeta, void* dy, int C, long nvox, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC || (TPB % (C / VEC)) != 0) return -1;
+  const int rows = pcms_bn_bwd_rows(dtype, C, nvox);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<bf16_t>, dim3(rows), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, part, C, nvox);
+  else
+    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<float>, dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, s, (const float*)part, rows, C,
+                     (double)nvox, gamma, invstd, dgamma, dbeta, coef);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const long nvec = nvox * C / VEC;
+  const int grid = grid_for(nvec, TPB);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, (const float*)coef, (bf16_t*)dy, C, nvec);
+  else
+    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, (const float*)coef, (float*)dy, C, nvec);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_maxpool_fwd(int dtype, const void* a, void* p, int N, int D, int H, int W, int C, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  const long total = (long)N * (D / 2) * (H / 2) * (W / 2) * (C / VEC);
+  const int grid = grid_for(total, TPB);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, (bf16_t*)p, N, D, H, W, C);
+  else hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, (float*)p, N, D, H, W, C);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_maxpool_bwd(int dtype, const void* a, const void* dp, void* da, int N, int D, int H, int W, int C,
+                     hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  const long total = (long)N * (D / 2) * (H / 2) * (W / 2) * (C / VEC);
+  const int grid = grid_for(total, TPB);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, (const bf16_t*)dp, (bf16_t*)da, N, D, H, W, C);
+  else hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, (const float*)dp, (float*)da, N, D, H, W, C);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_box_channel_sum(int dtype, const void* x, float* out, int N, int D, int H, int W, int C,
+                         int z0, int y0, int x0, int bd, int bh, int bw, hipStream_t s) {
+  const long nv = (long)N * bd * bh * bw;
+  const int grid = (int)std::min<long>(nv, 1024);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(box_channel_sum_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)x, out, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
+  else hipLaunchKernelGGL(box_channel_sum_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)x, out, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* logits, long nvox_per_n, int N,
+                  int ncls, hipStream_t s) {
+  const int grid = grid_for((long)N * nvox_per_n * 8, TPB);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, w, b, logits, nvox_per_n, N, ncls);
+  else hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, w, b, logits, nvox_per_n, N, ncls);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w, void* da, float* dw, float* db,
+                  long nvox_per_n, int N, int ncls, hipStream_t s) {
+  if (ncls > 4) return -1;
+  const int grid = grid_for((long)N * nvox_per_n * 8, TPB, 2048);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, dw, db, nvox_per_n, N, ncls);
+  else hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, dlogits, w, (float*)da, dw, db, nvox_per_n, N, ncls);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_loss_rows(long M) { return grid_for(M, TPB * 8, 1024); }
+
+// loss (device fp32 scalar) and sums (device fp64[4]); part: rows*4 floats
+int pcms_loss_fwd(const float* x, const float* t, long M, float smooth, float wb, float wd, float* part,
+                  double* sums, float* loss, hipStream_t s) {
+  const int rows = pcms_loss_rows(M);
+  hipLaunchKernelGGL(loss_partial_kernel, dim3(rows), dim3(TPB), 0, s, x, t, M, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, (const float*)part, rows, M, smooth, wb, wd, sums, loss);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_loss_bwd(const float* x, const float* t, long M, const double* sums, float smooth, float wb, float wd,
+                  const float* gout, float* dx, hipStream_t s) {
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(grid_for(M, TPB)), dim3(TPB), 0, s, x, t, M, sums, smooth, wb, wd, gout, dx);
+  PCMS_CHECK_LAUNCH();
+}
+
+// step_size = lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)  (host fp64 -> fp32)
+int pcms_adam(float* p, const float* g, float* m, float* v, long n, float step_size, float b1, float b2, float eps,
+              float wd, float bc2_sqrt, float gscale, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, TPB, 16384)), dim3(TPB), 0, s, p, g, m, v, n, step_size, b1, b2, eps, wd, bc2_sqrt, gscale);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_split_epilogue_rows(long nvox) { return cdiv(nvox, 64); }
+
+int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0, float* stats,
+                        int C, long nvox, hipStream_t s) {
+  if (C % 64) return -1;
+  if (y1 == nullptr) cy0 = C;
+  dim3 grid(cdiv(nvox, 64), C / 64);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(TPB), 0, s, acc, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox);
+  else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(TPB), 0, s, acc, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_add(int dtype, void* dst, const void* src, long n, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (n % VEC) return -1;
+  const long nvec = n / VEC;
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(add_kernel<bf16_t>, dim3(grid_for(nvec, TPB)), dim3(TPB), 0, s, (bf16_t*)dst, (const bf16_t*)src, nvec);
+  else hipLaunchKernelGGL(add_kernel<float>, dim3(grid_for(nvec, TPB)), dim3(TPB), 0, s, (float*)dst, (const float*)src, nvec);
+  PCMS_CHECK_LAUNCH();
+}
+
+}  // extern "C"

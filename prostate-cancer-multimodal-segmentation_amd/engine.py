@@ -1,0 +1,427 @@
+"""U-Net execution engine: the forward / backward schedule of the reference model over the
+HIP kernels of libpcms_hip.so.
+
+Reference call graph reproduced (models/unet3d.py):
+  inc -> down1..down4 (MaxPool3d(2) + DoubleConv) -> up1..up4 (ConvT + pad + cat[skip, up]
+  + DoubleConv) -> outc                                   forward @247-296
+and its autograd backward (aten convolution_backward / batch_norm_backward / ...).
+
+Layout: activations NDHWC in ``dtype`` (bf16 default, fp32 parity build); parameters live
+in ONE flat fp32 master buffer (the module's nn.Parameters are views into it, so
+``state_dict()`` keys/shapes are the reference's), gradients in one flat fp32 buffer
+(``param.grad`` views), BatchNorm running stats in one flat fp32 buffer.  Kernel weight
+packs (bf16 / fp32, MFMA-friendly order) are rebuilt from the master when it changes.
+
+The engine keeps the activations of the LAST training forward; ``backward`` must follow
+that forward (checked).  Only device code runs: there is no CPU path.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, call, query
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+_DT = {"bf16": (torch.bfloat16, BF16), "fp32": (torch.float32, F32)}
+
+
+class ConvSpec:
+    __slots__ = ("mod", "cin", "cout", "cin_store", "fwd", "dgrad")
+
+    def __init__(self, mod, cin, cout, cin_store):
+        self.mod, self.cin, self.cout, self.cin_store = mod, cin, cout, cin_store
+        self.fwd = None
+        self.dgrad = None
+
+
+class BNSpec:
+    __slots__ = ("mod", "c", "scale", "shift", "mean", "invstd")
+
+    def __init__(self, mod, c):
+        self.mod, self.c = mod, c
+        self.scale = self.shift = self.mean = self.invstd = None
+
+
+class BlockSpec:
+    """DoubleConv3D: conv0 -> bn0 -> relu -> conv1 -> bn1 -> relu (models/unet3d.py:27-40)."""
+
+    def __init__(self, dc, cin_store):
+        seq = dc.conv
+        self.c0 = ConvSpec(seq[0], seq[0].in_channels, seq[0].out_channels, cin_store)
+        self.b0 = BNSpec(seq[1], seq[1].num_features)
+        self.c1 = ConvSpec(seq[3], seq[3].in_channels, seq[3].out_channels, seq[3].in_channels)
+        self.b1 = BNSpec(seq[4], seq[4].num_features)
+        self.cout = self.c1.cout
+
+
+def _round8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+class UNetEngine:
+    def __init__(self, model, device: torch.device, precision: str = "bf16"):
+        if device.type != "cuda":
+            raise RuntimeError("pcms_amd runs on a ROCm device only (no CPU path); move the model to 'cuda'")
+        _lib.load()
+        self.model = model
+        self.device = device
+        self.precision = precision
+        self.tdtype, self.code = _DT[precision]
+        self.esize = 2 if self.code == BF16 else 4
+        self.ncls = model.n_classes
+        self.nmod = model.n_modalities
+        self.cp = _round8(self.nmod)
+        if self.ncls > 4:
+            raise ValueError("the fused output head supports n_classes <= 4")
+        m = model
+        self.enc = [BlockSpec(m.inc, self.cp)]
+        for i in range(1, 5):
+            dc = getattr(m, f"down{i}").maxpool_conv[1]
+            self.enc.append(BlockSpec(dc, dc.conv[0].in_channels))
+        self.ups = []
+        self.dec = []
+        for i in range(1, 5):
+            up = getattr(m, f"up{i}")
+            self.ups.append(up.up)
+            self.dec.append(BlockSpec(up.conv, up.conv.conv[0].in_channels))
+        self.convs: List[ConvSpec] = []
+        self.bns: List[BNSpec] = []
+        for b in self.enc + self.dec:
+            self.convs += [b.c0, b.c1]
+            self.bns += [b.b0, b.b1]
+        self.convt_packs: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._flat_ptrs = None
+        self._packed_version = -1
+        self._dirty = True
+        self.bufs = None
+        self.buf_key = None
+        self.epoch = 0
+        self.saved_epoch = -1
+        self.act_ckpt = False
+        self.wgrad_target = 512
+        self._flatten()
+        for bn in self.bns:
+            c = bn.c
+            bn.scale, bn.shift, bn.mean, bn.invstd = (torch.empty(c, device=device) for _ in range(4))
+
+    # ------------------------------------------------------------------ parameters
+    def _flatten(self):
+        """One flat fp32 master (params), grad and BN-buffer store; modules hold views."""
+        params = list(self.model.parameters())
+        total = sum(p.numel() for p in params)
+        flat = torch.empty(total, dtype=torch.float32, device=self.device)
+        gflat = torch.zeros(total, dtype=torch.float32, device=self.device)
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = flat[off:off + n].view_as(p)
+                if p.grad is not None:
+                    gflat[off:off + n].copy_(p.grad.reshape(-1))
+                p.grad = gflat[off:off + n].view_as(p)
+                off += n
+        bn_total = sum(2 * bn.c for bn in self.bns)
+        bflat = torch.empty(bn_total, dtype=torch.float32, device=self.device)
+        off = 0
+        with torch.no_grad():
+            for bn in self.bns:
+                for name in ("running_mean", "running_var"):
+                    t = getattr(bn.mod, name)
+                    bflat[off:off + bn.c].copy_(t.reshape(-1))
+                    t.data = bflat[off:off + bn.c]
+                    off += bn.c
+                nbt = bn.mod.num_batches_tracked
+                if nbt.device != self.device:
+                    nbt.data = nbt.data.to(self.device)
+        self.params = params
+        self.flat_p, self.flat_g, self.flat_bn = flat, gflat, bflat
+        self._flat_ptrs = [p.data_ptr() for p in params]
+        self._dirty = True
+
+    def sync_params(self):
+        """Re-flatten if a module op (``.to()``, ``.cuda()``, param reassignment) replaced
+        storage, and make every ``param.grad`` a view of the flat gradient again."""
+        if [p.data_ptr() for p in self.params] != self._flat_ptrs or list(self.model.parameters()) != self.params:
+            self._flatten()
+            return
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            g = p.grad
+            if g is None or g.data_ptr() != self.flat_g.data_ptr() + 4 * off:
+                view = self.flat_g[off:off + n].view_as(p)
+                with torch.no_grad():
+                    if g is None:
+                        view.zero_()
+                    else:
+                        view.copy_(g)
+                p.grad = view
+            off += n
+
+    def mark_dirty(self):
+        self._dirty = True
+
+    def _ensure_packs(self):
+        v = self.flat_p._version
+        if not self._dirty and v == self._packed_version:
+            return
+        ck = query("pcms_conv3_chunk", self.code)
+        for i, cs in enumerate(self.convs):
+            w = cs.mod.weight
+            if cs.fwd is None:
+                nch = -(-cs.cin // ck)
+                cs.fwd = torch.empty(nch * 27 * cs.cout * ck, dtype=self.tdtype, device=self.device)
+                if i != 0:  # the stem's input needs no gradient -> no dgrad pack
+                    nchd = -(-cs.cout // ck)
+                    cs.dgrad = torch.empty(nchd * 27 * cs.cin * ck, dtype=self.tdtype, device=self.device)
+            call("pcms_conv3_pack", self.code, w, cs.fwd, cs.cout, cs.cin, 0)
+            if cs.dgrad is not None:
+                call("pcms_conv3_pack", self.code, w, cs.dgrad, cs.cout, cs.cin, 1)
+        for i, up in enumerate(self.ups):
+            cin, cout = up.in_channels, up.out_channels
+            if i not in self.convt_packs:
+                self.convt_packs[i] = (torch.empty(8 * cin * cout, dtype=self.tdtype, device=self.device),
+                                       torch.empty(8 * cin * cout, dtype=self.tdtype, device=self.device))
+            f, d = self.convt_packs[i]
+            call("pcms_convt_pack", self.code, up.weight, f, cin, cout, 0)
+            call("pcms_convt_pack", self.code, up.weight, d, cin, cout, 1)
+        self._packed_version = self.flat_p._version
+        self._dirty = False
+
+    # ------------------------------------------------------------------ buffers
+    def _levels(self, D, H, W):
+        s = [(D, H, W)]
+        for _ in range(4):
+            d, h, w = s[-1]
+            s.append((d // 2, h // 2, w // 2))
+        return s
+
+    def _alloc(self, N, D, H, W):
+        key = (N, D, H, W)
+        if self.buf_key == key:
+            return
+        self.bufs = None
+        S = self._levels(D, H, W)
+        if min(S[4]) < 1:
+            raise ValueError(f"spatial size {(D, H, W)} is too small for 4 poolings")
+        nv = [N * d * h * w for (d, h, w) in S]
+        C = [64 * (1 << l) for l in range(5)]
+        T = self.tdtype
+        dev = self.device
+
+        def act(l, c):
+            return torch.empty(nv[l] * c, dtype=T, device=dev)
+
+        b: Dict[str, object] = {"S": S, "nv": nv, "C": C}
+        b["xin"] = act(0, self.cp)
+        for l in range(5):
+            if l > 0:
+                b[f"pool{l}"] = act(l, C[l - 1])
+            for k in ("y1", "a1", "y2", "x"):
+                b[f"e{l}_{k}"] = act(l, C[l])
+        for l in range(4):
+            for k in ("u", "y1", "a1", "y2", "a2"):
+                b[f"d{l}_{k}"] = act(l, C[l])
+        # gradient buffers
+        for l in range(5):
+            b[f"gx{l}"] = act(l, C[l])      # grad of encoder output x_l (skip + path)
+            b[f"gA{l}"] = act(l, C[l])      # grad of a1 / block outputs (scratch)
+            b[f"gY{l}"] = act(l, C[l])      # grad of pre-BN conv outputs (scratch)
+            b[f"gU{l}"] = act(l, C[l])      # grad of up output / pooled input (scratch)
+        b["gH"] = act(0, C[0])              # grad of the decoder output (head input)
+        # workspaces
+        rows_f = max(query("pcms_conv3_mblocks", N, *S[l]) for l in range(5))
+        rows_s = max(query("pcms_split_epilogue_rows", nv[l]) for l in range(5))
+        rows_b = max(query("pcms_bn_bwd_rows", self.code, C[l], nv[l]) for l in range(5))
+        b["stats"] = torch.empty(max(rows_f, rows_s, rows_b) * 1024 * 2, dtype=torch.float32, device=dev)
+        b["coef"] = torch.empty(3 * 1024, dtype=torch.float32, device=dev)
+        b["dwt"] = torch.empty(27 * 1024 * 1024, dtype=torch.float32, device=dev)
+        # split-K accumulators only where a level can be split (few workgroups along M)
+        split_lv = [l for l in range(5) if query("pcms_conv3_mblocks", N, *S[l]) * (C[l] // 64) < 192]
+        b["yacc"] = torch.empty(max([nv[l] * 2 * C[l] for l in split_lv] + [1]), dtype=torch.float32, device=dev)
+        b["ctws"] = torch.empty(8 * 1024 * 512, dtype=torch.float32, device=dev)
+        self.bufs = b
+        self.buf_key = key
+
+    # ------------------------------------------------------------------ primitives
+    def _splits(self, N, S, cin, cout):
+        mb = query("pcms_conv3_mblocks", N, *S)
+        wgs = mb * (cout // 64)
+        nch = -(-cin // query("pcms_conv3_chunk", self.code))
+        if wgs >= 192 or nch == 1:
+            return 1
+        return max(1, min(nch, -(-384 // wgs)))
+
+    def _conv(self, cs: ConvSpec, x0, c0, x1, c1, y, N, S, stats: bool, training: bool, bn: BNSpec):
+        """y = conv(x) + b; then BN statistics (train) or eval coefficients."""
+        b = self.bufs
+        nvox = N * S[0] * S[1] * S[2]
+        splits = self._splits(N, S, c0 + c1, cs.cout)
+        st = b["stats"] if training else None
+        if splits == 1:
+            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
+                 None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
+            rows = query("pcms_conv3_mblocks", N, *S)
+        else:
+            acc = b["yacc"][: nvox * cs.cout]
+            acc.zero_()
+            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
+                 acc, None, 0, N, S[0], S[1], S[2], cs.cout, splits)
+            call("pcms_split_epilogue", self.code, acc, cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox)
+            rows = query("pcms_split_epilogue_rows", nvox)
+        m = bn.mod
+        if training:
+            if nvox <= 1:
+                raise ValueError(f"Expected more than 1 value per channel when training, got input size "
+                                 f"torch.Size([{N}, {bn.c}, {S[0]}, {S[1]}, {S[2]}])")
+            call("pcms_bn_finalize", st, rows, bn.c, float(nvox), m.weight, m.bias, m.running_mean,
+                 m.running_var, m.num_batches_tracked, BN_MOMENTUM, BN_EPS, bn.scale, bn.shift, bn.mean,
+                 bn.invstd)
+        else:
+            call("pcms_bn_eval_coeffs", m.weight, m.bias, m.running_mean, m.running_var, BN_EPS, bn.c,
+                 bn.scale, bn.shift)
+
+    def _block_fwd(self, blk: BlockSpec, x0, c0, x1, c1, out: Dict[str, torch.Tensor], N, S, training):
+        nvox = N * S[0] * S[1] * S[2]
+        self._conv(blk.c0, x0, c0, x1, c1, out["y1"], N, S, True, training, blk.b0)
+        call("pcms_bn_relu", self.code, out["y1"], out["a1"], blk.b0.scale, blk.b0.shift, blk.c0.cout, nvox)
+        self._conv(blk.c1, out["a1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1)
+        call("pcms_bn_relu", self.code, out["y2"], out["a2"], blk.b1.scale, blk.b1.shift, blk.c1.cout, nvox)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
+        if x.dim() != 5 or x.shape[1] != self.nmod:
+            raise ValueError(f"expected input (N, {self.nmod}, D, H, W), got {tuple(x.shape)}")
+        if x.device != self.device:
+            raise ValueError(f"input on {x.device}, model on {self.device}")
+        x = x.contiguous()
+        if x.dtype != torch.float32:
+            x = x.float()
+        N, _, D, H, W = x.shape
+        self._ensure_packs()
+        self._alloc(N, D, H, W)
+        b = self.bufs
+        S, C = b["S"], b["C"]
+        call("pcms_pack_input", self.code, x, b["xin"], N, self.nmod, D * H * W, self.cp)
+        # encoder
+        inp, cin = b["xin"], self.cp
+        for l in range(5):
+            if l > 0:
+                call("pcms_maxpool_fwd", self.code, b[f"e{l - 1}_x"], b[f"pool{l}"], N, *S[l - 1], C[l - 1])
+                inp, cin = b[f"pool{l}"], C[l - 1]
+            out = {"y1": b[f"e{l}_y1"], "a1": b[f"e{l}_a1"], "y2": b[f"e{l}_y2"], "a2": b[f"e{l}_x"]}
+            self._block_fwd(self.enc[l], inp, cin, None, 0, out, N, S[l], training)
+        # decoder
+        h = b["e4_x"]
+        for i in range(4):
+            l = 3 - i
+            up = self.ups[i]
+            fpack, _ = self.convt_packs[i]
+            call("pcms_convt_fwd", self.code, h, fpack, up.bias, b[f"d{l}_u"], N, *S[l + 1], up.in_channels,
+                 up.out_channels, *S[l])
+            out = {"y1": b[f"d{l}_y1"], "a1": b[f"d{l}_a1"], "y2": b[f"d{l}_y2"], "a2": b[f"d{l}_a2"]}
+            self._block_fwd(self.dec[i], b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], out, N, S[l], training)
+            h = b[f"d{l}_a2"]
+        logits = torch.empty((N, self.ncls, D, H, W), dtype=torch.float32, device=self.device)
+        oc = self.model.outc
+        call("pcms_head_fwd", self.code, h, oc.weight, oc.bias, logits, D * H * W, N, self.ncls)
+        self.epoch += 1
+        if training:
+            self.saved_epoch = self.epoch
+        return logits
+
+    # ------------------------------------------------------------------ backward
+    def _block_bwd(self, blk: BlockSpec, ga2, acts, x0, c0, x1, c1, gx_out0, gx_out1, cy0, N, S, lvl):
+        """Backward of one DoubleConv block. ga2: grad of block output.  Writes the grad of
+        the block input into gx_out0 (channels [0, cy0)) / gx_out1 (rest); None = skip."""
+        b = self.bufs
+        nvox = N * S[0] * S[1] * S[2]
+        gY, gA = b[f"gY{lvl}"], b[f"gA{lvl}"]
+        # BN1/ReLU backward -> dy2
+        self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
+        call("pcms_conv3_wgrad", self.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
+             b["dwt"], N, *S, blk.c1.cout, self.wgrad_target)
+        # dgrad conv1 -> grad of a1
+        self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
+        # BN0/ReLU backward -> dy1 (reuse gY)
+        self._bn_bwd(blk.b0, gA, acts["y1"], gY, nvox)
+        call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gY, blk.c0.mod.weight.grad, b["dwt"], N, *S,
+             blk.c0.cout, self.wgrad_target)
+        if gx_out0 is not None:
+            self._dgrad(blk.c0, gY, gx_out0, gx_out1, cy0, N, S)
+
+    def _bn_bwd(self, bn: BNSpec, ga, y, gy, nvox):
+        b = self.bufs
+        m = bn.mod
+        call("pcms_bn_relu_bwd", self.code, ga, y, bn.scale, bn.shift, bn.mean, bn.invstd, m.weight,
+             b["stats"], b["coef"], m.weight.grad, m.bias.grad, gy, bn.c, nvox)
+
+    def _dgrad(self, cs: ConvSpec, gy, out0, out1, cy0, N, S):
+        b = self.bufs
+        nvox = N * S[0] * S[1] * S[2]
+        splits = self._splits(N, S, cs.cout, cs.cin)
+        if splits == 1:
+            call("pcms_conv3_fwd", self.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
+                 None, None, 0, N, *S, cs.cin, 1)
+        else:
+            acc = b["yacc"][: nvox * cs.cin]
+            acc.zero_()
+            call("pcms_conv3_fwd", self.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
+                 acc, None, 0, N, *S, cs.cin, splits)
+            call("pcms_split_epilogue", self.code, acc, None, out0, out1, cy0, None, cs.cin, nvox)
+
+    def backward(self, dlogits: torch.Tensor):
+        if self.saved_epoch != self.epoch:
+            raise RuntimeError("UNet3D backward must follow its own training forward (the engine keeps "
+                               "only the activations of the latest forward)")
+        self.sync_params()
+        b = self.bufs
+        S, C = b["S"], b["C"]
+        N = self.buf_key[0]
+        dlogits = dlogits.contiguous().float()
+        oc = self.model.outc
+        D, H, W = S[0]
+        call("pcms_head_bwd", self.code, b["d0_a2"], dlogits, oc.weight, b["gH"], oc.weight.grad, oc.bias.grad,
+             D * H * W, N, self.ncls)
+        g = b["gH"]
+        # decoder, last block first
+        for i in reversed(range(4)):
+            l = 3 - i
+            blk = self.dec[i]
+            acts = {"y1": b[f"d{l}_y1"], "a1": b[f"d{l}_a1"], "y2": b[f"d{l}_y2"]}
+            gu = b[f"gU{l}"]
+            self._block_bwd(blk, g, acts, b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], b[f"gx{l}"], gu, C[l], N,
+                            S[l], l)
+            up = self.ups[i]
+            _, dpack = self.convt_packs[i]
+            hin = b["e4_x"] if i == 0 else b[f"d{l + 1}_a2"]
+            call("pcms_convt_wgrad", self.code, hin, gu, up.weight.grad, b["ctws"], N, *S[l + 1], up.in_channels,
+                 up.out_channels, *S[l], 1024)
+            dz = (S[l][0] - 2 * S[l + 1][0]) // 2
+            dy_ = (S[l][1] - 2 * S[l + 1][1]) // 2
+            dx_ = (S[l][2] - 2 * S[l + 1][2]) // 2
+            call("pcms_box_channel_sum", self.code, gu, up.bias.grad, N, *S[l], C[l], dz, dy_, dx_,
+                 2 * S[l + 1][0], 2 * S[l + 1][1], 2 * S[l + 1][2])
+            gnext = b["gx4"] if i == 0 else b[f"gA{l + 1}"]
+            call("pcms_convt_dgrad", self.code, gu, dpack, gnext, N, *S[l + 1], up.in_channels, up.out_channels,
+                 *S[l])
+            g = gnext
+        # encoder, deepest first; gx{l} holds the skip gradient already (l < 4)
+        for l in reversed(range(5)):
+            blk = self.enc[l]
+            acts = {"y1": b[f"e{l}_y1"], "a1": b[f"e{l}_a1"], "y2": b[f"e{l}_y2"]}
+            if l == 0:
+                self._block_bwd(blk, b["gx0"], acts, b["xin"], self.cp, None, 0, None, None, 0, N, S[0], 0)
+            else:
+                gp = b[f"gU{l}"]
+                self._block_bwd(blk, b[f"gx{l}"], acts, b[f"pool{l}"], C[l - 1], None, 0, gp, None, C[l - 1], N,
+                                S[l], l)
+                call("pcms_maxpool_bwd", self.code, b[f"e{l - 1}_x"], gp, b[f"gx{l - 1}"], N, *S[l - 1], C[l - 1])
+        self.saved_epoch = -1

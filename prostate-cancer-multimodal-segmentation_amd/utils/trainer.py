@@ -1,0 +1,185 @@
+"""Drop-in ``BaseTrainer`` / ``Trainer`` for utils/trainer.py of the reference.
+
+The per-batch step of utils/trainer.py:179-195 becomes ``Trainer.step(batch) -> float``:
+
+    images, labels -> device      (:179-180)
+    optimizer.zero_grad()         (:183)
+    outputs = model(images)       (:184)   HIP forward
+    loss = criterion(outputs, y)  (:187)   HIP loss
+    loss.backward()               (:191)   HIP backward (+ RCCL all-reduce of the flat grads)
+    optimizer.step()              (:192)   one flat Adam launch
+    return loss.item()            (:188/195, one host sync instead of two)
+
+Data parallel (one process per GPU, ``torch.distributed`` with the "nccl" = RCCL backend):
+every rank runs the step on its shard; rank 0's BatchNorm running buffers are broadcast
+before the forward (DistributedDataParallel(broadcast_buffers=True) semantics) and the
+flat fp32 gradient is summed with ONE all-reduce, the 1/world mean folded into Adam.
+BatchNorm statistics and the global Dice stay per replica (plain BatchNorm3d).
+
+Config keys follow utils/trainer.py:40-49 (``device``, ``learning_rate``, ``batch_size``,
+``num_epochs``, ``save_dir``, ``validation`` ...) plus ``loss`` ('dice' | 'bce_dice'),
+``precision`` ('bf16' | 'fp32').  The NIfTI data pipeline (script/data_loader.py) is not
+part of this engine: pass ``train_loader`` / ``val_loader`` iterables of batch dicts.
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterable, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.unet3d import UNet3D
+from ..optim import FlatAdam
+from .losses import BCEDiceLoss, DiceLoss
+
+
+class BaseTrainer:
+    def __init__(self, config: dict, train_loader: Optional[Iterable] = None,
+                 val_loader: Optional[Iterable] = None, model: Optional[UNet3D] = None):
+        self.config = config
+        self.device = torch.device(config.get("device", "cuda"))
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.world_size = dist.get_world_size() if self.distributed else 1
+        self.rank = dist.get_rank() if self.distributed else 0
+        self.model = model if model is not None else self._create_model()
+        self.criterion = self._create_criterion()
+        self.optimizer = self._create_optimizer()
+        self.scheduler = self._create_scheduler()
+        self.train_loader = train_loader if train_loader is not None else self._create_dataloader("train")
+        self.val_loader = val_loader
+        if self.val_loader is None and config.get("validation", False):
+            self.val_loader = self._create_dataloader("test")
+        self._copy_stream = None
+        if self.distributed:
+            self._broadcast_params()
+        if config.get("save_dir"):
+            os.makedirs(config["save_dir"], exist_ok=True)
+
+    # ---- construction (utils/trainer.py:76-158) ----
+    def _create_model(self):
+        return UNet3D(n_modalities=self.config.get("n_modalities", 5), n_classes=1,
+                      precision=self.config.get("precision", "bf16")).to(self.device)
+
+    def _create_criterion(self):
+        return BCEDiceLoss() if self.config.get("loss", "dice") == "bce_dice" else DiceLoss()
+
+    def _create_optimizer(self):
+        return FlatAdam(self.model, lr=self.config["learning_rate"], weight_decay=1e-5)
+
+    def _create_scheduler(self):
+        return torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="min", patience=10, factor=0.5)
+
+    def _create_dataloader(self, mode):
+        if self.config.get("data_dir") is None:
+            return None
+        raise NotImplementedError("the NIfTI loader (script/data_loader.py) is outside this engine; "
+                                  "pass train_loader= / val_loader= iterables of {'image','label'} batches")
+
+    def _broadcast_params(self):
+        eng = self.model.engine()
+        dist.broadcast(eng.flat_p, src=0)
+        dist.broadcast(eng.flat_bn, src=0)
+        eng.mark_dirty()
+
+    # ---- the hot path ----
+    def step(self, batch) -> float:
+        loss = self.step_async(batch)
+        return loss.item()
+
+    def step_async(self, batch) -> torch.Tensor:
+        """One training step; returns the loss as a device tensor (no host sync)."""
+        images = batch["image"].to(self.device, non_blocking=True)
+        labels = batch["label"].to(self.device, non_blocking=True)
+        self.model.train()
+        self.optimizer.zero_grad()
+        if self.distributed:
+            dist.broadcast(self.model.engine().flat_bn, src=0)
+        outputs = self.model(images)
+        loss = self.criterion(outputs, labels)
+        loss.backward()
+        if self.distributed:
+            eng = self.model.engine()
+            dist.all_reduce(eng.flat_g, op=dist.ReduceOp.SUM)
+            self.optimizer.grad_scale = 1.0 / self.world_size
+        self.optimizer.step()
+        return loss.detach()
+
+    def _prefetched(self, loader):
+        """Yield batches whose H2D copy ran on a side stream while the previous step ran."""
+        if self.device.type != "cuda":
+            yield from loader
+            return
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(device=self.device)
+        cs = self._copy_stream
+        nxt = None
+        for batch in loader:
+            with torch.cuda.stream(cs):
+                staged = {k: (v.pin_memory().to(self.device, non_blocking=True)
+                              if torch.is_tensor(v) and v.device.type == "cpu" else v)
+                          for k, v in batch.items()}
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            if nxt is not None:
+                yield nxt
+            torch.cuda.current_stream().wait_event(ev)
+            nxt = staged
+        if nxt is not None:
+            yield nxt
+
+    def train_epoch(self):
+        self.model.train()
+        total, n = 0.0, 0
+        for batch in self._prefetched(self.train_loader):
+            total += self.step(batch)
+            n += 1
+        return total / max(n, 1)
+
+    def validate_epoch(self):
+        if self.val_loader is None:
+            return None
+        self.model.eval()
+        total, n = 0.0, 0
+        with torch.no_grad():
+            for batch in self.val_loader:
+                out = self.model(batch["image"].to(self.device))
+                total += self.criterion(out, batch["label"].to(self.device)).item()
+                n += 1
+        return total / max(n, 1)
+
+    def save_checkpoint(self, epoch, loss, is_best=False):
+        """utils/trainer.py:236-278 (same dict keys and file names)."""
+        if self.rank != 0:
+            return
+        ckpt = {"epoch": epoch, "model_state_dict": self.model.state_dict(),
+                "optimizer_state_dict": self.optimizer.state_dict(),
+                "scheduler_state_dict": self.scheduler.state_dict(), "loss": loss, "config": self.config}
+        torch.save(ckpt, os.path.join(self.config["save_dir"], "latest_checkpoint.pth"))
+        if is_best:
+            torch.save(self.model.state_dict(),
+                       os.path.join(self.config["save_dir"], f"best_model_epoch_{epoch}.pth"))
+
+    def train(self):
+        """Epoch loop with ReduceLROnPlateau and early stopping at patience 20 (:280-345)."""
+        best, patience = float("inf"), 0
+        for epoch in range(self.config["num_epochs"]):
+            train_loss = self.train_epoch()
+            val_loss = self.validate_epoch()
+            cur = val_loss if val_loss is not None else train_loss
+            self.scheduler.step(cur)
+            if cur < best:
+                best, patience = cur, 0
+                if self.config.get("save_dir"):
+                    self.save_checkpoint(epoch + 1, cur, is_best=True)
+            else:
+                patience += 1
+            if patience >= 20:
+                break
+        return best
+
+
+class Trainer(BaseTrainer):
+    """The ``Trainer`` that run.py:30 imports (absent from the reference); BaseTrainer + step()."""

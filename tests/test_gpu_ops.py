@@ -1,0 +1,361 @@
+"""Kernel-level numerics on the GPU: every entry point of libpcms_hip.so against a plain
+PyTorch CPU reference of the same op (fp64 on the same, already-rounded inputs).
+
+bf16 cases feed the CPU reference the bf16-rounded inputs, so the only differences left
+are fp32 accumulation order and the final bf16 rounding of the output.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _lib():
+    import pcms_amd  # noqa: F401
+    from pcms_amd import _lib as L
+    return L
+
+
+def ndhwc(x):  # (N,C,D,H,W) -> (N,D,H,W,C)
+    return x.permute(0, 2, 3, 4, 1).contiguous()
+
+
+def ncdhw(x):
+    return x.permute(0, 4, 1, 2, 3).contiguous()
+
+
+def q(x, dt):
+    """round to the storage dtype (on CPU), return (cpu fp64 copy, device tensor)."""
+    xd = x.to(dt)
+    return xd.double(), xd.to(DEV)
+
+
+def close(got, exp, tol, what=""):
+    got = got.double().cpu()
+    exp = exp.double().cpu()
+    scale = exp.abs().max().item() + 1e-12
+    err = (got - exp).abs().max().item()
+    assert err <= tol * scale, f"{what}: max err {err:.3e} > {tol:.1e} * {scale:.3e}"
+
+
+DTS = [(torch.float32, 0, 2e-5), (torch.bfloat16, 1, 1e-2)]
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+@pytest.mark.parametrize("N,cin,cout,S,split", [
+    (2, 8, 64, (16, 16, 16), 1),        # stem-like (5 real channels padded to 8)
+    (1, 64, 64, (9, 10, 11), 1),        # odd sizes, partial boxes
+    (2, 64, 128, (8, 8, 8), 1),
+    (1, 128, 64, (16, 16, 16), 1),
+    (2, 256, 128, (4, 4, 4), 4),        # split-K
+    (1, 64, 64, (1, 1, 1), 2),          # 1-voxel volume
+])
+def test_conv3_fwd(dt, code, tol, N, cin, cout, S, split):
+    L = _lib()
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    cin_real = 5 if cin == 8 else cin
+    x = torch.randn(N, cin_real, *S, generator=g)
+    w = torch.randn(cout, cin_real, 3, 3, 3, generator=g) / math.sqrt(27 * cin_real)
+    b = torch.randn(cout, generator=g)
+    xq, _ = q(x, dt)
+    wq = w.to(dt).double()
+    ref = F.conv3d(xq, wq, b.double(), padding=1)
+    xs = torch.zeros(N, cin, *S, dtype=dt)
+    xs[:, :cin_real] = x.to(dt)
+    xd = ndhwc(xs).to(DEV)
+    ck = L.query("pcms_conv3_chunk", code)
+    nch = -(-cin_real // ck)
+    wpack = torch.empty(nch * 27 * cout * ck, dtype=dt, device=DEV)
+    L.call("pcms_conv3_pack", code, w.to(DEV), wpack, cout, cin_real, 0)
+    y = torch.empty(N, *S, cout, dtype=dt, device=DEV)
+    nvox = N * S[0] * S[1] * S[2]
+    rows = L.query("pcms_conv3_mblocks", N, *S)
+    stats = torch.zeros(max(rows, L.query("pcms_split_epilogue_rows", nvox)) * cout * 2, device=DEV)
+    if split == 1:
+        L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, None, stats, 0,
+               N, *S, cout, 1)
+    else:
+        acc = torch.zeros(nvox * cout, device=DEV)
+        L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, acc, None, 0,
+               N, *S, cout, split)
+        L.call("pcms_split_epilogue", code, acc, b.to(DEV), y, None, cout, stats, cout, nvox)
+        rows = L.query("pcms_split_epilogue_rows", nvox)
+    torch.cuda.synchronize()
+    close(ncdhw(y.cpu()), ref, tol, "conv3 fwd")
+    st = stats.cpu()[: rows * cout * 2].view(rows, cout, 2).double().sum(0)
+    yref = ref.transpose(0, 1).reshape(cout, -1)
+    close(st[:, 0], yref.sum(1), 1e-3 if code else 1e-5, "stats sum")
+    close(st[:, 1], (yref * yref).sum(1), 1e-3 if code else 1e-5, "stats sumsq")
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+def test_conv3_dual_source_and_dgrad_split_output(dt, code, tol):
+    """Up3D: conv over cat([skip, up]) without materialising the cat, and the dgrad whose
+    output splits back into the two gradients."""
+    L = _lib()
+    g = torch.Generator().manual_seed(3)
+    N, S, cs, cout = 2, (8, 6, 10), 64, 64
+    skip = torch.randn(N, cs, *S, generator=g).to(dt)
+    up = torch.randn(N, cs, *S, generator=g).to(dt)
+    w = (torch.randn(cout, 2 * cs, 3, 3, 3, generator=g) / math.sqrt(27 * 2 * cs))
+    ref = F.conv3d(torch.cat([skip, up], 1).double(), w.to(dt).double(), None, padding=1)
+    ck = L.query("pcms_conv3_chunk", code)
+    wp = torch.empty(-(-2 * cs // ck) * 27 * cout * ck, dtype=dt, device=DEV)
+    L.call("pcms_conv3_pack", code, w.to(DEV), wp, cout, 2 * cs, 0)
+    y = torch.empty(N, *S, cout, dtype=dt, device=DEV)
+    L.call("pcms_conv3_fwd", code, ndhwc(skip).to(DEV), cs, ndhwc(up).to(DEV), cs, wp, None, y, None, cout,
+           None, None, 0, N, *S, cout, 1)
+    torch.cuda.synchronize()
+    close(ncdhw(y.cpu()), ref, tol, "dual-source fwd")
+    # dgrad: dX = conv_transpose of dy with W  (autograd reference)
+    dy = torch.randn(N, cout, *S, generator=g).to(dt)
+    xr = torch.cat([skip, up], 1).double().requires_grad_(True)
+    F.conv3d(xr, w.to(dt).double(), None, padding=1).backward(dy.double())
+    wd = torch.empty(-(-cout // ck) * 27 * 2 * cs * ck, dtype=dt, device=DEV)
+    L.call("pcms_conv3_pack", code, w.to(DEV), wd, cout, 2 * cs, 1)
+    gs = torch.empty(N, *S, cs, dtype=dt, device=DEV)
+    gu = torch.empty(N, *S, cs, dtype=dt, device=DEV)
+    L.call("pcms_conv3_fwd", code, ndhwc(dy).to(DEV), cout, None, 0, wd, None, gs, gu, cs, None, None, 0,
+           N, *S, 2 * cs, 1)
+    torch.cuda.synchronize()
+    close(ncdhw(gs.cpu()), xr.grad[:, :cs], tol, "dgrad skip part")
+    close(ncdhw(gu.cpu()), xr.grad[:, cs:], tol, "dgrad up part")
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+@pytest.mark.parametrize("N,c0,c1,cout,S", [
+    (2, 8, 0, 64, (16, 16, 16)),
+    (1, 64, 0, 64, (9, 10, 11)),
+    (2, 64, 64, 64, (8, 8, 8)),
+    (2, 128, 0, 128, (4, 4, 4)),
+    (2, 256, 0, 64, (1, 2, 1)),
+])
+def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
+    L = _lib()
+    g = torch.Generator().manual_seed(c0 + 3 * cout)
+    cin = c0 + c1
+    cin_real = 5 if cin == 8 else cin
+    x = torch.zeros(N, cin, *S)
+    x[:, :cin_real] = torch.randn(N, cin_real, *S, generator=g)
+    x = x.to(dt)
+    dy = torch.randn(N, cout, *S, generator=g).to(dt)
+    xr = x[:, :cin_real].double()
+    wr = torch.zeros(cout, cin_real, 3, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv3d(xr, wr, None, padding=1).backward(dy.double())
+    dw = torch.zeros(cout, cin_real, 3, 3, 3, device=DEV)
+    # kernel's Cin is the stored channel count; the pad channels carry zeros
+    dw_full = torch.zeros(cout, cin, 27, device=DEV)
+    ws = torch.empty(27 * cout * cin, device=DEV)
+    xs = ndhwc(x).to(DEV)
+    if c1:
+        L.call("pcms_conv3_wgrad", code, ndhwc(x[:, :c0]).to(DEV), c0, ndhwc(x[:, c0:]).to(DEV), c1,
+               ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, 256)
+    else:
+        L.call("pcms_conv3_wgrad", code, xs, c0, None, 0, ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, 256)
+    torch.cuda.synchronize()
+    got = dw_full.cpu().view(cout, cin, 3, 3, 3)[:, :cin_real]
+    close(got, wr.grad, 1e-4 if code else 2e-5, "wgrad")
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+def test_bn_relu_fwd_bwd(dt, code, tol):
+    L = _lib()
+    g = torch.Generator().manual_seed(11)
+    N, C, S = 2, 128, (6, 7, 8)
+    nvox = N * S[0] * S[1] * S[2]
+    y = (torch.randn(N, C, *S, generator=g) * 3 + 1).to(dt)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g)
+    rm, rv = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+    # statistics from per-voxel partial rows (one voxel per row here)
+    yv = ndhwc(y).reshape(nvox, C).double()
+    part = torch.stack([yv, yv * yv], -1).float().contiguous()
+    yr = y.double().requires_grad_(True)
+    rm_r, rv_r = rm.double().clone(), rv.double().clone()
+    out = F.relu(F.batch_norm(yr, rm_r, rv_r, gamma.double(), beta.double(), True, 0.1, 1e-5))
+    da = torch.randn(N, C, *S, generator=g).to(dt)
+    out.backward(da.double())
+    gd, bd = gamma.to(DEV), beta.to(DEV)
+    rmd, rvd = rm.clone().to(DEV), rv.clone().to(DEV)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    scale, shift, mean, invstd = (torch.empty(C, device=DEV) for _ in range(4))
+    L.call("pcms_bn_finalize", part.to(DEV), nvox, C, float(nvox), gd, bd, rmd, rvd, nbt, 0.1, 1e-5,
+           scale, shift, mean, invstd)
+    yd = ndhwc(y).to(DEV)
+    a = torch.empty_like(yd)
+    L.call("pcms_bn_relu", code, yd, a, scale, shift, C, nvox)
+    rows = L.query("pcms_bn_bwd_rows", code, C, nvox)
+    bpart = torch.empty(rows * C * 2, device=DEV)
+    coef = torch.empty(3 * C, device=DEV)
+    dgam, dbet = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dy = torch.empty_like(yd)
+    L.call("pcms_bn_relu_bwd", code, ndhwc(da).to(DEV), yd, scale, shift, mean, invstd, gd, bpart, coef,
+           dgam, dbet, dy, C, nvox)
+    torch.cuda.synchronize()
+    assert int(nbt) == 1
+    close(rmd.cpu(), rm_r, 1e-5, "running_mean")
+    close(rvd.cpu(), rv_r, 1e-5, "running_var")
+    close(ncdhw(a.cpu()), out.detach(), tol, "bn+relu fwd")
+    close(ncdhw(dy.cpu()), yr.grad, 5 * tol, "bn+relu bwd")
+    # reference grads of gamma/beta through autograd
+    gr = gamma.double().requires_grad_(True)
+    br = beta.double().requires_grad_(True)
+    F.relu(F.batch_norm(y.double(), None, None, gr, br, True, 0.1, 1e-5)).backward(da.double())
+    close(dgam.cpu(), gr.grad, 1e-3 if code else 1e-5, "dgamma")
+    close(dbet.cpu(), br.grad, 1e-3 if code else 1e-5, "dbeta")
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+def test_maxpool_fwd_bwd(dt, code, tol):
+    L = _lib()
+    g = torch.Generator().manual_seed(5)
+    N, C, S = 2, 64, (7, 6, 9)
+    a = torch.randn(N, C, *S, generator=g)
+    a[:, :, :2, :2, :2] = 0.0  # ties among zeros (ReLU outputs)
+    a = a.to(dt)
+    ar = a.double().requires_grad_(True)
+    p = F.max_pool3d(ar, 2)
+    dp = torch.randn(p.shape, generator=g).to(dt)
+    p.backward(dp.double())
+    ad = ndhwc(a).to(DEV)
+    pd = torch.empty(N, S[0] // 2, S[1] // 2, S[2] // 2, C, dtype=dt, device=DEV)
+    L.call("pcms_maxpool_fwd", code, ad, pd, N, *S, C)
+    base = torch.randn(N, C, *S, generator=g).to(dt)
+    da = ndhwc(base).to(DEV)
+    L.call("pcms_maxpool_bwd", code, ad, ndhwc(dp).to(DEV), da, N, *S, C)
+    torch.cuda.synchronize()
+    close(ncdhw(pd.cpu()), p.detach(), 0, "maxpool fwd")
+    close(ncdhw(da.cpu()), base.double() + ar.grad, tol, "maxpool bwd (accumulate)")
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+@pytest.mark.parametrize("Sin,Sout", [((4, 4, 2), (8, 8, 4)), ((2, 2, 3), (5, 4, 7))])
+def test_convt(dt, code, tol, Sin, Sout):
+    L = _lib()
+    g = torch.Generator().manual_seed(9)
+    N, cin, cout = 2, 128, 64
+    x = torch.randn(N, cin, *Sin, generator=g).to(dt)
+    w = (torch.randn(cin, cout, 2, 2, 2, generator=g) / math.sqrt(cin)).to(dt)
+    b = torch.randn(cout, generator=g)
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    u = F.conv_transpose3d(xr, wr, br, stride=2)
+    dz, dyy, dxx = (Sout[i] - u.shape[2 + i] for i in range(3))
+    up = F.pad(u, [dxx // 2, dxx - dxx // 2, dyy // 2, dyy - dyy // 2, dz // 2, dz - dz // 2])
+    gout = torch.randn(up.shape, generator=g).to(dt)
+    up.backward(gout.double())
+    fp = torch.empty(8 * cin * cout, dtype=dt, device=DEV)
+    dp = torch.empty(8 * cin * cout, dtype=dt, device=DEV)
+    wdev = w.float().to(DEV)
+    L.call("pcms_convt_pack", code, wdev, fp, cin, cout, 0)
+    L.call("pcms_convt_pack", code, wdev, dp, cin, cout, 1)
+    out = torch.full((N, *Sout, cout), float("nan"), dtype=dt, device=DEV)
+    L.call("pcms_convt_fwd", code, ndhwc(x).to(DEV), fp, b.to(DEV), out, N, *Sin, cin, cout, *Sout)
+    god = ndhwc(gout).to(DEV)
+    dx = torch.empty(N, *Sin, cin, dtype=dt, device=DEV)
+    L.call("pcms_convt_dgrad", code, god, dp, dx, N, *Sin, cin, cout, *Sout)
+    dw = torch.zeros(cin, cout, 2, 2, 2, device=DEV)
+    ws = torch.empty(8 * cin * cout, device=DEV)
+    L.call("pcms_convt_wgrad", code, ndhwc(x).to(DEV), god, dw, ws, N, *Sin, cin, cout, *Sout, 64)
+    db = torch.zeros(cout, device=DEV)
+    L.call("pcms_box_channel_sum", code, god, db, N, *Sout, cout, dz // 2, dyy // 2, dxx // 2,
+           2 * Sin[0], 2 * Sin[1], 2 * Sin[2])
+    torch.cuda.synchronize()
+    close(ncdhw(out.cpu()), up.detach(), tol, "convT fwd (+pad)")
+    close(ncdhw(dx.cpu()), xr.grad, tol, "convT dgrad")
+    close(dw.cpu(), wr.grad, 1e-4 if code else 2e-5, "convT wgrad")
+    close(db.cpu(), br.grad, 1e-4 if code else 1e-5, "convT bias grad")
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+@pytest.mark.parametrize("ncls", [1, 2])
+def test_head(dt, code, tol, ncls):
+    L = _lib()
+    g = torch.Generator().manual_seed(1)
+    N, S = 2, (5, 6, 7)
+    a = torch.relu(torch.randn(N, 64, *S, generator=g)).to(dt)
+    w = torch.randn(ncls, 64, 1, 1, 1, generator=g) * 0.1
+    b = torch.randn(ncls, generator=g)
+    ar = a.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    out = F.conv3d(ar, wr, br)
+    dl = torch.randn(out.shape, generator=g)
+    out.backward(dl.double())
+    V = S[0] * S[1] * S[2]
+    logits = torch.empty(N, ncls, *S, device=DEV)
+    ad = ndhwc(a).to(DEV)
+    L.call("pcms_head_fwd", code, ad, w.reshape(ncls, 64).to(DEV), b.to(DEV), logits, V, N, ncls)
+    da = torch.empty_like(ad)
+    dw = torch.zeros(ncls, 64, device=DEV)
+    db = torch.zeros(ncls, device=DEV)
+    L.call("pcms_head_bwd", code, ad, dl.to(DEV), w.reshape(ncls, 64).to(DEV), da, dw, db, V, N, ncls)
+    torch.cuda.synchronize()
+    close(logits.cpu(), out.detach(), 1e-5, "head fwd")
+    close(ncdhw(da.cpu()), ar.grad, tol, "head dgrad")
+    close(dw.cpu(), wr.grad.reshape(ncls, 64), 1e-5, "head wgrad")
+    close(db.cpu(), br.grad, 1e-5, "head bias grad")
+
+
+@pytest.mark.parametrize("wb,wd", [(0.0, 1.0), (0.5, 0.5)])
+def test_loss(wb, wd):
+    L = _lib()
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(2, 1, 9, 10, 11, generator=g) * 3
+    t = (torch.rand(x.shape, generator=g) < 0.3).float()
+    xr = x.double().requires_grad_(True)
+    p = torch.sigmoid(xr).reshape(-1)
+    tt = t.double().reshape(-1)
+    dice = 1 - (2 * (p * tt).sum() + 1) / (p.sum() + tt.sum() + 1)
+    ref = wb * F.binary_cross_entropy_with_logits(xr, t.double()) + wd * dice
+    ref.backward(torch.tensor(0.7, dtype=torch.float64))
+    M = x.numel()
+    rows = L.query("pcms_loss_rows", M)
+    part = torch.empty(rows * 4, device=DEV)
+    sums = torch.empty(4, dtype=torch.float64, device=DEV)
+    loss = torch.empty((), device=DEV)
+    xd, td = x.to(DEV), t.to(DEV)
+    L.call("pcms_loss_fwd", xd, td, M, 1.0, wb, wd, part, sums, loss)
+    dx = torch.empty_like(xd)
+    L.call("pcms_loss_bwd", xd, td, M, sums, 1.0, wb, wd, torch.tensor(0.7, device=DEV), dx)
+    torch.cuda.synchronize()
+    assert abs(loss.item() - ref.item()) < 1e-6
+    close(dx.cpu(), xr.grad, 1e-5, "loss grad")
+
+
+def test_adam_matches_torch():
+    L = _lib()
+    g = torch.Generator().manual_seed(4)
+    n = 10007
+    p0 = torch.randn(n, generator=g)
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=1e-3, weight_decay=1e-5)
+    pd = p0.clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    for step in range(1, 4):
+        gr = torch.randn(n, generator=g)
+        pt.grad = gr.clone()
+        opt.step()
+        L.call("pcms_adam", pd, gr.to(DEV), m, v, n, 1e-3 / (1 - 0.9 ** step), 0.9, 0.999, 1e-8, 1e-5,
+               math.sqrt(1 - 0.999 ** step), 1.0)
+    torch.cuda.synchronize()
+    close(pd.cpu(), pt.detach(), 1e-6, "adam")
+
+
+@pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
+def test_pack_input(dt, code):
+    L = _lib()
+    x = torch.rand(2, 5, 3, 4, 5)
+    out = torch.empty(2, 3, 4, 5, 8, dtype=dt, device=DEV)
+    L.call("pcms_pack_input", code, x.to(DEV), out, 2, 5, 60, 8)
+    torch.cuda.synchronize()
+    exp = torch.zeros(2, 3, 4, 5, 8)
+    exp[..., :5] = ndhwc(x)
+    close(out.cpu(), exp.to(dt), 0, "pack input")

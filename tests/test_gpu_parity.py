@@ -1,0 +1,149 @@
+"""End-to-end parity of the HIP engine against the golden vectors of the REFERENCE
+(tests/golden, produced by importing the reference's models/unet3d.py + utils/losses.py).
+
+fp32 build (precision="fp32"): the north-star bar —
+  * train-mode logits within 1e-3 of the reference, identical ``logit > 0`` masks on every
+    voxel whose reference |logit| >= 1e-3;
+  * loss, every gradient, the post-Adam parameters and BatchNorm buffers, eval logits,
+    and the second step's loss.
+bf16 build: a stated looser bound (bf16 storage cannot meet 1e-3: SURVEY F4/H3) —
+  loss within 1e-2 absolute, >= 99 % identical masks, logits within 0.1 * max|logit|.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+PRE_BN_BIAS = ("conv.0.bias", "conv.3.bias")  # exact grad 0, reference has noise
+
+
+def _build(name, precision):
+    import pcms_amd
+    from pcms_amd.models.unet3d import UNet3D
+    ncls = gu.CASES[name][0]
+    torch.manual_seed(0)
+    m = UNet3D(n_modalities=5, n_classes=ncls, precision=precision)
+    return m.cuda()
+
+
+def _crit(name):
+    from pcms_amd.utils.losses import BCEDiceLoss, DiceLoss
+    return BCEDiceLoss() if gu.CASES[name][4] == "bce_dice" else DiceLoss()
+
+
+def _opt(m, name):
+    from pcms_amd.optim import FlatAdam
+    return FlatAdam(m, lr=gu.CASES[name][5], weight_decay=1e-5)
+
+
+@pytest.mark.parametrize("name", list(gu.CASES))
+def test_fp32_parity_full_step(name):
+    g = gu.load(name)
+    m = _build(name, "fp32")
+    assert gu.sd_hash({k: v.cpu() for k, v in m.state_dict().items()}) == str(g["sd_sha256"])
+    crit, opt = _crit(name), _opt(m, name)
+    x, y = gu.batch(name, 0)
+    m.train()
+    opt.zero_grad()
+    logits = m(x.cuda())
+    loss = crit(logits, y.cuda())
+    loss.backward()
+    lg = logits.detach().cpu().numpy()
+    ref = g["logits_train"]
+    err = np.abs(lg - ref).max()
+    assert err <= 1e-3, f"logits max err {err}"
+    sure = np.abs(ref) >= 1e-3
+    assert np.array_equal((lg > 0)[sure], (ref > 0)[sure])
+    assert abs(float(loss) - float(g["loss0"])) < 1e-5
+    for k, p in m.named_parameters():
+        got = gu.sampled(p.grad, g["g_stride__" + k])
+        exp = g["g__" + k]
+        if k.endswith(PRE_BN_BIAS):
+            assert np.abs(got).max() < 1e-4, k
+            continue
+        scale = max(float(np.abs(exp).max()), 1e-12)
+        assert np.abs(got - exp).max() <= 2e-3 * scale + 1e-7, (k, np.abs(got - exp).max(), scale)
+    opt.step()
+    lr = gu.CASES[name][5]
+    for k, p in m.named_parameters():
+        if k.endswith(PRE_BN_BIAS):
+            assert np.abs(gu.sampled(p.detach(), g["p_stride__" + k]) - g["p__" + k]).max() <= 1.01 * lr + 1e-7
+            continue
+        got = gu.sampled(p.detach(), g["p_stride__" + k])
+        exp = g["p__" + k]
+        d = np.abs(got - exp)
+        # Adam's first step moves each weight by ~lr*sign(g): a grad that is ~0 in both
+        # builds may flip sign -> bounded by 2 lr; everything else matches tightly.
+        assert d.max() <= 2.01 * lr + 1e-6, (k, d.max())
+        assert np.mean(d > 1e-5 * np.abs(exp) + 1e-6) < 0.01, (k, np.mean(d > 1e-5 * np.abs(exp) + 1e-6))
+    sd = m.state_dict()
+    for k in sd:
+        if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+            np.testing.assert_allclose(sd[k].cpu().numpy(), g["b__" + k], rtol=1e-4, atol=1e-5, err_msg=k)
+    m.eval()
+    with torch.no_grad():
+        le = m(x.cuda()).cpu().numpy()
+    assert np.abs(le - g["logits_eval"]).max() <= 2e-3 * max(1.0, np.abs(g["logits_eval"]).max())
+    m.train()
+    x1, y1 = gu.batch(name, 1)
+    opt.zero_grad()
+    l1 = crit(m(x1.cuda()), y1.cuda())
+    l1.backward()
+    opt.step()
+    assert abs(float(l1) - float(g["loss1"])) < 2e-4
+
+
+@pytest.mark.parametrize("name", ["c16_bcedice", "cfg1_dice", "odd_bcedice"])
+def test_bf16_parity_step(name):
+    g = gu.load(name)
+    m = _build(name, "bf16")
+    crit, opt = _crit(name), _opt(m, name)
+    x, y = gu.batch(name, 0)
+    m.train()
+    opt.zero_grad()
+    logits = m(x.cuda())
+    loss = crit(logits, y.cuda())
+    loss.backward()
+    opt.step()
+    lg = logits.detach().cpu().numpy()
+    ref = g["logits_train"]
+    assert abs(float(loss) - float(g["loss0"])) < 1e-2
+    assert np.abs(lg - ref).max() <= 0.1 * np.abs(ref).max()
+    assert np.mean((lg > 0) == (ref > 0)) >= 0.99
+    for k, p in m.named_parameters():
+        assert torch.isfinite(p.grad).all(), k
+
+
+def test_predict_inference_and_trainer_step():
+    from pcms_amd.utils.trainer import Trainer
+    g = gu.load("c16_bcedice")
+    torch.manual_seed(0)
+    cfg = {"device": "cuda", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1, "loss": "bce_dice",
+           "precision": "fp32"}
+    tr = Trainer(cfg)
+    x, y = gu.batch("c16_bcedice", 0)
+    l0 = tr.step({"image": x, "label": y, "case_id": ["a", "b"]})
+    assert abs(l0 - float(g["loss0"])) < 1e-5
+    x1, y1 = gu.batch("c16_bcedice", 1)
+    l1 = tr.step({"image": x1, "label": y1, "case_id": ["a", "b"]})
+    assert abs(l1 - float(g["loss1"])) < 2e-4
+    probs = tr.model.predict(x.cuda())
+    mask = tr.model.inference(x.cuda())
+    assert probs.shape == (2, 1, 16, 16, 16)
+    assert torch.equal(mask, (probs > 0.5).float())
+
+
+def test_shape_mismatch_and_cpu_refusal():
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.utils.losses import DiceLoss
+    with pytest.raises(ValueError):
+        DiceLoss()(torch.zeros(1, 1, 2, 2, 2, device="cuda"), torch.zeros(1, 2, 2, 2, 2, device="cuda"))
+    m = UNet3D(n_modalities=5, n_classes=1)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 5, 16, 16, 16))
+    mm = UNet3D(n_modalities=5, n_classes=1).cuda()
+    with pytest.raises(ValueError):
+        mm(torch.zeros(1, 5, 16, 16, 16, device="cuda"))  # 1 value per channel at the bottleneck
