@@ -67,7 +67,7 @@ def stem_roofline(tr, N, spatial, reps):
                0, N, D, H, W, 64, 1)
 
     def wgrad(s):
-        L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 512)
+        L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
 
     res = {}
     for name, fn in (("fwd", fwd), ("wgrad", wgrad)):

@@ -42,10 +42,11 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
                    float* yacc, float* stats, int accumulate,
                    int N, int D, int H, int W, int Cout, int splits, hipStream_t s);
-/* dw [Cout][Cin][27] fp32 += sum_v dy[v, co] * x[v + tap, ci];  dwt = 27*Cout*Cin fp32 ws */
+/* dw [Cout][cin_w][27] fp32 += sum_v dy[v, co] * x[v + tap, ci] (ci < cin_w <= c0 + c1);
+ * dwt = 27*Cout*(c0+c1) fp32 workspace                                                   */
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
-                     float* dw, float* dwt, int N, int D, int H, int W, int Cout, int target_wgs,
-                     hipStream_t s);
+                     float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
+                     int target_wgs, hipStream_t s);
 int pcms_split_epilogue_rows(long nvox);
 int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0,
                         float* stats, int C, long nvox, hipStream_t s);

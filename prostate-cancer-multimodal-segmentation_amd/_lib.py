@@ -21,7 +21,7 @@ SIGNATURES = {
     "pcms_conv3_mblocks": "iiii",
     "pcms_conv3_pack": "ippiiis",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
-    "pcms_conv3_wgrad": "ipipipppiiiiiis",
+    "pcms_conv3_wgrad": "ipipipppiiiiiiis",
     "pcms_split_epilogue_rows": "l",
     "pcms_split_epilogue": "ippppipils",
     "pcms_bn_finalize": "piidpppppffpppps",

@@ -466,13 +466,14 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   }
 }
 
-// dwt [27][Cout][Cin] (fp32 workspace) -> dw [Cout][Cin][27] (+=), torch OIDHW layout
-__global__ void wgrad_permute_kernel(const float* dwt, float* dw, int Cout, int Cin) {
-  const long total = (long)Cout * Cin * 27;
+// dwt [27][Cout][Cin] (fp32 workspace, Cin = stored channels) -> dw [Cout][Cw][27] (+=),
+// torch OIDHW layout with the weight's own input-channel count Cw <= Cin (stem: 5 of 8)
+__global__ void wgrad_permute_kernel(const float* dwt, float* dw, int Cout, int Cin, int Cw) {
+  const long total = (long)Cout * Cw * 27;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int t = i % 27;
     const long oc = i / 27;
-    const int ci = oc % Cin, co = oc / Cin;
+    const int ci = oc % Cw, co = oc / Cw;
     dw[i] += dwt[((long)t * Cout + co) * Cin + ci];
   }
 }
@@ -505,7 +506,7 @@ int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
 // Pick a power-of-two box (<= maxvol voxels, halo <= maxhalo rows) minimising padded
 // volume (then maximising box size) for a D x H x W grid.
 Box choose_box(int D, int H, int W, int maxvol, int maxhalo, int minw, int minvol) {
-  Box best{0, 0, 0};
+  Box best{3, 3, 3};  // (8,8,8): always valid (vol 512, halo 1000) -- overwritten below
   double best_cost = 1e30;
   for (int a = 0; a <= 4; ++a)
     for (int b = 0; b <= 5; ++b)
@@ -514,9 +515,6 @@ Box choose_box(int D, int H, int W, int maxvol, int maxhalo, int minw, int minvo
         if (bd * bh * bw > maxvol || bd * bh * bw < minvol) continue;
         if ((bd + 2) * (bh + 2) * (bw + 2) > maxhalo) continue;
         if (bw < minw && bw < W) continue;
-        if (bd > 2 * D && bd > 1) continue;
-        if (bh > 2 * H && bh > 1) continue;
-        if (bw > 2 * W && bw > 1) continue;
         const double padded = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh * cdiv(W, bw) * bw;
         const double halo = (double)cdiv(D, bd) * cdiv(H, bh) * cdiv(W, bw) * (bd + 2) * (bh + 2) * (bw + 2);
         const double cost = padded + 0.15 * halo;
@@ -587,12 +585,14 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   PCMS_CHECK_LAUNCH();
 }
 
-// Weight gradient: dw (torch layout [Cout][Cin][27], fp32) += sum_v dy (x) x.
+// Weight gradient: dw (torch layout [Cout][cin_w][27], fp32) += sum_v dy (x) x, where
+// cin_w <= c0 + c1 is the weight's input-channel count (the stored input may be padded).
 // dwt: fp32 workspace of 27*Cout*Cin floats (zeroed here).
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
-                     float* dw, float* dwt, int N, int D, int H, int W, int Cout, int target_wgs,
+                     float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w, int target_wgs,
                      hipStream_t s) {
   const int Cin = c0 + c1;
+  if (cin_w <= 0 || cin_w > Cin) return -4;
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0) return -1;
   const int bv = dtype == PCMS_BF16 ? WTraits<bf16_t>::BV : WTraits<float>::BV;
@@ -623,9 +623,9 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   }
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const long total = 27L * Cout * Cin;
+  const long total = 27L * Cout * cin_w;
   hipLaunchKernelGGL(wgrad_permute_kernel, dim3((int)std::min<long>(4096, (total + 255) / 256)), dim3(256), 0, s,
-                     (const float*)dwt, dw, Cout, Cin);
+                     (const float*)dwt, dw, Cout, Cin, cin_w);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -347,13 +347,13 @@ class UNetEngine:
         # BN1/ReLU backward -> dy2
         self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         call("pcms_conv3_wgrad", self.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
-             b["dwt"], N, *S, blk.c1.cout, self.wgrad_target)
+             b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target)
         # dgrad conv1 -> grad of a1
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
         # BN0/ReLU backward -> dy1 (reuse gY)
         self._bn_bwd(blk.b0, gA, acts["y1"], gY, nvox)
         call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gY, blk.c0.mod.weight.grad, b["dwt"], N, *S,
-             blk.c0.cout, self.wgrad_target)
+             blk.c0.cout, blk.c0.cin, self.wgrad_target)
         if gx_out0 is not None:
             self._dgrad(blk.c0, gY, gx_out0, gx_out1, cy0, N, S)
 

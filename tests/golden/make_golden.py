@@ -20,6 +20,7 @@ Fixtures (``tests/golden/<case>.npz``, numpy arrays only, no pickles):
   p__<key>             parameter after step-1 Adam (same sampling)
   b__<key>             every BN buffer after step 1
   logits_eval          eval-mode forward after step 1
+  *64 / g64__<key>     the same quantities from the reference run in float64
 """
 from __future__ import annotations
 
@@ -108,6 +109,30 @@ def run_case(name, n_classes, n, spatial, lab_kind, loss_kind, lr):
                 out["logits_eval"] = model(x0).numpy().copy()
             model.train()
     out["loss0"], out["loss1"] = np.array(losses[0]), np.array(losses[1])
+    # the same two steps in float64: the fp64 "truth" that tells how ill-conditioned each
+    # gradient is (the fp32 reference itself differs from it by up to ~10 % on some tensors)
+    torch.manual_seed(0)
+    model = UNet3D(n_modalities=5, n_classes=n_classes).double()
+    opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-5)
+    model.train()
+    for step in range(2):
+        b = synthetic.make_batch(n, spatial, seed=synthetic.step_seed(0, step), label=lab_kind)
+        x, y = b["image"].double(), b["label"].double()
+        if n_classes != 1:
+            y = y.repeat(1, n_classes, 1, 1, 1)
+        opt.zero_grad()
+        logits = model(x)
+        loss = crit(logits, y)
+        loss.backward()
+        if step == 0:
+            out["logits_train64"] = logits.detach().numpy().copy()
+            out["loss0_64"] = np.array(float(loss))
+            for k, p in model.named_parameters():
+                s_, _ = sample(p.grad)
+                out["g64__" + k] = s_
+        else:
+            out["loss1_64"] = np.array(float(loss))
+        opt.step()
     return out
 
 

@@ -147,18 +147,20 @@ def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
     xr = x[:, :cin_real].double()
     wr = torch.zeros(cout, cin_real, 3, 3, 3, dtype=torch.float64, requires_grad=True)
     F.conv3d(xr, wr, None, padding=1).backward(dy.double())
-    dw = torch.zeros(cout, cin_real, 3, 3, 3, device=DEV)
-    # kernel's Cin is the stored channel count; the pad channels carry zeros
-    dw_full = torch.zeros(cout, cin, 27, device=DEV)
+    # the stored input may carry zero pad channels (stem: 5 of 8); dw has the weight's Cin
+    guard = 4096
+    dw_full = torch.zeros(cout * cin_real * 27 + guard, device=DEV)
     ws = torch.empty(27 * cout * cin, device=DEV)
     xs = ndhwc(x).to(DEV)
     if c1:
         L.call("pcms_conv3_wgrad", code, ndhwc(x[:, :c0]).to(DEV), c0, ndhwc(x[:, c0:]).to(DEV), c1,
-               ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, 256)
+               ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, cin_real, 256)
     else:
-        L.call("pcms_conv3_wgrad", code, xs, c0, None, 0, ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, 256)
+        L.call("pcms_conv3_wgrad", code, xs, c0, None, 0, ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, cin_real,
+               256)
     torch.cuda.synchronize()
-    got = dw_full.cpu().view(cout, cin, 3, 3, 3)[:, :cin_real]
+    assert dw_full[-guard:].abs().max().item() == 0.0, "wgrad wrote past the weight gradient"
+    got = dw_full[:-guard].cpu().view(cout, cin_real, 3, 3, 3)
     close(got, wr.grad, 1e-4 if code else 2e-5, "wgrad")
 
 
