@@ -251,22 +251,35 @@ __global__ void maxpool_bwd_kernel(const T* a, const T* dp, T* da, int N, int D,
 }
 
 // ---------------- sum over a sub-box of an NDHWC tensor (ConvT bias grad) ----------
+// Block: 256 threads = (256 / CG) voxel lanes x CG groups of VEC channels; 16-byte loads,
+// LDS reduce over voxel lanes, one atomic per channel per block.
 template <typename T>
-__global__ void box_channel_sum_kernel(const T* x, float* out, int N, int D, int H, int W, int C,
-                                       int z0, int y0, int x0, int bd, int bh, int bw) {
-  // one voxel per block iteration, threads over channels (loop for C > 256)
+__global__ void __launch_bounds__(TPB) box_channel_sum_kernel(const T* x, float* out, int N, int D, int H, int W,
+                                                              int C, int z0, int y0, int x0, int bd, int bh, int bw) {
+  constexpr int VEC = Elem<T>::kVec;
+  __shared__ float red[TPB * VEC];
+  const int CG = C / VEC;
+  const int cg = threadIdx.x % CG, vl = threadIdx.x / CG, VL = TPB / CG;
   const long nv = (long)N * bd * bh * bw;
-  for (int cb = 0; cb < C; cb += TPB) {
-    const int c = cb + threadIdx.x;
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  for (long i = (long)blockIdx.x * VL + vl; i < nv; i += (long)gridDim.x * VL) {
+    const int w = i % bw; long r = i / bw;
+    const int h = r % bh; r /= bh;
+    const int d = r % bd; const long n = r / bd;
+    float v[VEC];
+    load16<T>(x + (((n * D + z0 + d) * H + y0 + h) * W + x0 + w) * C + cg * VEC, v);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] += v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) red[vl * C + cg * VEC + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += TPB) {
     float s = 0.f;
-    if (c < C)
-      for (long i = blockIdx.x; i < nv; i += gridDim.x) {
-        const int w = i % bw; long r = i / bw;
-        const int h = r % bh; r /= bh;
-        const int d = r % bd; const long n = r / bd;
-        s += Elem<T>::ld(x + (((n * D + z0 + d) * H + y0 + h) * W + x0 + w) * C + c);
-      }
-    if (c < C) atomicAdd(out + c, s);
+    for (int l = 0; l < VL; ++l) s += red[l * C + c];
+    atomicAdd(out + c, s);
   }
 }
 
@@ -561,8 +574,11 @@ int pcms_maxpool_bwd(int dtype, const void* a, const void* dp, void* da, int N, 
 
 int pcms_box_channel_sum(int dtype, const void* x, float* out, int N, int D, int H, int W, int C,
                          int z0, int y0, int x0, int bd, int bh, int bw, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC || TPB % (C / VEC)) return -1;
   const long nv = (long)N * bd * bh * bw;
-  const int grid = (int)std::min<long>(nv, 1024);
+  const int VL = TPB / (C / VEC);
+  const int grid = grid_for(nv, VL * 8, 1024);
   if (dtype == PCMS_BF16) hipLaunchKernelGGL(box_channel_sum_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)x, out, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
   else hipLaunchKernelGGL(box_channel_sum_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)x, out, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
   PCMS_CHECK_LAUNCH();
