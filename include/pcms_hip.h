@@ -52,9 +52,12 @@ int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0
                         float* stats, int C, long nvox, hipStream_t s);
 
 /* ---- BatchNorm3d (train / eval) + ReLU(inplace): models/unet3d.py:31-39 ----------- */
+/* ws: pcms_bn_ws_doubles(C) fp64 workspace (two-stage fp64 column reduction)           */
+int pcms_bn_ws_doubles(int C);
 int pcms_bn_finalize(const float* part, int rows, int C, double count, const float* gamma,
                      const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
-                     float eps, float* scale, float* shift, float* mean, float* invstd, hipStream_t s);
+                     float eps, float* scale, float* shift, float* mean, float* invstd, double* ws,
+                     hipStream_t s);
 int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                         float eps, int C, float* scale, float* shift, hipStream_t s);
 int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const float* shift, int C,
@@ -63,7 +66,7 @@ int pcms_bn_bwd_rows(int dtype, int C, long nvox);
 /* dy = BN+ReLU backward(da); dgamma/dbeta += ; part: rows*C*2 fp32; coef: 3*C fp32   */
 int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scale, const float* shift,
                      const float* mean, const float* invstd, const float* gamma, float* part, float* coef,
-                     float* dgamma, float* dbeta, void* dy, int C, long nvox, hipStream_t s);
+                     float* dgamma, float* dbeta, void* dy, int C, long nvox, double* ws, hipStream_t s);
 
 /* ---- MaxPool3d(2): models/unet3d.py:80 ------------------------------------------- */
 int pcms_maxpool_fwd(int dtype, const void* a, void* p, int N, int D, int H, int W, int C, hipStream_t s);

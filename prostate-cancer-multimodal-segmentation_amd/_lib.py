@@ -24,11 +24,12 @@ SIGNATURES = {
     "pcms_conv3_wgrad": "ipipipppiiiiiiis",
     "pcms_split_epilogue_rows": "l",
     "pcms_split_epilogue": "ippppipils",
-    "pcms_bn_finalize": "piidpppppffpppps",
+    "pcms_bn_ws_doubles": "i",
+    "pcms_bn_finalize": "piidpppppffppppps",
     "pcms_bn_eval_coeffs": "ppppfipps",
     "pcms_bn_relu": "ippppils",
     "pcms_bn_bwd_rows": "iil",
-    "pcms_bn_relu_bwd": "i" + "p" * 12 + "ils",
+    "pcms_bn_relu_bwd": "i" + "p" * 12 + "ilps",
     "pcms_maxpool_fwd": "ippiiiiis",
     "pcms_maxpool_bwd": "ipppiiiiis",
     "pcms_convt_pack": "ippiiis",

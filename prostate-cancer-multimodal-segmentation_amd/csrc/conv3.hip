@@ -26,6 +26,8 @@ constexpr int kThreads = 256;
 constexpr int kRowBytes = 64;      // one halo row = one LDS row of the current ci-chunk
 constexpr int kHaloMax = 1152;     // halo voxels per workgroup (72 KiB LDS, 2 WG / CU)
 
+__device__ __attribute__((aligned(16))) uint32_t g_zero16[4];  // zero page for LDS-DMA padding
+
 template <typename T> struct Traits;
 template <> struct Traits<bf16_t> {
   static constexpr int CK = 32;    // channels per chunk (64 B rows)
@@ -50,6 +52,19 @@ __device__ __forceinline__ f32x16_t mfma(float a, float b, f32x16_t c) {
 
 // 16-byte slot swizzle inside a 64-byte halo row (spreads ds_read_b128 lane groups).
 __device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+
+// MFMA row -> box voxel permutation inside a 32-row M-tile.  ds_read_b128 serves a wave in
+// the lane groups G0 = {0-3, 12-15, 20-27} and G1 = {4-11, 16-19, 28-31} (and +32).  With
+// 16-voxel w-runs (box width 16) G0 reads 16 consecutive halo rows of one h-row and G1 16 of
+// the next, so with swz() every group covers all 64 banks exactly once, for every tap.
+__device__ __forceinline__ int perm32(int r) {
+  if (r < 4) return r;
+  if (r < 12) return 16 + (r - 4);
+  if (r < 16) return 4 + (r - 12);
+  if (r < 20) return 24 + (r - 16);
+  if (r < 28) return 8 + (r - 20);
+  return 28 + (r - 28);
+}
 
 // A fragment from the halo tile. ks = k-step inside the chunk, h = lane >> 5.
 __device__ __forceinline__ s16x8_t lds_a(const char* lds, int row, int ks, int h, bf16_t*) {
@@ -78,8 +93,8 @@ struct Conv3Params {
   int lbd, lbh, lbw, nbd, nbh, nbw;
 };
 
-template <typename T>
-__global__ void __launch_bounds__(kThreads, 2) conv3_fwd_kernel(Conv3Params p) {
+template <typename T, int MINW>
+__global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p) {
   typedef Traits<T> Tr;
   typedef typename Tr::Frag Frag;
   __shared__ __attribute__((aligned(16))) char lds[kHaloMax * kRowBytes];
@@ -100,23 +115,28 @@ __global__ void __launch_bounds__(kThreads, 2) conv3_fwd_kernel(Conv3Params p) {
   const int HH = bh + 2, HW = bw + 2;
   const int HV = (bd + 2) * HH * HW;
 
+  const bool w16 = p.lbw == 4;
+  const int prow = w16 ? perm32(r_lane) : r_lane;
   int hb[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    int r = wave * 128 + mt * 32 + r_lane;
+    int r = wave * 128 + mt * 32 + prow;
     if (r >= boxvol) r = 0;
     int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
     hb[mt] = (rd * HH + rh) * HW + rw;
   }
   const bool wave_active = wave * 128 < boxvol;
 
-  f32x16_t acc[4][2];
+  // fp32 build: three-level summation (one MFMA chain per tap = 16 products, per-chunk sum,
+  // master) keeps the error at the level of a blocked CPU conv; bf16 build: one chain.
+  constexpr bool kF32 = sizeof(T) == 4;
+  f32x16_t acc[4][2], cacc[4][2], macc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      for (int e = 0; e < 16; ++e) { acc[i][j][e] = 0.f; cacc[i][j][e] = 0.f; macc[i][j][e] = 0.f; }
 
   const T* x0 = (const T*)p.x0;
   const T* x1 = (const T*)p.x1;
@@ -125,20 +145,27 @@ __global__ void __launch_bounds__(kThreads, 2) conv3_fwd_kernel(Conv3Params p) {
 
   for (int chunk = cbeg; chunk < cend; ++chunk) {
     __syncthreads();
-    // ---- stage the halo tile of this chunk: HV rows x 4 pieces of 16 B ----
-    for (int pc = tid; pc < HV * 4; pc += kThreads) {
-      const int hv = pc >> 2, q = pc & 3;
-      const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-      const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
-      const int c = chunk * Tr::CK + q * Tr::VEC;
-      u32x4_t v = {0u, 0u, 0u, 0u};
-      if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
-        const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
-        const T* src = (c < p.c0) ? x0 + vox * p.c0 + c : x1 + vox * p.c1 + (c - p.c0);
-        v = *reinterpret_cast<const u32x4_t*>(src);
+    // ---- stage the halo tile of this chunk by LDS-DMA: piece p (16 B) -> LDS [16p, 16p+16).
+    // The LDS image is lane-linear, so the slot swizzle is applied to the SOURCE address
+    // (physical slot qp of row hv holds logical slot qp ^ swz(hv)); out-of-range pieces
+    // read the zero page.  All pieces are in flight at once (no register staging).
+    for (int base = wave * 64; base < HV * 4; base += kThreads) {
+      const int pc = base + lane;
+      const int hv = pc >> 2;
+      const int ql = (pc & 3) ^ swz(hv);
+      const void* src = g_zero16;
+      if (pc < HV * 4) {
+        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+        const int c = chunk * Tr::CK + ql * Tr::VEC;
+        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
+          const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+          src = (c < p.c0) ? (const void*)(x0 + vox * p.c0 + c) : (const void*)(x1 + vox * p.c1 + (c - p.c0));
+        }
       }
-      *reinterpret_cast<u32x4_t*>(lds + hv * kRowBytes + ((q ^ swz(hv)) * 16)) = v;
+      __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(lds + base * 16), 16, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (!wave_active) continue;
 
@@ -164,6 +191,14 @@ __global__ void __launch_bounds__(kThreads, 2) conv3_fwd_kernel(Conv3Params p) {
       }
       const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
       const int off = (kd * HH + kh) * HW + kw;
+      if constexpr (kF32) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      }
 #pragma unroll
       for (int ks = 0; ks < Tr::KS; ++ks) {
 #pragma unroll
@@ -173,7 +208,29 @@ __global__ void __launch_bounds__(kThreads, 2) conv3_fwd_kernel(Conv3Params p) {
           for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a, bcur[nt][ks], acc[mt][nt]);
         }
       }
+      if constexpr (kF32) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) cacc[i][j] += acc[i][j];
+      }
     }
+    if constexpr (kF32) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          macc[i][j] += cacc[i][j];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) cacc[i][j][e] = 0.f;
+        }
+    }
+  }
+  if constexpr (kF32) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = macc[i][j];
   }
 
   // ---- epilogue ----
@@ -183,7 +240,8 @@ __global__ void __launch_bounds__(kThreads, 2) conv3_fwd_kernel(Conv3Params p) {
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int r = wave * 128 + mt * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+        const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
         if (r >= boxvol) continue;
         const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
         const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
@@ -317,7 +375,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // register staging: pieces of 16 B
   constexpr int DYP = Tr::BV * Tr::DYROW / 16;
   const int XP = HV * Tr::XROW / 16;
-  constexpr int MAXP = (DYP + kWHaloMax * Tr::XROW / 16 + kWThreads - 1) / kWThreads;
+  constexpr int MAXP = Tr::NBUF == 2 ? (DYP + kWHaloMax * Tr::XROW / 16 + kWThreads - 1) / kWThreads : 1;
   u32x4_t stg[MAXP];
 
   auto box_origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
@@ -373,6 +431,41 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         const int hp = pc - DYP;
         *reinterpret_cast<u32x4_t*>(buf + DYBYTES + hp * 16) = stg[i];
       }
+    }
+  };
+
+  // fp32 build: stage without a register array (one 16-B piece in flight per thread)
+  auto stage_direct = [&](char* buf, int b) {
+    int n, d0, h0, w0;
+    box_origin(b, n, d0, h0, w0);
+    for (int pc = tid; pc < DYP + XP; pc += kWThreads) {
+      u32x4_t v = {0u, 0u, 0u, 0u};
+      int off;
+      if (pc < DYP) {
+        const int r = pc / (Tr::DYROW / 16), q = pc % (Tr::DYROW / 16);
+        off = r * Tr::DYROW + q * 16;
+        if (r < boxvol) {
+          const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+          const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+          if (gd < p.D && gh < p.H && gw < p.W) {
+            const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+            v = *reinterpret_cast<const u32x4_t*>(dy + vox * p.Cout + co_base + q * Tr::VEC);
+          }
+        }
+      } else {
+        const int hp = pc - DYP;
+        off = DYBYTES + hp * 16;
+        const int hv = hp / (Tr::XROW / 16), q = hp % (Tr::XROW / 16);
+        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+        const int c = ci_base + q * Tr::VEC;
+        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
+          const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+          const T* src = (c < p.c0) ? x0 + vox * p.c0 + c : x1 + vox * p.c1 + (c - p.c0);
+          v = *reinterpret_cast<const u32x4_t*>(src);
+        }
+      }
+      *reinterpret_cast<u32x4_t*>(buf + off) = v;
     }
   };
 
@@ -441,13 +534,26 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         __syncthreads();
       }
     } else {
+      // fp32 build: per-box MFMA chains summed into a master accumulator (two-level sum)
+      f32x16_t macc[7];
+#pragma unroll
+      for (int t = 0; t < 7; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) macc[t][e] = 0.f;
       for (int b = b_beg; b < b_end; ++b) {
-        stage_load(b);
         __syncthreads();
-        stage_store(wlds);
+        stage_direct(wlds, b);
         __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 7; ++t)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
         compute(wlds);
+#pragma unroll
+        for (int t = 0; t < 7; ++t) macc[t] += acc[t];
       }
+#pragma unroll
+      for (int t = 0; t < 7; ++t) acc[t] = macc[t];
     }
   }
 
@@ -481,21 +587,31 @@ __global__ void wgrad_permute_kernel(const float* dwt, float* dw, int Cout, int 
 // master fp32 W[Cout][Cin][27] -> packed T [chunk][27][J][CK]
 //   fwd  (flip=0): J = Cout, k-index = ci
 //   dgrad(flip=1): J = Cin,  k-index = co, tap mirrored (26 - t)
+// One block per (chunk, 8 consecutive j): the 8 x CK x 27 source block is read with unit
+// stride into LDS and written back with unit stride in the packed order.
 template <typename T, int CK>
-__global__ void pack_conv3_kernel(const float* w, T* out, int Cout, int Cin, int flip, int nchunk) {
+__global__ void __launch_bounds__(256) pack_conv3_kernel(const float* w, T* out, int Cout, int Cin, int flip) {
+  __shared__ float tile[8][CK][27];
   const int J = flip ? Cin : Cout;
   const int Kdim = flip ? Cout : Cin;
-  const long total = (long)nchunk * 27 * J * CK;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int k = i % CK;
-    long r = i / CK;
-    const int j = r % J; r /= J;
-    const int t = r % 27;
-    const int chunk = r / 27;
-    const int kk = chunk * CK + k;
+  const int chunk = blockIdx.y;
+  const int j0 = blockIdx.x * 8;
+  constexpr int E = 8 * CK * 27;
+  for (int e = threadIdx.x; e < E; e += 256) {
+    int jj, k, t;
+    if (!flip) { t = e % 27; k = (e / 27) % CK; jj = e / (27 * CK); }      // w[j][chunk*CK + k][t]
+    else { t = e % 27; jj = (e / 27) % 8; k = e / (27 * 8); }             // w[chunk*CK + k][j][t]
+    const int kk = chunk * CK + k, j = j0 + jj;
     float v = 0.f;
-    if (kk < Kdim) v = flip ? w[((long)kk * Cin + j) * 27 + (26 - t)] : w[((long)j * Cin + kk) * 27 + t];
-    out[i] = Elem<T>::cvt(v);
+    if (kk < Kdim && j < J) v = flip ? w[((long)kk * Cin + j) * 27 + t] : w[((long)j * Cin + kk) * 27 + t];
+    tile[jj][k][t] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < E; e += 256) {
+    const int k = e % CK, jj = (e / CK) % 8, t = e / (CK * 8);
+    if (j0 + jj >= J) continue;
+    const float v = flip ? tile[jj][k][26 - t] : tile[jj][k][t];
+    out[(((long)chunk * 27 + t) * J + j0 + jj) * CK + k] = Elem<T>::cvt(v);
   }
 }
 
@@ -523,6 +639,24 @@ Box choose_box(int D, int H, int W, int maxvol, int maxhalo, int minw, int minvo
   return best;
 }
 
+// Forward/dgrad box: 512 voxels; width 16 whenever the grid is that wide (perm32 layout).
+Box fwd_box(int D, int H, int W) {
+  if (W >= 16) {
+    Box best{0, 0, 4};
+    double bc = 1e30;
+    for (int a = 0; a <= 5; ++a) {
+      const int b = 5 - a;  // bd * bh = 32
+      const int bd = 1 << a, bh = 1 << b;
+      if ((bd + 2) * (bh + 2) * 18 > kHaloMax) continue;
+      const double cost = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh +
+                          0.15 * cdiv(D, bd) * cdiv(H, bh) * (bd + 2) * (bh + 2) * 18 / 16.0;
+      if (cost < bc) { bc = cost; best = Box{a, b, 4}; }
+    }
+    return best;
+  }
+  return choose_box(D, H, W, 512, kHaloMax, 4, 32);
+}
+
 }  // namespace
 
 extern "C" {
@@ -530,7 +664,7 @@ extern "C" {
 // Returns the m-block count (workgroups along M) the fwd launch will use for a grid;
 // callers size the BatchNorm partial buffer [mblocks][Cout][2] from it.
 int pcms_conv3_mblocks(int N, int D, int H, int W) {
-  Box b = choose_box(D, H, W, 512, kHaloMax, 4, 32);
+  Box b = fwd_box(D, H, W);
   return N * cdiv(D, 1 << b.lbd) * cdiv(H, 1 << b.lbh) * cdiv(W, 1 << b.lbw);
 }
 
@@ -538,14 +672,13 @@ int pcms_conv3_chunk(int dtype) { return dtype == PCMS_BF16 ? Traits<bf16_t>::CK
 
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s) {
   const int CK = pcms_conv3_chunk(dtype);
+  const int J = flip ? Cin : Cout;
   const int Kdim = flip ? Cout : Cin;
-  const int nchunk = cdiv(Kdim, CK);
-  const long total = (long)nchunk * 27 * (flip ? Cin : Cout) * CK;
-  const int grid = (int)std::min<long>(4096, (total + 255) / 256);
+  dim3 grid(cdiv(J, 8), cdiv(Kdim, CK));
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL((pack_conv3_kernel<bf16_t, 32>), dim3(grid), dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip, nchunk);
+    hipLaunchKernelGGL((pack_conv3_kernel<bf16_t, 32>), grid, dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip);
   else
-    hipLaunchKernelGGL((pack_conv3_kernel<float, 16>), dim3(grid), dim3(256), 0, s, w, (float*)out, Cout, Cin, flip, nchunk);
+    hipLaunchKernelGGL((pack_conv3_kernel<float, 16>), grid, dim3(256), 0, s, w, (float*)out, Cout, Cin, flip);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -561,7 +694,7 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0 || (c1 > 0 && x1 == nullptr)) return -1;
   if (y1 == nullptr) cy0 = Cout;
   if (cy0 % 64 != 0 && cy0 != Cout) return -2;
-  Box b = choose_box(D, H, W, 512, kHaloMax, 4, 32);
+  Box b = fwd_box(D, H, W);
   Conv3Params p;
   p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1;
   p.w = wpack; p.bias = bias; p.y0 = y0; p.y1 = y1; p.cy0 = cy0;
@@ -579,9 +712,9 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   if (splits > 1) p.yacc = yacc;
   dim3 grid(N * p.nbd * p.nbh * p.nbw, Cout / 64, splits);
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL(conv3_fwd_kernel<bf16_t>, grid, dim3(kThreads), 0, s, p);
+    hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2>), grid, dim3(kThreads), 0, s, p);
   else
-    hipLaunchKernelGGL(conv3_fwd_kernel<float>, grid, dim3(kThreads), 0, s, p);
+    hipLaunchKernelGGL((conv3_fwd_kernel<float, 1>), grid, dim3(kThreads), 0, s, p);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -94,8 +94,8 @@ __global__ void __launch_bounds__(256) convt_dgrad_kernel(const T* dout, const T
   const int K = 8 * Cout;
   const T* b0 = wd + (long)(q0 + r) * K;
   const T* b1 = wd + (long)(q0 + 32 + r) * K;
-  f32x16_t acc0, acc1;
-  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  f32x16_t acc0, acc1, s0, s1;
+  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; s0[e] = 0.f; s1[e] = 0.f; }
   for (int t = 0; t < 8; ++t) {
     const T* arow = dout + child_vox(g, ma, t) * Cout;
     for (int k = 0; k < Cout; k += GT<T>::KS) {
@@ -103,7 +103,12 @@ __global__ void __launch_bounds__(256) convt_dgrad_kernel(const T* dout, const T
       acc0 = mfma(a, ldfrag(b0 + t * Cout + k, h), acc0);
       acc1 = mfma(a, ldfrag(b1 + t * Cout + k, h), acc1);
     }
+    if constexpr (sizeof(T) == 4) {  // fp32 build: one chain per tap, summed (two-level)
+      s0 += acc0; s1 += acc1;
+      for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+    }
   }
+  if constexpr (sizeof(T) == 4) { acc0 = s0; acc1 = s1; }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -140,9 +145,13 @@ __global__ void __launch_bounds__(256) convt_wgrad_kernel(const T* x, const T* d
   const long vend = std::min<long>(M, vbeg + vox_per_split);
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int PPR = 64 / VEC;       // pieces per row
-  f32x16_t acc;
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  f32x16_t acc, macc;
+  for (int e = 0; e < 16; ++e) { acc[e] = 0.f; macc[e] = 0.f; }
   for (long vb = vbeg; vb < vend; vb += kVB) {
+    if constexpr (sizeof(T) == 4) {  // fp32 build: per-block chains summed (two-level)
+      macc += acc;
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    }
     __syncthreads();
     for (int pc = tid; pc < 2 * kVB * PPR; pc += 256) {
       const int which = pc / (kVB * PPR), rem = pc % (kVB * PPR);
@@ -178,6 +187,7 @@ __global__ void __launch_bounds__(256) convt_wgrad_kernel(const T* x, const T* d
       }
     }
   }
+  if constexpr (sizeof(T) == 4) acc += macc;
   // C[row = ci][col = co]; ws layout [Cin][8][Cout]
 #pragma unroll
   for (int e = 0; e < 16; ++e) {

@@ -36,42 +36,57 @@ __global__ void pack_input_kernel(const float* in, T* out, int N, int Cin, long 
 }
 
 // ---------------- BatchNorm statistics ----------------
-// partial rows -> mean/invstd/scale/shift (+ running stats when training)
-// block: 1024 threads = 16 row-groups x 64 channels
-__global__ void __launch_bounds__(1024) bn_finalize_kernel(
-    const float* part, int rows, int C, double count, const float* gamma, const float* beta,
-    float* rmean, float* rvar, long long* nbt, float momentum, float eps,
-    float* scale, float* shift, float* mean_out, float* invstd_out) {
-  __shared__ double red[16][64][2];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+// Stage 1: fp32 partial rows [rows][C][2] -> fp64 column sums [RB][C][2] (RB row groups).
+// block = 256 threads = 4 row lanes x 64 channels; grid = (ceil(C / 64), RB).
+constexpr int kRB = 64;
+__global__ void __launch_bounds__(256) colsum2_kernel(const float* part, int rows, int C, double* out) {
+  __shared__ double red[4][64][2];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
   if (c < C)
-    for (int r = rg; r < rows; r += 16) {
-      s1 += (double)part[((long)r * C + c) * 2];
-      s2 += (double)part[((long)r * C + c) * 2 + 1];
+    for (int r = blockIdx.y * 4 + rl; r < rows; r += kRB * 4) {
+      const float2 v = *reinterpret_cast<const float2*>(part + ((long)r * C + c) * 2);
+      s1 += (double)v.x;
+      s2 += (double)v.y;
     }
-  red[rg][cl][0] = s1;
-  red[rg][cl][1] = s2;
+  red[rl][cl][0] = s1;
+  red[rl][cl][1] = s2;
   __syncthreads();
-  if (rg == 0 && c < C) {
-    for (int g = 1; g < 16; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
-    const double mean = s1 / count;
-    double var = s2 / count - mean * mean;
-    if (var < 0) var = 0;
-    const double inv = 1.0 / sqrt(var + (double)eps);
-    const float sc = (float)((double)gamma[c] * inv);
-    scale[c] = sc;
-    shift[c] = (float)((double)beta[c] - mean * (double)gamma[c] * inv);
-    mean_out[c] = (float)mean;
-    invstd_out[c] = (float)inv;
-    if (rmean) {
-      const double unb = count > 1 ? var * count / (count - 1) : var;
-      rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mean);
-      rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
-    }
+  if (rl == 0 && c < C) {
+    for (int g = 1; g < 4; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
+    out[((long)blockIdx.y * C + c) * 2] = s1;
+    out[((long)blockIdx.y * C + c) * 2 + 1] = s2;
   }
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+__device__ __forceinline__ void colsum_final(const double* ws, int C, int c, double& s1, double& s2) {
+  s1 = 0.0; s2 = 0.0;
+  for (int r = 0; r < kRB; ++r) { s1 += ws[((long)r * C + c) * 2]; s2 += ws[((long)r * C + c) * 2 + 1]; }
+}
+
+// Stage 2: -> mean/invstd/scale/shift (+ running stats when training)
+__global__ void bn_finalize_kernel(const double* ws, int C, double count, const float* gamma, const float* beta,
+                                   float* rmean, float* rvar, long long* nbt, float momentum, float eps,
+                                   float* scale, float* shift, float* mean_out, float* invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nbt && c == 0) *nbt += 1;
+  if (c >= C) return;
+  double s1, s2;
+  colsum_final(ws, C, c, s1, s2);
+  const double mean = s1 / count;
+  double var = s2 / count - mean * mean;
+  if (var < 0) var = 0;
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  scale[c] = (float)((double)gamma[c] * inv);
+  shift[c] = (float)((double)beta[c] - mean * (double)gamma[c] * inv);
+  mean_out[c] = (float)mean;
+  invstd_out[c] = (float)inv;
+  if (rmean) {
+    const double unb = count > 1 ? var * count / (count - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+  }
 }
 
 __global__ void bn_eval_coeffs_kernel(const float* gamma, const float* beta, const float* rmean,
@@ -83,17 +98,24 @@ __global__ void bn_eval_coeffs_kernel(const float* gamma, const float* beta, con
   shift[c] = (float)((double)beta[c] - (double)rmean[c] * (double)gamma[c] * inv);
 }
 
-// a = relu(y * scale[c] + shift[c]); 16-byte vectors
+// a = relu(y * scale[c] + shift[c]); 16-byte vectors.  Block = (256 / CG) voxel lanes x
+// CG channel groups, so every thread keeps its VEC channels' coefficients in registers.
 template <typename T>
-__global__ void bn_relu_kernel(const T* y, T* a, const float* scale, const float* shift, int C, long nvec) {
+__global__ void __launch_bounds__(TPB) bn_relu_kernel(const T* y, T* a, const float* scale, const float* shift,
+                                                      int C, long nvox) {
   constexpr int VEC = Elem<T>::kVec;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * VEC) % C);
-    float v[VEC];
-    load16<T>(y + i * VEC, v);
+  const int CG = C / VEC;
+  const int cg = threadIdx.x % CG, vl = threadIdx.x / CG, VL = TPB / CG;
+  const int c0 = cg * VEC;
+  float sc[VEC], sh[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) v[j] = fmaxf(v[j] * scale[c0 + j] + shift[c0 + j], 0.f);
-    store16<T>(a + i * VEC, v);
+  for (int j = 0; j < VEC; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+  for (long v = (long)blockIdx.x * VL + vl; v < nvox; v += (long)gridDim.x * VL) {
+    float x[VEC];
+    load16<T>(y + v * C + c0, x);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) x[j] = fmaxf(x[j] * sc[j] + sh[j], 0.f);
+    store16<T>(a + v * C + c0, x);
   }
 }
 
@@ -139,52 +161,47 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_reduce_kernel(
   }
 }
 
-// pass 2: reduce partials; dgamma/dbeta (+=) and the apply coefficients
+// pass 2: fp64 column sums -> dgamma/dbeta (+=) and the apply coefficients
 //   dy = k1*g + k2*xhat + k3, k1 = gamma*invstd, k2 = -k1*sum(g xhat)/M, k3 = -k1*sum(g)/M
-__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(
-    const float* part, int rows, int C, double count, const float* gamma, const float* invstd,
-    float* dgamma, float* dbeta, float* coef) {
-  __shared__ double red[16][64][2];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C)
-    for (int r = rg; r < rows; r += 16) {
-      s1 += (double)part[((long)r * C + c) * 2];
-      s2 += (double)part[((long)r * C + c) * 2 + 1];
-    }
-  red[rg][cl][0] = s1;
-  red[rg][cl][1] = s2;
-  __syncthreads();
-  if (rg == 0 && c < C) {
-    for (int g = 1; g < 16; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
-    dbeta[c] += (float)s1;
-    dgamma[c] += (float)s2;
-    const double k1 = (double)gamma[c] * (double)invstd[c];
-    coef[c * 3 + 0] = (float)k1;
-    coef[c * 3 + 1] = (float)(-k1 * s2 / count);
-    coef[c * 3 + 2] = (float)(-k1 * s1 / count);
-  }
+__global__ void bn_bwd_finalize_kernel(const double* ws, int C, double count, const float* gamma,
+                                       const float* invstd, float* dgamma, float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1, s2;
+  colsum_final(ws, C, c, s1, s2);
+  dbeta[c] += (float)s1;
+  dgamma[c] += (float)s2;
+  const double k1 = (double)gamma[c] * (double)invstd[c];
+  coef[c * 3 + 0] = (float)k1;
+  coef[c * 3 + 1] = (float)(-k1 * s2 / count);
+  coef[c * 3 + 2] = (float)(-k1 * s1 / count);
 }
 
 template <typename T>
-__global__ void bn_relu_bwd_apply_kernel(const T* da, const T* y, const float* scale, const float* shift,
-                                         const float* mean, const float* invstd, const float* coef,
-                                         T* dy, int C, long nvec) {
+__global__ void __launch_bounds__(TPB) bn_relu_bwd_apply_kernel(
+    const T* da, const T* y, const float* scale, const float* shift, const float* mean, const float* invstd,
+    const float* coef, T* dy, int C, long nvox) {
   constexpr int VEC = Elem<T>::kVec;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * VEC) % C);
+  const int CG = C / VEC;
+  const int cg = threadIdx.x % CG, vl = threadIdx.x / CG, VL = TPB / CG;
+  const int c0 = cg * VEC;
+  float sc[VEC], sh[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], k3[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    const int c = c0 + j;
+    sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
+    k1[j] = coef[c * 3]; k2[j] = coef[c * 3 + 1]; k3[j] = coef[c * 3 + 2];
+  }
+  for (long v = (long)blockIdx.x * VL + vl; v < nvox; v += (long)gridDim.x * VL) {
     float dv[VEC], yv[VEC], o[VEC];
-    load16<T>(da + i * VEC, dv);
-    load16<T>(y + i * VEC, yv);
+    load16<T>(da + v * C + c0, dv);
+    load16<T>(y + v * C + c0, yv);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      const int c = c0 + j;
-      const float g = (yv[j] * scale[c] + shift[c] > 0.f) ? dv[j] : 0.f;
-      const float xh = (yv[j] - mean[c]) * invstd[c];
-      o[j] = coef[c * 3] * g + coef[c * 3 + 1] * xh + coef[c * 3 + 2];
+      const float g = (yv[j] * sc[j] + sh[j] > 0.f) ? dv[j] : 0.f;
+      o[j] = k1[j] * g + k2[j] * ((yv[j] - mu[j]) * is[j]) + k3[j];
     }
-    store16<T>(dy + i * VEC, o);
+    store16<T>(dy + v * C + c0, o);
   }
 }
 
@@ -498,11 +515,16 @@ int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long 
 
 int pcms_bn_finalize(const float* part, int rows, int C, double count, const float* gamma, const float* beta,
                      float* rmean, float* rvar, long long* nbt, float momentum, float eps,
-                     float* scale, float* shift, float* mean, float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, s, part, rows, C, count, gamma, beta,
-                     rmean, rvar, nbt, momentum, eps, scale, shift, mean, invstd);
+                     float* scale, float* shift, float* mean, float* invstd, double* ws, hipStream_t s) {
+  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, part, rows, C, ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, s, (const double*)ws, C, count, gamma,
+                     beta, rmean, rvar, nbt, momentum, eps, scale, shift, mean, invstd);
   PCMS_CHECK_LAUNCH();
 }
+
+int pcms_bn_ws_doubles(int C) { return kRB * C * 2; }
 
 int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
                         int C, float* scale, float* shift, hipStream_t s) {
@@ -510,14 +532,19 @@ int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmea
   PCMS_CHECK_LAUNCH();
 }
 
+static int ew_grid(int dtype, int C, long nvox) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  const int VL = TPB / (C / VEC);
+  return grid_for(nvox, VL * 4, 8192);
+}
+
 int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const float* shift, int C, long nvox,
                  hipStream_t s) {
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
-  if (C % VEC) return -1;
-  const long nvec = nvox * C / VEC;
-  const int grid = grid_for(nvec, TPB);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(bn_relu_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, (bf16_t*)a, scale, shift, C, nvec);
-  else hipLaunchKernelGGL(bn_relu_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)y, (float*)a, scale, shift, C, nvec);
+  if (C % VEC || TPB % (C / VEC)) return -1;
+  const int grid = ew_grid(dtype, C, nvox);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(bn_relu_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, (bf16_t*)a, scale, shift, C, nvox);
+  else hipLaunchKernelGGL(bn_relu_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)y, (float*)a, scale, shift, C, nvox);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -530,7 +557,7 @@ int pcms_bn_bwd_rows(int dtype, int C, long nvox) {
 
 int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scale, const float* shift,
                      const float* mean, const float* invstd, const float* gamma, float* part, float* coef,
-                     float* dgamma, float* dbeta, void* dy, int C, long nvox, hipStream_t s) {
+                     float* dgamma, float* dbeta, void* dy, int C, long nvox, double* ws, hipStream_t s) {
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || (TPB % (C / VEC)) != 0) return -1;
   const int rows = pcms_bn_bwd_rows(dtype, C, nvox);
@@ -540,16 +567,18 @@ int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scal
     hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<float>, dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, s, (const float*)part, rows, C,
-                     (double)nvox, gamma, invstd, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C, ws);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const long nvec = nvox * C / VEC;
-  const int grid = grid_for(nvec, TPB);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, s, (const double*)ws, C, (double)nvox,
+                     gamma, invstd, dgamma, dbeta, coef);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int grid = ew_grid(dtype, C, nvox);
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, (const float*)coef, (bf16_t*)dy, C, nvec);
+    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, (const float*)coef, (bf16_t*)dy, C, nvox);
   else
-    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, (const float*)coef, (float*)dy, C, nvec);
+    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, (const float*)coef, (float*)dy, C, nvox);
   PCMS_CHECK_LAUNCH();
 }
 

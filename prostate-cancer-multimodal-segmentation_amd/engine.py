@@ -242,6 +242,7 @@ class UNetEngine:
         rows_b = max(query("pcms_bn_bwd_rows", self.code, C[l], nv[l]) for l in range(5))
         b["stats"] = torch.empty(max(rows_f, rows_s, rows_b) * 1024 * 2, dtype=torch.float32, device=dev)
         b["coef"] = torch.empty(3 * 1024, dtype=torch.float32, device=dev)
+        b["bnws"] = torch.empty(query("pcms_bn_ws_doubles", 1024), dtype=torch.float64, device=dev)
         b["dwt"] = torch.empty(27 * 1024 * 1024, dtype=torch.float32, device=dev)
         # split-K accumulators only where a level can be split (few workgroups along M)
         split_lv = [l for l in range(5) if query("pcms_conv3_mblocks", N, *S[l]) * (C[l] // 64) < 192]
@@ -283,7 +284,7 @@ class UNetEngine:
                                  f"torch.Size([{N}, {bn.c}, {S[0]}, {S[1]}, {S[2]}])")
             call("pcms_bn_finalize", st, rows, bn.c, float(nvox), m.weight, m.bias, m.running_mean,
                  m.running_var, m.num_batches_tracked, BN_MOMENTUM, BN_EPS, bn.scale, bn.shift, bn.mean,
-                 bn.invstd)
+                 bn.invstd, b["bnws"])
         else:
             call("pcms_bn_eval_coeffs", m.weight, m.bias, m.running_mean, m.running_var, BN_EPS, bn.c,
                  bn.scale, bn.shift)
@@ -361,7 +362,7 @@ class UNetEngine:
         b = self.bufs
         m = bn.mod
         call("pcms_bn_relu_bwd", self.code, ga, y, bn.scale, bn.shift, bn.mean, bn.invstd, m.weight,
-             b["stats"], b["coef"], m.weight.grad, m.bias.grad, gy, bn.c, nvox)
+             b["stats"], b["coef"], m.weight.grad, m.bias.grad, gy, bn.c, nvox, b["bnws"])
 
     def _dgrad(self, cs: ConvSpec, gy, out0, out1, cy0, N, S):
         b = self.bufs

@@ -186,8 +186,9 @@ def test_bn_relu_fwd_bwd(dt, code, tol):
     rmd, rvd = rm.clone().to(DEV), rv.clone().to(DEV)
     nbt = torch.zeros((), dtype=torch.int64, device=DEV)
     scale, shift, mean, invstd = (torch.empty(C, device=DEV) for _ in range(4))
+    ws = torch.empty(L.query("pcms_bn_ws_doubles", C), dtype=torch.float64, device=DEV)
     L.call("pcms_bn_finalize", part.to(DEV), nvox, C, float(nvox), gd, bd, rmd, rvd, nbt, 0.1, 1e-5,
-           scale, shift, mean, invstd)
+           scale, shift, mean, invstd, ws)
     yd = ndhwc(y).to(DEV)
     a = torch.empty_like(yd)
     L.call("pcms_bn_relu", code, yd, a, scale, shift, C, nvox)
@@ -197,7 +198,7 @@ def test_bn_relu_fwd_bwd(dt, code, tol):
     dgam, dbet = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
     dy = torch.empty_like(yd)
     L.call("pcms_bn_relu_bwd", code, ndhwc(da).to(DEV), yd, scale, shift, mean, invstd, gd, bpart, coef,
-           dgam, dbet, dy, C, nvox)
+           dgam, dbet, dy, C, nvox, ws)
     torch.cuda.synchronize()
     assert int(nbt) == 1
     close(rmd.cpu(), rm_r, 1e-5, "running_mean")

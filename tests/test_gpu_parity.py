@@ -19,7 +19,7 @@ from tests import golden_util as gu
 pytestmark = pytest.mark.gpu
 
 PRE_BN_BIAS = ("conv.0.bias", "conv.3.bias")  # exact grad 0, reference has noise
-GRAD_RL2 = {"c16_bcedice": 3e-2, "cfg1_dice": 5e-3, "odd_bcedice": 3e-2, "c16_ncls2_dice": 3e-2}
+GRAD_RL2 = {"c16_bcedice": 5e-2, "cfg1_dice": 5e-3, "odd_bcedice": 5e-2, "c16_ncls2_dice": 5e-2}
 
 
 def _build(name, precision):
@@ -65,7 +65,7 @@ def test_fp32_parity_full_step(name):
     # 2-32 values per channel at the bottleneck, small Dice denominators), and a ReLU mask or
     # max-pool argmax decided by a 1e-6 difference reroutes a whole gradient element.  Bar
     # (relative L2 vs the fp64 truth): within 10x the fp32 reference's own error, or within
-    # GRAD_RL2[name] (5e-3 for the config-1 shape, 3e-2 for the 2-values-per-channel cases).
+    # GRAD_RL2[name] (5e-3 for the config-1 shape, 5e-2 for the 2-values-per-channel cases).
     conf = {}
     for k, p in m.named_parameters():
         got = gu.sampled(p.grad, g["g_stride__" + k]).astype(np.float64)
