@@ -170,49 +170,49 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     if (!wave_active) continue;
 
     const T* wchunk = wp + (long)chunk * 27 * p.Cout * Tr::CK;
-    Frag bcur[2][Tr::KS], bnxt[2][Tr::KS];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int ks = 0; ks < Tr::KS; ++ks)
-        bnxt[nt][ks] = gl_b(wchunk + (long)(co_base + nt * 32 + r_lane) * Tr::CK, ks, hsel);
-
-    for (int tap = 0; tap < 27; ++tap) {
+    // B fragments rotate through 3 register sets: the loads of tap t+2 are issued while
+    // tap t computes (kw unrolled, so every set index is a compile-time constant).
+    Frag bset[3][2][Tr::KS];
+    auto load_b = [&](Frag (&dst)[2][Tr::KS], int tap) {
+      const T* wt = wchunk + ((long)tap * p.Cout + co_base + r_lane) * Tr::CK;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int ks = 0; ks < Tr::KS; ++ks) bcur[nt][ks] = bnxt[nt][ks];
-      if (tap + 1 < 27) {
-        const T* wt = wchunk + ((long)(tap + 1) * p.Cout + co_base + r_lane) * Tr::CK;
+        for (int ks = 0; ks < Tr::KS; ++ks) dst[nt][ks] = gl_b(wt + nt * 32 * Tr::CK, ks, hsel);
+    };
+    load_b(bset[0], 0);
+    load_b(bset[1], 1);
+    for (int kdh = 0; kdh < 9; ++kdh) {
+      const int kd = kdh / 3, kh = kdh % 3;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kdh * 3 + kw;
+        if (tap + 2 < 27) load_b(bset[(kw + 2) % 3], tap + 2);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
+        const int off = (kd * HH + kh) * HW + kw;
+        if constexpr (kF32) {
 #pragma unroll
-          for (int ks = 0; ks < Tr::KS; ++ks) bnxt[nt][ks] = gl_b(wt + nt * 32 * Tr::CK, ks, hsel);
-      }
-      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-      const int off = (kd * HH + kh) * HW + kw;
-      if constexpr (kF32) {
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-      }
-#pragma unroll
-      for (int ks = 0; ks < Tr::KS; ++ks) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          Frag a = lds_a(lds, hb[mt] + off, ks, hsel, (T*)nullptr);
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a, bcur[nt][ks], acc[mt][nt]);
+              for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
         }
-      }
-      if constexpr (kF32) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int ks = 0; ks < Tr::KS; ++ks) {
 #pragma unroll
-          for (int j = 0; j < 2; ++j) cacc[i][j] += acc[i][j];
+          for (int mt = 0; mt < 4; ++mt) {
+            Frag a = lds_a(lds, hb[mt] + off, ks, hsel, (T*)nullptr);
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a, bset[kw][nt][ks], acc[mt][nt]);
+          }
+        }
+        if constexpr (kF32) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) cacc[i][j] += acc[i][j];
+        }
       }
     }
     if constexpr (kF32) {
@@ -235,7 +235,50 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
 
   // ---- epilogue ----
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
-  if (wave_active) {
+  float bias_l[2] = {0.f, 0.f};
+  if (p.bias) {
+    bias_l[0] = p.bias[co_base + r_lane];
+    bias_l[1] = p.bias[co_base + 32 + r_lane];
+  }
+  constexpr int kRedOff = 512 * 64 * 2;  // bf16 C tile [512][64] occupies the first 64 KiB
+  if (!kF32 && !p.yacc && !p.accumulate) {
+    // bf16 fast path: + bias, stats from the fp32 values, C tile -> LDS (box order), then
+    // 16-byte coalesced stores (one box row = a contiguous w-run of voxels).
+    __syncthreads();  // every wave is done reading the halo
+    bf16_t* ct = reinterpret_cast<bf16_t*>(lds);
+    if (wave_active) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+          const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
+          bool valid = r < boxvol;
+          if (valid) {
+            const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+            valid = d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
+          }
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const float v = acc[mt][nt][e] + bias_l[nt];
+            ct[r * 64 + nt * 32 + r_lane] = f2bf(v);
+            if (valid) { s1[nt] += v; s2[nt] += v * v; }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int pc = tid; pc < boxvol * 8; pc += kThreads) {
+      const int r = pc >> 3, q = pc & 7;
+      const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+      const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+      if (gd >= p.D || gh >= p.H || gw >= p.W) continue;
+      const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+      const int co = co_base + q * 8;
+      T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
+      *reinterpret_cast<u32x4_t*>(dst) = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
+    }
+  } else if (wave_active) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -255,7 +298,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
             atomicAdd(p.yacc + vox * p.Cout + co, v);
             continue;
           }
-          if (p.bias) v += p.bias[co];
+          v += bias_l[nt];
           T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co
                                 : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
           if (p.accumulate) v += Elem<T>::ld(dst);
@@ -267,8 +310,8 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     }
   }
   if (p.stats && !p.yacc) {
-    __syncthreads();  // halo no longer read: reuse LDS for the cross-wave reduction
-    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();  // halo / C tile no longer read: reuse LDS for the cross-wave reduction
+    float* red = reinterpret_cast<float*>(lds + (kF32 ? 0 : kRedOff));
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       s1[nt] += __shfl_xor(s1[nt], 32, 64);

@@ -81,6 +81,12 @@ def main():
                            N, D, H, W, cout, 1)
             t = timeit(f, a.reps)
             out.append(f"fwd {t * 1e6:8.1f}us {flop / t / 1e12:7.1f}TF")
+        if only and "fwdplain" in only:
+            def f(i):
+                L.call("pcms_conv3_fwd", code, xs[i], cin, None, 0, wf, None, ys[i], None, cout, None, None, 0,
+                       N, D, H, W, cout, 1)
+            t = timeit(f, a.reps)
+            out.append(f"fwd(no bias/stats) {t * 1e6:8.1f}us {flop / t / 1e12:7.1f}TF")
         if not only or "dgrad" in only:
             splits = 1 if l < 3 else 4
             def f(i):
