@@ -62,12 +62,20 @@ def stem_roofline(tr, N, spatial, reps):
     dw = torch.zeros(64 * 5 * 27, device="cuda")
     dwt = torch.empty(27 * 64 * eng.cp, device="cuda")
 
+    eng._ensure_packs()
+
     def fwd(s):
-        L.call("pcms_conv3_fwd", code, s[0], eng.cp, None, 0, cs.fwd, cs.mod.bias, s[1], None, 64, None, stats,
-               0, N, D, H, W, 64, 1)
+        if eng.stem_fast:
+            L.call("pcms_stem_fwd", s[0], eng.stem_pack, cs.mod.bias, s[1], stats, N, D, H, W)
+        else:
+            L.call("pcms_conv3_fwd", code, s[0], eng.cp, None, 0, cs.fwd, cs.mod.bias, s[1], None, 64, None,
+                   stats, 0, N, D, H, W, 64, 1)
 
     def wgrad(s):
-        L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
+        if eng.stem_fast:
+            L.call("pcms_stem_wgrad", s[0], s[2], dw, 5, N, D, H, W, 256)
+        else:
+            L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
 
     res = {}
     for name, fn in (("fwd", fwd), ("wgrad", wgrad)):
@@ -91,7 +99,7 @@ def stem_roofline(tr, N, spatial, reps):
     achieved = (fwd_bytes + wg_bytes) / t
     return {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
-            "kernel": "stem conv3d 5->64 fwd + wgrad (conv3_fwd_kernel + conv3_wgrad_kernel)",
+            "kernel": "stem conv3d 5->64 fwd + wgrad (stem_fwd_kernel + stem_wgrad_kernel)",
             "algorithmic_bytes": fwd_bytes + wg_bytes, "t_fwd_us": round(res["fwd"] * 1e6, 1),
             "t_wgrad_us": round(res["wgrad"] * 1e6, 1)}
 

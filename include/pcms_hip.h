@@ -47,6 +47,14 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, hipStream_t s);
+/* Stem (inc.conv.0, bf16 build): input stored with 8 channels (n_modalities <= 8).
+ * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32).                  */
+int pcms_stem_pack_elems(void);
+int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
+int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
+                  int N, int D, int H, int W, hipStream_t s);
+int pcms_stem_wgrad(const void* x, const void* dy, float* dw, int cin_w, int N, int D, int H, int W,
+                    int target_wgs, hipStream_t s);
 int pcms_split_epilogue_rows(long nvox);
 int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0,
                         float* stats, int C, long nvox, hipStream_t s);

@@ -22,6 +22,10 @@ SIGNATURES = {
     "pcms_conv3_pack": "ippiiis",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
     "pcms_conv3_wgrad": "ipipipppiiiiiiis",
+    "pcms_stem_pack_elems": "",
+    "pcms_stem_pack": "ppis",
+    "pcms_stem_fwd": "pppppiiiis",
+    "pcms_stem_wgrad": "pppiiiiiis",
     "pcms_split_epilogue_rows": "l",
     "pcms_split_epilogue": "ippppipils",
     "pcms_bn_ws_doubles": "i",

@@ -700,6 +700,305 @@ Box fwd_box(int D, int H, int W) {
   return choose_box(D, H, W, 512, kHaloMax, 4, 32);
 }
 
+// ------------------------------------------------------------------------------------
+// Stem conv (inc.conv.0: n_modalities -> 64, input stored with 8 channels), bf16.
+// The generic kernel would spend 4x its MFMA work on zero channels (K = 27 x 32); here the
+// K dimension packs two taps per MFMA k-step: k = (tap 2s + h, channel c), h = lane >> 5,
+// so K = 14 x 16 = 224 (135 real).  HBM-bound: 16 B in + 128 B out per voxel.
+// ------------------------------------------------------------------------------------
+constexpr int kStemSteps = 14;                    // 28 taps (27 + 1 zero) / 2
+constexpr int kStemWBytes = kStemSteps * 64 * 16 * 2;  // packed weights [14][64][16] bf16
+
+// master W[64][cin_w][27] fp32 -> [14][64][16] bf16, k = h * 8 + c <-> (tap 2s + h, c)
+__global__ void stem_pack_kernel(const float* w, bf16_t* out, int cin_w) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kStemSteps * 64 * 16) return;
+  const int k = i & 15, co = (i >> 4) & 63, s = i >> 10;
+  const int tap = 2 * s + (k >> 3), c = k & 7;
+  float v = 0.f;
+  if (tap < 27 && c < cin_w) v = w[((long)co * cin_w + c) * 27 + tap];
+  out[i] = f2bf(v);
+}
+
+__device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
+  if (tap >= 27) return 0;  // zero-weight pad tap: any in-halo row
+  const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+  return (kd * HH + kh) * HW + kw;
+}
+
+__global__ void __launch_bounds__(kThreads, 2) stem_fwd_kernel(Conv3Params p) {
+  // LDS: [weights 28 KiB][halo 18 KiB]; the epilogue reuses it as the 64 KiB C tile
+  __shared__ __attribute__((aligned(16))) char lds[512 * 64 * 2 + 2048];
+  char* wl = lds;
+  char* hl = lds + kStemWBytes;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r_lane = lane & 31, hsel = lane >> 5;
+  int mb = blockIdx.x;
+  const int bwi = mb % p.nbw; mb /= p.nbw;
+  const int bhi = mb % p.nbh; mb /= p.nbh;
+  const int bdi = mb % p.nbd;
+  const int n = mb / p.nbd;
+  const int bd = 1 << p.lbd, bh = 1 << p.lbh, bw = 1 << p.lbw;
+  const int boxvol = bd * bh * bw;
+  const int d0 = bdi * bd, h0 = bhi * bh, w0 = bwi * bw;
+  const int HH = bh + 2, HW = bw + 2;
+  const int HV = (bd + 2) * HH * HW;
+  const long plane = (long)p.H * p.W;
+  const bf16_t* x0 = (const bf16_t*)p.x0;
+  const bool w16 = p.lbw == 4;
+  const int prow = w16 ? perm32(r_lane) : r_lane;
+  int hb[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    int r = wave * 128 + mt * 32 + prow;
+    if (r >= boxvol) r = 0;
+    const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+    hb[mt] = (rd * HH + rh) * HW + rw;
+  }
+  const bool wave_active = wave * 128 < boxvol;
+  // ---- stage weights (linear copy) and the 8-channel halo (16 B per row) by LDS-DMA ----
+  for (int base = wave * 64; base < kStemWBytes / 16; base += kThreads)
+    __builtin_amdgcn_global_load_lds((const char*)p.w + (base + lane) * 16, (LDS_AS void*)(wl + base * 16), 16, 0, 0);
+  for (int base = wave * 64; base < HV; base += kThreads) {
+    const int hv = base + lane;
+    const void* src = g_zero16;
+    if (hv < HV) {
+      const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+      const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+      if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W)
+        src = x0 + (((long)n * p.D + gd) * plane + (long)gh * p.W + gw) * 8;
+    }
+    __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(hl + base * 16), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x16_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  if (wave_active) {
+#pragma unroll 2
+    for (int st = 0; st < kStemSteps; ++st) {
+      const int off = tap_off(2 * st + hsel, HH, HW);
+      s16x8_t b0 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + r_lane) * 16 + hsel * 8) * 2);
+      s16x8_t b1 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + 32 + r_lane) * 16 + hsel * 8) * 2);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        s16x8_t a = *reinterpret_cast<const s16x8_t*>(hl + (hb[mt] + off) * 16);
+        acc[mt][0] = mfma(a, b0, acc[mt][0]);
+        acc[mt][1] = mfma(a, b1, acc[mt][1]);
+      }
+    }
+  }
+  // ---- epilogue (as conv3_fwd_kernel's bf16 path) ----
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  float bias_l[2] = {0.f, 0.f};
+  if (p.bias) { bias_l[0] = p.bias[r_lane]; bias_l[1] = p.bias[32 + r_lane]; }
+  __syncthreads();
+  bf16_t* ct = reinterpret_cast<bf16_t*>(lds);
+  if (wave_active) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+        const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
+        bool valid = r < boxvol;
+        if (valid) {
+          const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+          valid = d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const float v = acc[mt][nt][e] + bias_l[nt];
+          ct[r * 64 + nt * 32 + r_lane] = f2bf(v);
+          if (valid) { s1[nt] += v; s2[nt] += v * v; }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int pc = tid; pc < boxvol * 8; pc += kThreads) {
+    const int r = pc >> 3, q = pc & 7;
+    const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+    const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+    if (gd >= p.D || gh >= p.H || gw >= p.W) continue;
+    const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
+    *reinterpret_cast<u32x4_t*>((bf16_t*)p.y0 + vox * 64 + q * 8) = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
+  }
+  if (p.stats) {
+    float* red = reinterpret_cast<float*>(lds + 512 * 64 * 2);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      s1[nt] += __shfl_xor(s1[nt], 32, 64);
+      s2[nt] += __shfl_xor(s2[nt], 32, 64);
+      if (hsel == 0) {
+        red[(wave * 64 + nt * 32 + r_lane) * 2 + 0] = s1[nt];
+        red[(wave * 64 + nt * 32 + r_lane) * 2 + 1] = s2[nt];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) { a += red[(w * 64 + tid) * 2]; b += red[(w * 64 + tid) * 2 + 1]; }
+      float* stp = p.stats + ((long)blockIdx.x * 64 + tid) * 2;
+      stp[0] = a;
+      stp[1] = b;
+    }
+  }
+}
+
+// Stem weight gradient.  dW[co][c][t] = sum_v dy[v][co] * x[v + t][c], c < cin_w <= 8.
+// Output columns j = (t, c) = 8 t + c, 224 of them in 7 tiles of 32 (= 4 taps x 8 channels).
+// Wave w: both co tiles (64 co), column tiles {w, w + 4} (w < 3) or {3}.  Voxel boxes of
+// 256 are double-buffered through LDS (register-staged prefetch); one atomic flush per WG.
+constexpr int kSBV = 256;
+constexpr int kSHalo = 648;                         // (4+2)(4+2)(16+2) for the 4x4x16 box
+constexpr int kSBuf = kSBV * 128 + kSHalo * 16;     // dy tile (128 B rows) + halo (16 B rows)
+
+__global__ void __launch_bounds__(256, 1) stem_wgrad_kernel(const bf16_t* x, const bf16_t* dy, float* dw,
+                                                            int N, int D, int H, int W, int cin_w,
+                                                            int lbd, int lbh, int lbw, int nbd, int nbh, int nbw,
+                                                            int nbox, int boxes_per_split) {
+  extern __shared__ __attribute__((aligned(16))) char slds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hsel = lane >> 5;
+  const int bd = 1 << lbd, bh = 1 << lbh, bw = 1 << lbw;
+  const int HH = bh + 2, HW = bw + 2;
+  const int HV = (bd + 2) * HH * HW;
+  const int boxvol = bd * bh * bw;
+  const long plane = (long)H * W;
+  const int nj = (wave < 3) ? 2 : 1;
+  const int jt0 = wave, jt1 = wave + 4;
+  const int b_beg = blockIdx.x * boxes_per_split;
+  const int b_end = min(nbox, b_beg + boxes_per_split);
+  f32x16_t acc[2][2];  // [co tile][column tile slot]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  constexpr int DYP = kSBV * 8;                      // 16-B pieces of the dy tile
+  constexpr int MAXP = (DYP + kSHalo + 255) / 256;  // per thread
+  u32x4_t stg[MAXP];
+  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    int bwi = b % nbw; b /= nbw;
+    int bhi = b % nbh; b /= nbh;
+    int bdi = b % nbd;
+    n = b / nbd;
+    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
+  };
+  auto stage_load = [&](int b) {
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int pc = tid + i * 256;
+      u32x4_t v = {0u, 0u, 0u, 0u};
+      if (pc < DYP) {
+        const int r = pc >> 3, q = pc & 7;
+        if (r < boxvol) {
+          const int rd = r >> (lbh + lbw), rh = (r >> lbw) & (bh - 1), rw = r & (bw - 1);
+          const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+          if (gd < D && gh < H && gw < W)
+            v = *reinterpret_cast<const u32x4_t*>(dy + (((long)n * D + gd) * plane + (long)gh * W + gw) * 64 + q * 8);
+        }
+      } else if (pc < DYP + HV) {
+        const int hv = pc - DYP;
+        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+        if (gd >= 0 && gd < D && gh >= 0 && gh < H && gw >= 0 && gw < W)
+          v = *reinterpret_cast<const u32x4_t*>(x + (((long)n * D + gd) * plane + (long)gh * W + gw) * 8);
+      }
+      stg[i] = v;
+    }
+  };
+  auto stage_store = [&](char* buf) {
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int pc = tid + i * 256;
+      if (pc < DYP) {
+        const int r = pc >> 3, q = pc & 7;
+        *reinterpret_cast<u32x4_t*>(buf + dy_off_bf16(r, q * 8)) = stg[i];
+      } else if (pc < DYP + HV) {
+        *reinterpret_cast<u32x4_t*>(buf + kSBV * 128 + (pc - DYP) * 16) = stg[i];
+      }
+    }
+  };
+  auto halo_row = [&](int r) {
+    const int rd = r >> (lbh + lbw), rh = (r >> lbw) & (bh - 1), rw = r & (bw - 1);
+    return (rd * HH + rh) * HW + rw;
+  };
+  // per-lane column -> (tap, channel half) for the transposed B reads: in a 16-lane group
+  // lane 4q+p supplies row q and columns 4p..4p+3 of its 16-column block
+  const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+  auto compute = [&](const char* buf) {
+    const char* xb = buf + kSBV * 128;
+    for (int k0 = 0; k0 < boxvol; k0 += 16) {
+      const int v_a = k0 + 8 * hsel + qq;
+      s16x8_t a[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const int co = ct * 32 + g * 16 + pp * 4;
+        s16x4_t lo = tr_read(buf, dy_off_bf16(v_a, co)), hi = tr_read(buf, dy_off_bf16(v_a + 4, co));
+        a[ct] = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int hr0 = halo_row(v_a), hr1 = halo_row(v_a + 4);
+#pragma unroll
+      for (int js = 0; js < 2; ++js) {
+        if (js >= nj) break;
+        const int jt = js ? jt1 : jt0;
+        // column block of this lane group: 16 columns = taps 4 jt + 2 g, +1; lane: tap + (pp >> 1), ch 4 (pp & 1)
+        const int tap = 4 * jt + 2 * g + (pp >> 1);
+        const int off = tap_off(tap, HH, HW);
+        const int cb = (pp & 1) * 8;  // byte offset of channels 4..7
+        s16x4_t lo = tr_read(xb, (hr0 + off) * 16 + cb), hi = tr_read(xb, (hr1 + off) * 16 + cb);
+        s16x8_t bfr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct][js] = mfma(a[ct], bfr, acc[ct][js]);
+      }
+    }
+  };
+  if (b_beg < b_end) {
+    stage_load(b_beg);
+    stage_store(slds);
+    __syncthreads();
+    for (int b = b_beg; b < b_end; ++b) {
+      const int cur = (b - b_beg) & 1;
+      if (b + 1 < b_end) stage_load(b + 1);
+      compute(slds + cur * kSBuf);
+      if (b + 1 < b_end) stage_store(slds + (cur ^ 1) * kSBuf);
+      __syncthreads();
+    }
+  }
+  // flush: C tile -> LDS [co][t][c] (fp32), then coalesced atomics into dw[co][c][t]
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(slds);  // 64 x 28 x 8 floats = 56 KiB
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int js = 0; js < 2; ++js) {
+      if (js >= nj) continue;
+      const int jt = js ? jt1 : jt0;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+        const int j = jt * 32 + (lane & 31);  // column = 8 t + c
+        red[co * 224 + j] = acc[ct][js][e];
+      }
+    }
+  __syncthreads();
+  const int total = 64 * cin_w * 27;
+  for (int i = tid; i < total; i += 256) {
+    const int t = i % 27, c = (i / 27) % cin_w, co = i / (27 * cin_w);
+    atomicAdd(dw + i, red[co * 224 + t * 8 + c]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -758,6 +1057,49 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
     hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2>), grid, dim3(kThreads), 0, s, p);
   else
     hipLaunchKernelGGL((conv3_fwd_kernel<float, 1>), grid, dim3(kThreads), 0, s, p);
+  PCMS_CHECK_LAUNCH();
+}
+
+
+// ---- stem (inc.conv.0), bf16: dedicated HBM-bound kernels ----
+int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s) {
+  if (cin_w > 8) return -1;
+  hipLaunchKernelGGL(stem_pack_kernel, dim3(cdiv(kStemSteps * 64 * 16, 256)), dim3(256), 0, s, w, (bf16_t*)out, cin_w);
+  PCMS_CHECK_LAUNCH();
+}
+int pcms_stem_pack_elems(void) { return kStemSteps * 64 * 16; }
+
+// x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_conv3_mblocks
+int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
+                  int N, int D, int H, int W, hipStream_t s) {
+  Box b = fwd_box(D, H, W);
+  Conv3Params p;
+  p.x0 = x; p.x1 = nullptr; p.c0 = 8; p.c1 = 0;
+  p.w = wpack; p.bias = bias; p.y0 = y; p.y1 = nullptr; p.cy0 = 64;
+  p.yacc = nullptr; p.stats = stats; p.accumulate = 0;
+  p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = 8; p.Cout = 64;
+  p.nchunk = 1; p.chunks_per_split = 1;
+  p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
+  p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
+  hipLaunchKernelGGL(stem_fwd_kernel, dim3(N * p.nbd * p.nbh * p.nbw), dim3(kThreads), 0, s, p);
+  PCMS_CHECK_LAUNCH();
+}
+
+// dw [64][cin_w][27] fp32 += stem weight gradient (x: 8-channel bf16 input, dy: 64 ch)
+int pcms_stem_wgrad(const void* x, const void* dy, float* dw, int cin_w, int N, int D, int H, int W,
+                    int target_wgs, hipStream_t s) {
+  if (cin_w > 8) return -1;
+  Box b = choose_box(D, H, W, kSBV, kSHalo, 4, 16);
+  const int nbd = cdiv(D, 1 << b.lbd), nbh = cdiv(H, 1 << b.lbh), nbw = cdiv(W, 1 << b.lbw);
+  const int nbox = N * nbd * nbh * nbw;
+  if (target_wgs <= 0) target_wgs = 256;
+  int splits = std::max(1, std::min(nbox, target_wgs));
+  const int bps = cdiv(nbox, splits);
+  splits = cdiv(nbox, bps);
+  const size_t lds = 2 * (size_t)kSBuf;
+  (void)hipFuncSetAttribute((const void*)stem_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(splits), dim3(256), lds, s, (const bf16_t*)x, (const bf16_t*)dy, dw,
+                     N, D, H, W, cin_w, b.lbd, b.lbh, b.lbw, nbd, nbh, nbw, nbox, bps);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -96,6 +96,9 @@ class UNetEngine:
             self.convs += [b.c0, b.c1]
             self.bns += [b.b0, b.b1]
         self.convt_packs: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+        # bf16 build: the stem runs on dedicated tap-packed kernels (HBM-bound)
+        self.stem_fast = self.code == BF16 and self.cp == 8
+        self.stem_pack = None
         self._flat_ptrs = None
         self._packed_version = -1
         self._dirty = True
@@ -184,6 +187,10 @@ class UNetEngine:
             call("pcms_conv3_pack", self.code, w, cs.fwd, cs.cout, cs.cin, 0)
             if cs.dgrad is not None:
                 call("pcms_conv3_pack", self.code, w, cs.dgrad, cs.cout, cs.cin, 1)
+        if self.stem_fast:
+            if self.stem_pack is None:
+                self.stem_pack = torch.empty(query("pcms_stem_pack_elems"), dtype=self.tdtype, device=self.device)
+            call("pcms_stem_pack", self.convs[0].mod.weight, self.stem_pack, self.nmod)
         for i, up in enumerate(self.ups):
             cin, cout = up.in_channels, up.out_channels
             if i not in self.convt_packs:
@@ -266,7 +273,10 @@ class UNetEngine:
         nvox = N * S[0] * S[1] * S[2]
         splits = self._splits(N, S, c0 + c1, cs.cout)
         st = b["stats"] if training else None
-        if splits == 1:
+        if cs is self.convs[0] and self.stem_fast:
+            call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2])
+            rows = query("pcms_conv3_mblocks", N, *S)
+        elif splits == 1:
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
             rows = query("pcms_conv3_mblocks", N, *S)
@@ -353,8 +363,11 @@ class UNetEngine:
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
         # BN0/ReLU backward -> dy1 (reuse gY)
         self._bn_bwd(blk.b0, gA, acts["y1"], gY, nvox)
-        call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gY, blk.c0.mod.weight.grad, b["dwt"], N, *S,
-             blk.c0.cout, blk.c0.cin, self.wgrad_target)
+        if blk is self.enc[0] and self.stem_fast:
+            call("pcms_stem_wgrad", x0, gY, blk.c0.mod.weight.grad, blk.c0.cin, N, *S, 256)
+        else:
+            call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gY, blk.c0.mod.weight.grad, b["dwt"], N, *S,
+                 blk.c0.cout, blk.c0.cin, self.wgrad_target)
         if gx_out0 is not None:
             self._dgrad(blk.c0, gY, gx_out0, gx_out1, cy0, N, S)
 

@@ -17,7 +17,7 @@ def _prototypes():
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     protos = {}
     for m in re.finditer(r"\bint\s+(pcms_\w+)\s*\(([^)]*)\)\s*;", src):
-        protos[m.group(1)] = [a.strip() for a in m.group(2).split(",") if a.strip()]
+        protos[m.group(1)] = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
     return protos
 
 

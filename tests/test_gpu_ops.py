@@ -362,3 +362,38 @@ def test_pack_input(dt, code):
     exp = torch.zeros(2, 3, 4, 5, 8)
     exp[..., :5] = ndhwc(x)
     close(out.cpu(), exp.to(dt), 0, "pack input")
+
+
+@pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (1, (9, 10, 11)), (2, (8, 8, 4)), (1, (6, 20, 33))])
+def test_stem_fwd_wgrad_bf16(N, S):
+    """Dedicated stem kernels (tap-pair packed K) vs torch conv3d on the bf16-rounded input."""
+    L = _lib()
+    g = torch.Generator().manual_seed(sum(S))
+    x = torch.rand(N, 5, *S, generator=g).to(torch.bfloat16)
+    w = (torch.randn(64, 5, 3, 3, 3, generator=g) * 0.2)
+    b = torch.randn(64, generator=g)
+    xs = torch.zeros(N, 8, *S, dtype=torch.bfloat16)
+    xs[:, :5] = x
+    xd = ndhwc(xs).to(DEV)
+    wp = torch.empty(L.query("pcms_stem_pack_elems"), dtype=torch.bfloat16, device=DEV)
+    L.call("pcms_stem_pack", w.to(DEV), wp, 5)
+    y = torch.empty(N, *S, 64, dtype=torch.bfloat16, device=DEV)
+    rows = L.query("pcms_conv3_mblocks", N, *S)
+    stats = torch.zeros(rows * 64 * 2, device=DEV)
+    L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y, stats, N, *S)
+    xr = x.double()
+    wr = w.to(torch.bfloat16).double().requires_grad_(True)
+    ref = F.conv3d(xr, wr, b.double(), padding=1)
+    dy = torch.randn(ref.shape, generator=g).to(torch.bfloat16)
+    ref.backward(dy.double())
+    guard = 4096
+    dw = torch.zeros(64 * 5 * 27 + guard, device=DEV)
+    L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, 5, N, *S, 64)
+    torch.cuda.synchronize()
+    close(ncdhw(y.cpu()), ref.detach(), 1e-2, "stem fwd")
+    st = stats.cpu().view(rows, 64, 2).double().sum(0)
+    yr = ref.detach().transpose(0, 1).reshape(64, -1)
+    close(st[:, 0], yr.sum(1), 1e-3, "stem stats sum")
+    close(st[:, 1], (yr * yr).sum(1), 1e-3, "stem stats sumsq")
+    assert dw[-guard:].abs().max().item() == 0.0
+    close(dw[:-guard].cpu().view(64, 5, 3, 3, 3), wr.grad, 1e-4, "stem wgrad")
