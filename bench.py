@@ -58,7 +58,7 @@ def stem_roofline(tr, N, spatial, reps):
         dy = torch.randn(nvox * 64, device="cuda").to(T)
         sets.append((xin, y, dy))
     rows = L.query("pcms_conv3_mblocks", N, D, H, W)
-    stats = torch.empty(rows * 64 * 2, device="cuda")
+    stats = torch.empty(rows * (64 * 2 + 1), device="cuda")
     dw = torch.zeros(64 * 5 * 27, device="cuda")
     dwt = torch.empty(27 * 64 * eng.cp, device="cuda")
 

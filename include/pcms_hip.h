@@ -35,7 +35,9 @@ int pcms_conv3_mblocks(int N, int D, int H, int W);/* rows of the BN partial buf
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s);
 /* Y = conv(X) + bias, X = channel-concat(x0[:, :c0], x1[:, :c1]) (Up3D cat, :156),
  * output channels [0, cy0) -> y0, [cy0, Cout) -> y1 (dgrad concat split).
- * stats: [mblocks][Cout][2] fp32 BN partials (sum, sumsq) or NULL.  splits > 1: fp32
+ * stats: BN partials or NULL: [mblocks][Cout][2] fp32 (sum, M2 = sum of squared
+ * deviations from the row's own mean) followed by [mblocks] fp32 row voxel counts
+ * (numerically stable moments; consumed by pcms_bn_finalize).  splits > 1: fp32
  * atomic accumulation into the zeroed yacc [Nvox][Cout]; finish with
  * pcms_split_epilogue.  Also used for dgrad with the flip pack.                      */
 int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
@@ -55,12 +57,15 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
                   int N, int D, int H, int W, hipStream_t s);
 int pcms_stem_wgrad(const void* x, const void* dy, float* dw, int cin_w, int N, int D, int H, int W,
                     int target_wgs, hipStream_t s);
+/* stats layout as pcms_conv3_fwd with rows = pcms_split_epilogue_rows(nvox)              */
 int pcms_split_epilogue_rows(long nvox);
 int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0,
                         float* stats, int C, long nvox, hipStream_t s);
 
 /* ---- BatchNorm3d (train / eval) + ReLU(inplace): models/unet3d.py:31-39 ----------- */
-/* ws: pcms_bn_ws_doubles(C) fp64 workspace (two-stage fp64 column reduction)           */
+/* part: the [rows][C][2] (sum, M2) partials + [rows] counts written by the conv / stem /
+ * split-epilogue kernels; ws: pcms_bn_ws_doubles(C) fp64 workspace (two-stage fp64
+ * column reduction, rows merged with Chan's parallel-variance formula)                  */
 int pcms_bn_ws_doubles(int C);
 int pcms_bn_finalize(const float* part, int rows, int C, double count, const float* gamma,
                      const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,

@@ -10,7 +10,7 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpcms_hip.so")
+LIB_PATH = os.environ.get("PCMS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpcms_hip.so")
 
 F32, BF16 = 0, 1
 

@@ -93,8 +93,11 @@ struct Conv3Params {
   int lbd, lbh, lbw, nbd, nbh, nbw;
 };
 
-template <typename T, int MINW>
+// LBD/LBH/LBW >= 0: compile-time box geometry (the hot (4, 8, 16) box: halo decode and tap
+// offsets become constant arithmetic); -1: runtime geometry from p.
+template <typename T, int MINW, int LBD, int LBH, int LBW>
 __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p) {
+  const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   typedef Traits<T> Tr;
   typedef typename Tr::Frag Frag;
   __shared__ __attribute__((aligned(16))) char lds[kHaloMax * kRowBytes];
@@ -109,20 +112,20 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
   const int co_base = blockIdx.y * 64;
   const int cbeg = blockIdx.z * p.chunks_per_split;
   const int cend = min(p.nchunk, cbeg + p.chunks_per_split);
-  const int bd = 1 << p.lbd, bh = 1 << p.lbh, bw = 1 << p.lbw;
+  const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
   const int boxvol = bd * bh * bw;
   const int d0 = bdi * bd, h0 = bhi * bh, w0 = bwi * bw;
   const int HH = bh + 2, HW = bw + 2;
   const int HV = (bd + 2) * HH * HW;
 
-  const bool w16 = p.lbw == 4;
+  const bool w16 = lbw_ == 4;
   const int prow = w16 ? perm32(r_lane) : r_lane;
   int hb[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
     int r = wave * 128 + mt * 32 + prow;
     if (r >= boxvol) r = 0;
-    int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+    int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
     hb[mt] = (rd * HH + rh) * HW + rw;
   }
   const bool wave_active = wave * 128 < boxvol;
@@ -234,11 +237,33 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
   }
 
   // ---- epilogue ----
+  // BatchNorm partials per workgroup row: (sum, M2 = sum of squared deviations from the
+  // row's own mean) + the row's voxel count.  Each wave first forms its own per-channel
+  // mean (two passes over the accumulator registers), waves are merged with Chan's formula:
+  // no E[x^2] - E[x]^2 cancellation (BN over few voxels / large |mean| / std).
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
   float bias_l[2] = {0.f, 0.f};
   if (p.bias) {
     bias_l[0] = p.bias[co_base + r_lane];
     bias_l[1] = p.bias[co_base + 32 + r_lane];
+  }
+  const bool want_stats = p.stats && !p.yacc;
+  const bool interior = d0 + bd <= p.D && h0 + bh <= p.H && w0 + bw <= p.W;
+  uint64_t vmask = 0;  // bit mt * 16 + e: row valid
+  if (wave_active) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+        const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
+        bool valid = r < boxvol;
+        if (valid && !interior) {
+          const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+          valid = d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
+        }
+        if (valid) vmask |= 1ull << (mt * 16 + e);
+      }
   }
   constexpr int kRedOff = 512 * 64 * 2;  // bf16 C tile [512][64] occupies the first 64 KiB
   if (!kF32 && !p.yacc && !p.accumulate) {
@@ -253,16 +278,12 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
         for (int e = 0; e < 16; ++e) {
           const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
           const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
-          bool valid = r < boxvol;
-          if (valid) {
-            const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
-            valid = d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
-          }
+          const bool valid = (vmask >> (mt * 16 + e)) & 1;
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
             const float v = acc[mt][nt][e] + bias_l[nt];
             ct[r * 64 + nt * 32 + r_lane] = f2bf(v);
-            if (valid) { s1[nt] += v; s2[nt] += v * v; }
+            if (valid) s1[nt] += v;
           }
         }
       }
@@ -270,9 +291,9 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     __syncthreads();
     for (int pc = tid; pc < boxvol * 8; pc += kThreads) {
       const int r = pc >> 3, q = pc & 7;
-      const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+      const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
       const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
-      if (gd >= p.D || gh >= p.H || gw >= p.W) continue;
+      if (!interior && (gd >= p.D || gh >= p.H || gw >= p.W)) continue;
       const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
       const int co = co_base + q * 8;
       T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
@@ -283,12 +304,11 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
+        if (!((vmask >> (mt * 16 + e)) & 1)) continue;
         const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
         const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
-        if (r >= boxvol) continue;
-        const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+        const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
         const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
-        if (gd >= p.D || gh >= p.H || gw >= p.W) continue;
         const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
@@ -301,37 +321,69 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
           v += bias_l[nt];
           T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co
                                 : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
-          if (p.accumulate) v += Elem<T>::ld(dst);
+          if (p.accumulate) v += Elem<T>::ld(dst);  // (stats are refused with accumulate)
           Elem<T>::st(dst, v);
           s1[nt] += v;
-          s2[nt] += v * v;
         }
       }
     }
   }
-  if (p.stats && !p.yacc) {
+  if (want_stats) {
+    // wave-level mean per channel (rows of a channel live in lanes r_lane and r_lane + 32)
+    const float nw = (float)(__popcll(vmask) + __shfl_xor(__popcll(vmask), 32, 64));
+    float mw[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      s1[nt] += __shfl_xor(s1[nt], 32, 64);
+      mw[nt] = nw > 0.f ? s1[nt] / nw : 0.f;
+    }
+    if (wave_active) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          if (!((vmask >> (mt * 16 + e)) & 1)) continue;
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const float d = acc[mt][nt][e] + bias_l[nt] - mw[nt];
+            s2[nt] += d * d;
+          }
+        }
+    }
     __syncthreads();  // halo / C tile no longer read: reuse LDS for the cross-wave reduction
     float* red = reinterpret_cast<float*>(lds + (kF32 ? 0 : kRedOff));
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
-      s1[nt] += __shfl_xor(s1[nt], 32, 64);
       s2[nt] += __shfl_xor(s2[nt], 32, 64);
       if (hsel == 0) {
-        red[(wave * 64 + nt * 32 + r_lane) * 2 + 0] = s1[nt];
-        red[(wave * 64 + nt * 32 + r_lane) * 2 + 1] = s2[nt];
+        float* rp = red + (wave * 64 + nt * 32 + r_lane) * 3;
+        rp[0] = s1[nt];
+        rp[1] = s2[nt];
+        rp[2] = nw;
       }
     }
     __syncthreads();
     if (tid < 64) {
-      float a = 0.f, b = 0.f;
+      float S = 0.f, Nn = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        a += red[(w * 64 + tid) * 2 + 0];
-        b += red[(w * 64 + tid) * 2 + 1];
+        S += red[(w * 64 + tid) * 3 + 0];
+        Nn += red[(w * 64 + tid) * 3 + 2];
+      }
+      const float m = Nn > 0.f ? S / Nn : 0.f;
+      float M2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float c = red[(w * 64 + tid) * 3 + 2];
+        if (c > 0.f) {
+          const float d = red[(w * 64 + tid) * 3 + 0] / c - m;
+          M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+        }
       }
       float* st = p.stats + ((long)blockIdx.x * p.Cout + co_base + tid) * 2;
-      st[0] = a;
-      st[1] = b;
+      st[0] = S;
+      st[1] = M2;
+      if (tid == 0 && blockIdx.y == 0) p.stats[(long)gridDim.x * p.Cout * 2 + blockIdx.x] = Nn;
     }
   }
 }
@@ -381,8 +433,9 @@ __device__ __forceinline__ s16x4_t tr_read(const char* lds, int byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + byte_off));
 }
 
-template <typename T>
+template <typename T, int LBD, int LBH, int LBW>
 __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p) {
+  const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   typedef WTraits<T> Tr;
   typedef typename Tr::Frag Frag;
   constexpr int DYBYTES = Tr::BV * Tr::DYROW;
@@ -397,7 +450,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   const int ntap = (tg == 3) ? 6 : 7;
   const int co_base = blockIdx.y * 64;
   const int ci_base = blockIdx.z * 32;
-  const int bd = 1 << p.lbd, bh = 1 << p.lbh, bw = 1 << p.lbw;
+  const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
   const int HH = bh + 2, HW = bw + 2;
   const int HV = (bd + 2) * HH * HW;
   const int boxvol = bd * bh * bw;
@@ -438,7 +491,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       if (pc < DYP) {
         const int r = pc / (Tr::DYROW / 16), q = pc % (Tr::DYROW / 16);
         if (r < boxvol) {
-          const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+          const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
           const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
           if (gd < p.D && gh < p.H && gw < p.W) {
             const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
@@ -488,7 +541,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         const int r = pc / (Tr::DYROW / 16), q = pc % (Tr::DYROW / 16);
         off = r * Tr::DYROW + q * 16;
         if (r < boxvol) {
-          const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+          const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
           const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
           if (gd < p.D && gh < p.H && gw < p.W) {
             const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
@@ -514,12 +567,13 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
 
   // per-lane voxel-row helpers for the k index (voxel inside the box)
   auto halo_row = [&](int r) {
-    const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+    const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
     return (rd * HH + rh) * HW + rw;
   };
 
   auto compute = [&](const char* buf) {
     const char* xb = buf + DYBYTES;
+#pragma unroll 2
     for (int k0 = 0; k0 < boxvol; k0 += Tr::KV) {
       Frag a;
       Frag bf[7];
@@ -531,7 +585,9 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         s16x4_t lo = tr_read(buf, dy_off_bf16(v_a, co));
         s16x4_t hi = tr_read(buf, dy_off_bf16(v_a + 4, co));
         a = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const int hr0 = halo_row(v_a), hr1 = halo_row(v_a + 4);
+        // with a compile-time box of width >= 16 the lane's rows share (rd, rh) with k0
+        const int hr0 = LBW >= 4 ? halo_row(k0) + 8 * hsel + qq : halo_row(v_a);
+        const int hr1 = LBW >= 4 ? hr0 + 4 : halo_row(v_a + 4);
         const int ci = g * 16 + pp * 4;
 #pragma unroll
         for (int j = 0; j < 7; ++j) {
@@ -693,7 +749,7 @@ Box fwd_box(int D, int H, int W) {
       if ((bd + 2) * (bh + 2) * 18 > kHaloMax) continue;
       const double cost = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh +
                           0.15 * cdiv(D, bd) * cdiv(H, bh) * (bd + 2) * (bh + 2) * 18 / 16.0;
-      if (cost < bc) { bc = cost; best = Box{a, b, 4}; }
+      if (cost < bc - 1e-9 || (cost < bc + 1e-9 && a == 2)) { bc = cost; best = Box{a, b, 4}; }
     }
     return best;
   }
@@ -726,129 +782,196 @@ __device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
   return (kd * HH + kh) * HW + kw;
 }
 
-__global__ void __launch_bounds__(kThreads, 2) stem_fwd_kernel(Conv3Params p) {
-  // LDS: [weights 28 KiB][halo 18 KiB]; the epilogue reuses it as the 64 KiB C tile
-  __shared__ __attribute__((aligned(16))) char lds[512 * 64 * 2 + 2048];
+// Persistent stem forward: one 8-wave workgroup per CU walks boxes b = blockIdx.x,
+// b += gridDim.x.  LDS: weights (loaded once) | halo x2 (LDS-DMA, next box prefetched while
+// the current one computes) | bf16 C tile (16-B coalesced stores).  Every thread issues
+// exactly kStemStores stores per box (invalid ones go to a sink), so the next halo's DMA,
+// issued before them, is retired by s_waitcnt vmcnt(kStemStores).
+constexpr int kStemThreads = 512;
+constexpr int kStemHaloBytes = kHaloMax * 16;                 // 18 KiB
+constexpr int kStemCtOff = kStemWBytes + 2 * kStemHaloBytes;   // C tile offset
+constexpr int kStemLds = kStemCtOff + 512 * 64 * 2 + 6144;     // + stats reduction [8][64][3]
+constexpr int kStemStores = 512 * 8 / kStemThreads;            // 16-B stores per thread per box
+__device__ __attribute__((aligned(16))) uint32_t g_sink[4 * 512];
+
+template <int LBD, int LBH, int LBW>
+__global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p, int nbox) {
+  const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   char* wl = lds;
-  char* hl = lds + kStemWBytes;
+  bf16_t* ct = reinterpret_cast<bf16_t*>(lds + kStemCtOff);
+  float* red = reinterpret_cast<float*>(lds + kStemCtOff + 512 * 64 * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r_lane = lane & 31, hsel = lane >> 5;
-  int mb = blockIdx.x;
-  const int bwi = mb % p.nbw; mb /= p.nbw;
-  const int bhi = mb % p.nbh; mb /= p.nbh;
-  const int bdi = mb % p.nbd;
-  const int n = mb / p.nbd;
-  const int bd = 1 << p.lbd, bh = 1 << p.lbh, bw = 1 << p.lbw;
+  const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
   const int boxvol = bd * bh * bw;
-  const int d0 = bdi * bd, h0 = bhi * bh, w0 = bwi * bw;
   const int HH = bh + 2, HW = bw + 2;
   const int HV = (bd + 2) * HH * HW;
   const long plane = (long)p.H * p.W;
   const bf16_t* x0 = (const bf16_t*)p.x0;
-  const bool w16 = p.lbw == 4;
+  const bool w16 = lbw_ == 4;
   const int prow = w16 ? perm32(r_lane) : r_lane;
-  int hb[4];
+  int hb[2];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    int r = wave * 128 + mt * 32 + prow;
+  for (int mt = 0; mt < 2; ++mt) {
+    int r = wave * 64 + mt * 32 + prow;
     if (r >= boxvol) r = 0;
-    const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
+    const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
     hb[mt] = (rd * HH + rh) * HW + rw;
   }
-  const bool wave_active = wave * 128 < boxvol;
-  // ---- stage weights (linear copy) and the 8-channel halo (16 B per row) by LDS-DMA ----
-  for (int base = wave * 64; base < kStemWBytes / 16; base += kThreads)
-    __builtin_amdgcn_global_load_lds((const char*)p.w + (base + lane) * 16, (LDS_AS void*)(wl + base * 16), 16, 0, 0);
-  for (int base = wave * 64; base < HV; base += kThreads) {
-    const int hv = base + lane;
-    const void* src = g_zero16;
-    if (hv < HV) {
-      const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-      const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
-      if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W)
-        src = x0 + (((long)n * p.D + gd) * plane + (long)gh * p.W + gw) * 8;
-    }
-    __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(hl + base * 16), 16, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  f32x16_t acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  if (wave_active) {
-#pragma unroll 2
-    for (int st = 0; st < kStemSteps; ++st) {
-      const int off = tap_off(2 * st + hsel, HH, HW);
-      s16x8_t b0 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + r_lane) * 16 + hsel * 8) * 2);
-      s16x8_t b1 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + 32 + r_lane) * 16 + hsel * 8) * 2);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        s16x8_t a = *reinterpret_cast<const s16x8_t*>(hl + (hb[mt] + off) * 16);
-        acc[mt][0] = mfma(a, b0, acc[mt][0]);
-        acc[mt][1] = mfma(a, b1, acc[mt][1]);
-      }
-    }
-  }
-  // ---- epilogue (as conv3_fwd_kernel's bf16 path) ----
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  const bool wave_active = wave * 64 < boxvol;
   float bias_l[2] = {0.f, 0.f};
   if (p.bias) { bias_l[0] = p.bias[r_lane]; bias_l[1] = p.bias[32 + r_lane]; }
+
+  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    int bwi = b % p.nbw; b /= p.nbw;
+    int bhi = b % p.nbh; b /= p.nbh;
+    int bdi = b % p.nbd;
+    n = b / p.nbd;
+    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
+  };
+  auto stage_halo = [&](int b, char* hl) {
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    for (int base = wave * 64; base < HV; base += kStemThreads) {
+      const int hv = base + lane;
+      const void* src = g_zero16;
+      if (hv < HV) {
+        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W)
+          src = x0 + (((long)n * p.D + gd) * plane + (long)gh * p.W + gw) * 8;
+      }
+      __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(hl + base * 16), 16, 0, 0);
+    }
+  };
+  // prologue: weights + first halo
+  int b = blockIdx.x;
+  for (int base = wave * 64; base < kStemWBytes / 16; base += kStemThreads)
+    __builtin_amdgcn_global_load_lds((const char*)p.w + (base + lane) * 16, (LDS_AS void*)(wl + base * 16), 16, 0, 0);
+  if (b < nbox) stage_halo(b, lds + kStemWBytes);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  bf16_t* ct = reinterpret_cast<bf16_t*>(lds);
-  if (wave_active) {
+  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
+    char* hl = lds + kStemWBytes + (it & 1) * kStemHaloBytes;
+    const int bn = b + gridDim.x;
+    if (bn < nbox) stage_halo(bn, lds + kStemWBytes + ((it + 1) & 1) * kStemHaloBytes);
+    f32x16_t acc[2][2];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
-        const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
-        bool valid = r < boxvol;
-        if (valid) {
-          const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
-          valid = d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
-        }
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const float v = acc[mt][nt][e] + bias_l[nt];
-          ct[r * 64 + nt * 32 + r_lane] = f2bf(v);
-          if (valid) { s1[nt] += v; s2[nt] += v * v; }
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    if (wave_active) {
+#pragma unroll
+      for (int st = 0; st < kStemSteps; ++st) {
+        const int off = hsel ? tap_off(2 * st + 1, HH, HW) : tap_off(2 * st, HH, HW);
+        s16x8_t b0 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + r_lane) * 16 + hsel * 8) * 2);
+        s16x8_t b1 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + 32 + r_lane) * 16 + hsel * 8) * 2);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          s16x8_t a = *reinterpret_cast<const s16x8_t*>(hl + (hb[mt] + off) * 16);
+          acc[mt][0] = mfma(a, b0, acc[mt][0]);
+          acc[mt][1] = mfma(a, b1, acc[mt][1]);
         }
       }
     }
-  }
-  __syncthreads();
-  for (int pc = tid; pc < boxvol * 8; pc += kThreads) {
-    const int r = pc >> 3, q = pc & 7;
-    const int rd = r >> (p.lbh + p.lbw), rh = (r >> p.lbw) & (bh - 1), rw = r & (bw - 1);
-    const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
-    if (gd >= p.D || gh >= p.H || gw >= p.W) continue;
-    const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
-    *reinterpret_cast<u32x4_t*>((bf16_t*)p.y0 + vox * 64 + q * 8) = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
-  }
-  if (p.stats) {
-    float* red = reinterpret_cast<float*>(lds + 512 * 64 * 2);
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const bool interior = d0 + bd <= p.D && h0 + bh <= p.H && w0 + bw <= p.W;
+    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+    uint32_t vmask = 0;  // bit mt * 16 + e: row valid
+    if (wave_active) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      s1[nt] += __shfl_xor(s1[nt], 32, 64);
-      s2[nt] += __shfl_xor(s2[nt], 32, 64);
-      if (hsel == 0) {
-        red[(wave * 64 + nt * 32 + r_lane) * 2 + 0] = s1[nt];
-        red[(wave * 64 + nt * 32 + r_lane) * 2 + 1] = s2[nt];
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+          const int r = wave * 64 + mt * 32 + (w16 ? perm32(rr) : rr);
+          bool valid = r < boxvol;
+          if (valid && !interior) {
+            const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+            valid = d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
+          }
+          if (valid) vmask |= 1u << (mt * 16 + e);
+        }
+    }
+    __syncthreads();  // previous box's C-tile reads (stores) are done in every wave
+    if (wave_active) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+          const int r = wave * 64 + mt * 32 + (w16 ? perm32(rr) : rr);
+          const bool valid = (vmask >> (mt * 16 + e)) & 1;
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const float v = acc[mt][nt][e] + bias_l[nt];
+            ct[r * 64 + nt * 32 + r_lane] = f2bf(v);
+            if (valid) s1[nt] += v;
+          }
+        }
+      }
+    }
+    if (p.stats) {
+      // per-wave mean, then squared deviations (see conv3_fwd_kernel's epilogue)
+      const float nw = (float)(__popc(vmask) + __shfl_xor(__popc(vmask), 32, 64));
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        s1[nt] += __shfl_xor(s1[nt], 32, 64);
+        const float mw = nw > 0.f ? s1[nt] / nw : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float d = acc[mt][nt][e] + bias_l[nt] - mw;
+            if ((vmask >> (mt * 16 + e)) & 1) s2[nt] += d * d;
+          }
+        s2[nt] += __shfl_xor(s2[nt], 32, 64);
+        if (hsel == 0) {
+          float* rp = red + (wave * 64 + nt * 32 + r_lane) * 3;
+          rp[0] = s1[nt];
+          rp[1] = s2[nt];
+          rp[2] = nw;
+        }
       }
     }
     __syncthreads();
-    if (tid < 64) {
-      float a = 0.f, b = 0.f;
+    if (p.stats && tid < 64) {
+      float S = 0.f, Nn = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) { a += red[(w * 64 + tid) * 2]; b += red[(w * 64 + tid) * 2 + 1]; }
-      float* stp = p.stats + ((long)blockIdx.x * 64 + tid) * 2;
-      stp[0] = a;
-      stp[1] = b;
+      for (int w = 0; w < kStemThreads / 64; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
+      const float m = Nn > 0.f ? S / Nn : 0.f;
+      float M2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < kStemThreads / 64; ++w) {
+        const float c = red[(w * 64 + tid) * 3 + 2];
+        if (c > 0.f) {
+          const float d = red[(w * 64 + tid) * 3] / c - m;
+          M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+        }
+      }
+      float* stp = p.stats + ((long)b * 64 + tid) * 2;
+      stp[0] = S;
+      stp[1] = M2;
+      if (tid == 0) p.stats[(long)nbox * 64 * 2 + b] = Nn;
     }
+#pragma unroll 2
+    for (int i = 0; i < kStemStores; ++i) {
+      const int pc = tid + i * kStemThreads;
+      const int r = pc >> 3, q = pc & 7;
+      const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+      const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+      u32x4_t* dst = reinterpret_cast<u32x4_t*>(g_sink) + (tid & 511);
+      if (r < boxvol && (interior || (gd < p.D && gh < p.H && gw < p.W)))
+        dst = reinterpret_cast<u32x4_t*>((bf16_t*)p.y0 + (((long)n * p.D + gd) * plane + (long)gh * p.W + gw) * 64 + q * 8);
+      *dst = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
+    }
+    // the next halo's LDS-DMA (issued before the stores) has landed; make it visible
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStemStores) : "memory");
+    __syncthreads();
   }
 }
 
@@ -860,10 +983,12 @@ constexpr int kSBV = 256;
 constexpr int kSHalo = 648;                         // (4+2)(4+2)(16+2) for the 4x4x16 box
 constexpr int kSBuf = kSBV * 128 + kSHalo * 16;     // dy tile (128 B rows) + halo (16 B rows)
 
+template <int LBD, int LBH, int LBW>
 __global__ void __launch_bounds__(256, 1) stem_wgrad_kernel(const bf16_t* x, const bf16_t* dy, float* dw,
                                                             int N, int D, int H, int W, int cin_w,
-                                                            int lbd, int lbh, int lbw, int nbd, int nbh, int nbw,
+                                                            int lbd_r, int lbh_r, int lbw_r, int nbd, int nbh, int nbw,
                                                             int nbox, int boxes_per_split) {
+  const int lbd = LBW >= 0 ? LBD : lbd_r, lbh = LBW >= 0 ? LBH : lbh_r, lbw = LBW >= 0 ? LBW : lbw_r;
   extern __shared__ __attribute__((aligned(16))) char slds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hsel = lane >> 5;
   const int bd = 1 << lbd, bh = 1 << lbh, bw = 1 << lbw;
@@ -938,6 +1063,7 @@ __global__ void __launch_bounds__(256, 1) stem_wgrad_kernel(const bf16_t* x, con
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
   auto compute = [&](const char* buf) {
     const char* xb = buf + kSBV * 128;
+#pragma unroll 4
     for (int k0 = 0; k0 < boxvol; k0 += 16) {
       const int v_a = k0 + 8 * hsel + qq;
       s16x8_t a[2];
@@ -947,7 +1073,9 @@ __global__ void __launch_bounds__(256, 1) stem_wgrad_kernel(const bf16_t* x, con
         s16x4_t lo = tr_read(buf, dy_off_bf16(v_a, co)), hi = tr_read(buf, dy_off_bf16(v_a + 4, co));
         a[ct] = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
-      const int hr0 = halo_row(v_a), hr1 = halo_row(v_a + 4);
+      // with a compile-time box of width >= 16 the lane's rows share (rd, rh) with k0
+        const int hr0 = LBW >= 4 ? halo_row(k0) + 8 * hsel + qq : halo_row(v_a);
+        const int hr1 = LBW >= 4 ? hr0 + 4 : halo_row(v_a + 4);
 #pragma unroll
       for (int js = 0; js < 2; ++js) {
         if (js >= nj) break;
@@ -1034,6 +1162,7 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   const int CK = pcms_conv3_chunk(dtype);
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0 || (c1 > 0 && x1 == nullptr)) return -1;
+  if (stats && accumulate) return -6;  // BN statistics describe a fresh output only
   if (y1 == nullptr) cy0 = Cout;
   if (cy0 % 64 != 0 && cy0 != Cout) return -2;
   Box b = fwd_box(D, H, W);
@@ -1053,10 +1182,13 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
   if (splits > 1) p.yacc = yacc;
   dim3 grid(N * p.nbd * p.nbh * p.nbw, Cout / 64, splits);
-  if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2>), grid, dim3(kThreads), 0, s, p);
-  else
-    hipLaunchKernelGGL((conv3_fwd_kernel<float, 1>), grid, dim3(kThreads), 0, s, p);
+  const bool hot = b.lbd == 2 && b.lbh == 3 && b.lbw == 4;
+  if (dtype == PCMS_BF16) {
+    if (hot) hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2, 2, 3, 4>), grid, dim3(kThreads), 0, s, p);
+    else hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
+  } else {
+    hipLaunchKernelGGL((conv3_fwd_kernel<float, 1, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
+  }
   PCMS_CHECK_LAUNCH();
 }
 
@@ -1081,7 +1213,21 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
   p.nchunk = 1; p.chunks_per_split = 1;
   p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
   p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3(N * p.nbd * p.nbh * p.nbw), dim3(kThreads), 0, s, p);
+  const int nbox = N * p.nbd * p.nbh * p.nbw;
+  if ((1 << (b.lbd + b.lbh + b.lbw)) > 512) return -5;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  if (b.lbd == 2 && b.lbh == 3 && b.lbw == 4) {
+    (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<2, 3, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kStemLds);
+    hipLaunchKernelGGL((stem_fwd_kernel<2, 3, 4>), dim3(std::min(nbox, ncu)), dim3(kStemThreads), kStemLds, s, p, nbox);
+  } else {
+    (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<-1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, kStemLds);
+    hipLaunchKernelGGL((stem_fwd_kernel<-1, -1, -1>), dim3(std::min(nbox, ncu)), dim3(kStemThreads), kStemLds, s, p, nbox);
+  }
   PCMS_CHECK_LAUNCH();
 }
 
@@ -1097,8 +1243,9 @@ int pcms_stem_wgrad(const void* x, const void* dy, float* dw, int cin_w, int N, 
   const int bps = cdiv(nbox, splits);
   splits = cdiv(nbox, bps);
   const size_t lds = 2 * (size_t)kSBuf;
-  (void)hipFuncSetAttribute((const void*)stem_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(splits), dim3(256), lds, s, (const bf16_t*)x, (const bf16_t*)dy, dw,
+  auto kern = (b.lbd == 2 && b.lbh == 2 && b.lbw == 4) ? stem_wgrad_kernel<2, 2, 4> : stem_wgrad_kernel<-1, -1, -1>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(splits), dim3(256), lds, s, (const bf16_t*)x, (const bf16_t*)dy, dw,
                      N, D, H, W, cin_w, b.lbd, b.lbh, b.lbw, nbd, nbh, nbw, nbox, bps);
   PCMS_CHECK_LAUNCH();
 }
@@ -1132,12 +1279,15 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   size_t lds;
   if (dtype == PCMS_BF16) {
     lds = (size_t)WTraits<bf16_t>::NBUF * (WTraits<bf16_t>::BV * WTraits<bf16_t>::DYROW + kWHaloMax * WTraits<bf16_t>::XROW);
-    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(conv3_wgrad_kernel<bf16_t>, grid, dim3(kWThreads), lds, s, p);
+    auto kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1>;
+    if (b.lbd == 2 && b.lbh == 2 && b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
+    else if (b.lbd == 1 && b.lbh == 3 && b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
   } else {
     lds = (size_t)WTraits<float>::NBUF * (WTraits<float>::BV * WTraits<float>::DYROW + kWHaloMax * WTraits<float>::XROW);
-    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(conv3_wgrad_kernel<float>, grid, dim3(kWThreads), lds, s, p);
+    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<float, -1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((conv3_wgrad_kernel<float, -1, -1, -1>), grid, dim3(kWThreads), lds, s, p);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;

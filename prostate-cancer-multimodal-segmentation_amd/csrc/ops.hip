@@ -38,8 +38,11 @@ __global__ void pack_input_kernel(const float* in, T* out, int N, int Cin, long 
 // ---------------- BatchNorm statistics ----------------
 // Stage 1: fp32 partial rows [rows][C][2] -> fp64 column sums [RB][C][2] (RB row groups).
 // block = 256 threads = 4 row lanes x 64 channels; grid = (ceil(C / 64), RB).
+// cnt != NULL: rows are (sum, M2 about the row mean) with per-row voxel counts cnt[rows];
+// column 2 then accumulates M2 + sum^2 / count (= the row's sum of squares, formed in fp64).
 constexpr int kRB = 64;
-__global__ void __launch_bounds__(256) colsum2_kernel(const float* part, int rows, int C, double* out) {
+__global__ void __launch_bounds__(256) colsum2_kernel(const float* part, int rows, int C, const float* cnt,
+                                                      double* out) {
   __shared__ double red[4][64][2];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -48,7 +51,12 @@ __global__ void __launch_bounds__(256) colsum2_kernel(const float* part, int row
     for (int r = blockIdx.y * 4 + rl; r < rows; r += kRB * 4) {
       const float2 v = *reinterpret_cast<const float2*>(part + ((long)r * C + c) * 2);
       s1 += (double)v.x;
-      s2 += (double)v.y;
+      if (cnt) {
+        const double n = (double)cnt[r];
+        s2 += (double)v.y + (n > 0.0 ? (double)v.x * (double)v.x / n : 0.0);
+      } else {
+        s2 += (double)v.y;
+      }
     }
   red[rl][cl][0] = s1;
   red[rl][cl][1] = s2;
@@ -466,26 +474,52 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n
 template <typename T>
 __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, const float* bias, T* y0, T* y1,
                                                              int cy0, float* stats, int C, long nvox) {
-  __shared__ float red[TPB / 64][64][2];
+  // stats row = (sum, M2 about the row mean), count row after the [rows][C][2] block
+  constexpr int NV = TPB / 64, KPT = 64 / NV;
+  __shared__ float red[NV][64][3];
   const int cl = threadIdx.x & 63, vl = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
   const long v0 = (long)blockIdx.x * 64;
+  const float bc = bias ? bias[c] : 0.f;
+  float xs[KPT];
   float s1 = 0.f, s2 = 0.f;
-  for (int k = vl; k < 64; k += TPB / 64) {
-    const long v = v0 + k;
-    if (v >= nvox) break;
-    float x = acc[v * C + c] + (bias ? bias[c] : 0.f);
+  int cntv = 0;
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    const long v = v0 + vl + i * NV;
+    xs[i] = 0.f;
+    if (v >= nvox) continue;
+    const float x = acc[v * C + c] + bc;
     T* dst = c < cy0 ? y0 + v * cy0 + c : y1 + v * (C - cy0) + (c - cy0);
     Elem<T>::st(dst, x);
-    s1 += x; s2 += x * x;
+    xs[i] = x;
+    s1 += x;
+    ++cntv;
   }
+  if (!stats) return;
+  const float m = cntv ? s1 / cntv : 0.f;
+#pragma unroll
+  for (int i = 0; i < KPT; ++i)
+    if (v0 + vl + i * NV < nvox) s2 += (xs[i] - m) * (xs[i] - m);
   red[vl][cl][0] = s1;
   red[vl][cl][1] = s2;
+  red[vl][cl][2] = (float)cntv;
   __syncthreads();
-  if (vl == 0 && stats) {
-    for (int k = 1; k < TPB / 64; ++k) { s1 += red[k][cl][0]; s2 += red[k][cl][1]; }
-    stats[((long)blockIdx.x * C + c) * 2] = s1;
-    stats[((long)blockIdx.x * C + c) * 2 + 1] = s2;
+  if (vl == 0) {
+    float S = 0.f, Nn = 0.f;
+    for (int k = 0; k < NV; ++k) { S += red[k][cl][0]; Nn += red[k][cl][2]; }
+    const float mb = Nn > 0.f ? S / Nn : 0.f;
+    float M2 = 0.f;
+    for (int k = 0; k < NV; ++k) {
+      const float n = red[k][cl][2];
+      if (n > 0.f) {
+        const float d = red[k][cl][0] / n - mb;
+        M2 += red[k][cl][1] + n * d * d;
+      }
+    }
+    stats[((long)blockIdx.x * C + c) * 2] = S;
+    stats[((long)blockIdx.x * C + c) * 2 + 1] = M2;
+    if (cl == 0 && blockIdx.y == 0) stats[(long)gridDim.x * C * 2 + blockIdx.x] = Nn;
   }
 }
 
@@ -516,7 +550,8 @@ int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long 
 int pcms_bn_finalize(const float* part, int rows, int C, double count, const float* gamma, const float* beta,
                      float* rmean, float* rvar, long long* nbt, float momentum, float eps,
                      float* scale, float* shift, float* mean, float* invstd, double* ws, hipStream_t s) {
-  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, part, rows, C, ws);
+  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, part, rows, C,
+                     part + (long)rows * C * 2, ws);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, s, (const double*)ws, C, count, gamma,
@@ -567,7 +602,8 @@ int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scal
     hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<float>, dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C, ws);
+  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C,
+                     (const float*)nullptr, ws);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, s, (const double*)ws, C, (double)nvox,

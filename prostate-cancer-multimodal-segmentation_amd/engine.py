@@ -247,7 +247,8 @@ class UNetEngine:
         rows_f = max(query("pcms_conv3_mblocks", N, *S[l]) for l in range(5))
         rows_s = max(query("pcms_split_epilogue_rows", nv[l]) for l in range(5))
         rows_b = max(query("pcms_bn_bwd_rows", self.code, C[l], nv[l]) for l in range(5))
-        b["stats"] = torch.empty(max(rows_f, rows_s, rows_b) * 1024 * 2, dtype=torch.float32, device=dev)
+        # BN partials [rows][C][2] + [rows] voxel counts
+        b["stats"] = torch.empty(max(rows_f, rows_s, rows_b) * (1024 * 2 + 1), dtype=torch.float32, device=dev)
         b["coef"] = torch.empty(3 * 1024, dtype=torch.float32, device=dev)
         b["bnws"] = torch.empty(query("pcms_bn_ws_doubles", 1024), dtype=torch.float64, device=dev)
         b["dwt"] = torch.empty(27 * 1024 * 1024, dtype=torch.float32, device=dev)

@@ -64,7 +64,7 @@ def main():
         L.call("pcms_conv3_pack", code, w, wf, cout, cin, 0)
         L.call("pcms_conv3_pack", code, w, wd, cout, cin, 1)
         rows = L.query("pcms_conv3_mblocks", N, D, H, W)
-        stats = torch.empty(rows * cout * 2, device="cuda")
+        stats = torch.empty(rows * (cout * 2 + 1), device="cuda")
         bias = torch.zeros(cout, device="cuda")
         dw = torch.zeros(cout * cin * 27, device="cuda")
         dwt = torch.empty(27 * cout * cin, device="cuda")

@@ -1,0 +1,49 @@
+"""Time the stem kernels (fwd / wgrad) at config 2 in isolation (for rocprofv3 PMC runs)."""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+
+
+def main():
+    import pcms_amd  # noqa
+    from pcms_amd import _lib as L
+    which = sys.argv[1] if len(sys.argv) > 1 else "both"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    N, D, H, W = 2, 128, 128, 64
+    nvox = N * D * H * W
+    T = torch.bfloat16
+    sets = [(torch.rand(nvox * 8, device="cuda").to(T), torch.empty(nvox * 64, dtype=T, device="cuda"),
+             torch.randn(nvox * 64, device="cuda").to(T)) for _ in range(3)]
+    w = torch.randn(64, 5, 27, device="cuda") * 0.2
+    wp = torch.empty(L.query("pcms_stem_pack_elems"), dtype=T, device="cuda")
+    L.call("pcms_stem_pack", w, wp, 5)
+    bias = torch.zeros(64, device="cuda")
+    stats = torch.empty(L.query("pcms_conv3_mblocks", N, D, H, W) * 129, device="cuda")
+    dw = torch.zeros(64 * 5 * 27, device="cuda")
+    for name in ("fwd", "wgrad"):
+        if which not in ("both", name):
+            continue
+        def f(i):
+            x, y, dy = sets[i % 3]
+            if name == "fwd":
+                L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W)
+            else:
+                L.call("pcms_stem_wgrad", x, dy, dw, 5, N, D, H, W, 256)
+        for i in range(3):
+            f(i)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            f(i)
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1) / reps * 1e-3
+        byts = nvox * 5 * 2 + nvox * 64 * 2
+        print(f"stem {name}: {t * 1e6:.1f} us  {byts / t / 1e9:.0f} GB/s algorithmic", flush=True)
+
+
+if __name__ == "__main__":
+    main()

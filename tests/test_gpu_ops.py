@@ -46,6 +46,20 @@ def close(got, exp, tol, what=""):
 DTS = [(torch.float32, 0, 2e-5), (torch.bfloat16, 1, 1e-2)]
 
 
+def bn_moments(stats, rows, C, nvox):
+    """(mean, biased var) per channel from the kernels' BN partials: [rows][C][2] rows of
+    (sum, M2 about the row mean) + [rows] counts, merged in fp64 (Chan)."""
+    st = stats.detach().cpu().double()
+    part = st[: rows * C * 2].view(rows, C, 2)
+    cnt = st[rows * C * 2: rows * C * 2 + rows]
+    assert cnt.sum().item() == nvox, (cnt.sum().item(), nvox)
+    mean = part[:, :, 0].sum(0) / nvox
+    nz = cnt > 0
+    rmean = part[nz, :, 0] / cnt[nz, None]
+    m2 = part[:, :, 1].sum(0) + (cnt[nz, None] * (rmean - mean) ** 2).sum(0)
+    return mean, m2 / nvox
+
+
 @pytest.mark.parametrize("dt,code,tol", DTS)
 @pytest.mark.parametrize("N,cin,cout,S,split", [
     (2, 8, 64, (16, 16, 16), 1),        # stem-like (5 real channels padded to 8)
@@ -75,7 +89,7 @@ def test_conv3_fwd(dt, code, tol, N, cin, cout, S, split):
     y = torch.empty(N, *S, cout, dtype=dt, device=DEV)
     nvox = N * S[0] * S[1] * S[2]
     rows = L.query("pcms_conv3_mblocks", N, *S)
-    stats = torch.zeros(max(rows, L.query("pcms_split_epilogue_rows", nvox)) * cout * 2, device=DEV)
+    stats = torch.zeros(max(rows, L.query("pcms_split_epilogue_rows", nvox)) * (cout * 2 + 1), device=DEV)
     if split == 1:
         L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, None, stats, 0,
                N, *S, cout, 1)
@@ -87,10 +101,50 @@ def test_conv3_fwd(dt, code, tol, N, cin, cout, S, split):
         rows = L.query("pcms_split_epilogue_rows", nvox)
     torch.cuda.synchronize()
     close(ncdhw(y.cpu()), ref, tol, "conv3 fwd")
-    st = stats.cpu()[: rows * cout * 2].view(rows, cout, 2).double().sum(0)
+    mean, var = bn_moments(stats, rows, cout, nvox)
     yref = ref.transpose(0, 1).reshape(cout, -1)
-    close(st[:, 0], yref.sum(1), 1e-3 if code else 1e-5, "stats sum")
-    close(st[:, 1], (yref * yref).sum(1), 1e-3 if code else 1e-5, "stats sumsq")
+    close(mean, yref.mean(1), 1e-3 if code else 1e-5, "stats mean")
+    close(var, yref.var(1, unbiased=False), 1e-3 if code else 1e-5, "stats var")
+
+
+@pytest.mark.parametrize("N,S,split", [(2, (1, 1, 1), 4), (2, (2, 2, 2), 1), (1, (16, 16, 16), 1),
+                                       (2, (3, 5, 7), 2)])
+def test_bn_stats_large_mean(N, S, split):
+    """BN partial moments stay accurate when |mean| >> std (fp32 E[x^2] - E[x]^2 would lose
+    most digits of the variance: BatchNorm over 2 voxels per channel at the deepest level)."""
+    L = _lib()
+    g = torch.Generator().manual_seed(5)
+    cin, cout = 64, 64
+    x = torch.randn(N, cin, *S, generator=g) * 0.05
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+    b = 100.0 + torch.randn(cout, generator=g)
+    ref = F.conv3d(x.double(), w.double(), b.double(), padding=1)
+    ck = L.query("pcms_conv3_chunk", 0)
+    wpack = torch.empty(-(-cin // ck) * 27 * cout * ck, device=DEV)
+    L.call("pcms_conv3_pack", 0, w.to(DEV), wpack, cout, cin, 0)
+    y = torch.empty(N, *S, cout, device=DEV)
+    nvox = N * S[0] * S[1] * S[2]
+    rows = L.query("pcms_conv3_mblocks", N, *S) if split == 1 else L.query("pcms_split_epilogue_rows", nvox)
+    stats = torch.zeros(rows * (cout * 2 + 1), device=DEV)
+    xd = ndhwc(x).to(DEV)
+    if split == 1:
+        L.call("pcms_conv3_fwd", 0, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, None, stats, 0,
+               N, *S, cout, 1)
+    else:
+        acc = torch.zeros(nvox * cout, device=DEV)
+        L.call("pcms_conv3_fwd", 0, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, acc, None, 0,
+               N, *S, cout, split)
+        L.call("pcms_split_epilogue", 0, acc, b.to(DEV), y, None, cout, stats, cout, nvox)
+    torch.cuda.synchronize()
+    mean, var = bn_moments(stats, rows, cout, nvox)
+    yref = ref.transpose(0, 1).reshape(cout, -1)
+    # the variance of the kernel's own fp32 outputs (what BN normalises) vs the fp64 truth
+    yk = ncdhw(y.cpu()).double().transpose(0, 1).reshape(cout, -1)
+    vk = yk.var(1, unbiased=False)
+    vr = yref.var(1, unbiased=False)
+    assert ((var - vk).abs() / vk).max().item() < 1e-3
+    assert ((var - vr).abs() / vr.mean()).max().item() < 2e-3
+    close(mean, yref.mean(1), 1e-6, "mean")
 
 
 @pytest.mark.parametrize("dt,code,tol", DTS)
@@ -176,7 +230,8 @@ def test_bn_relu_fwd_bwd(dt, code, tol):
     rm, rv = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
     # statistics from per-voxel partial rows (one voxel per row here)
     yv = ndhwc(y).reshape(nvox, C).double()
-    part = torch.stack([yv, yv * yv], -1).float().contiguous()
+    part = torch.cat([torch.stack([yv, torch.zeros_like(yv)], -1).flatten(), torch.ones(nvox, dtype=yv.dtype)])
+    part = part.float().contiguous()
     yr = y.double().requires_grad_(True)
     rm_r, rv_r = rm.double().clone(), rv.double().clone()
     out = F.relu(F.batch_norm(yr, rm_r, rv_r, gamma.double(), beta.double(), True, 0.1, 1e-5))
@@ -379,7 +434,7 @@ def test_stem_fwd_wgrad_bf16(N, S):
     L.call("pcms_stem_pack", w.to(DEV), wp, 5)
     y = torch.empty(N, *S, 64, dtype=torch.bfloat16, device=DEV)
     rows = L.query("pcms_conv3_mblocks", N, *S)
-    stats = torch.zeros(rows * 64 * 2, device=DEV)
+    stats = torch.zeros(rows * (64 * 2 + 1), device=DEV)
     L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y, stats, N, *S)
     xr = x.double()
     wr = w.to(torch.bfloat16).double().requires_grad_(True)
@@ -391,9 +446,9 @@ def test_stem_fwd_wgrad_bf16(N, S):
     L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, 5, N, *S, 64)
     torch.cuda.synchronize()
     close(ncdhw(y.cpu()), ref.detach(), 1e-2, "stem fwd")
-    st = stats.cpu().view(rows, 64, 2).double().sum(0)
+    mean, var = bn_moments(stats, rows, 64, N * S[0] * S[1] * S[2])
     yr = ref.detach().transpose(0, 1).reshape(64, -1)
-    close(st[:, 0], yr.sum(1), 1e-3, "stem stats sum")
-    close(st[:, 1], (yr * yr).sum(1), 1e-3, "stem stats sumsq")
+    close(mean, yr.mean(1), 1e-3, "stem stats mean")
+    close(var, yr.var(1, unbiased=False), 1e-3, "stem stats var")
     assert dw[-guard:].abs().max().item() == 0.0
     close(dw[:-guard].cpu().view(64, 5, 3, 3, 3), wr.grad, 1e-4, "stem wgrad")
