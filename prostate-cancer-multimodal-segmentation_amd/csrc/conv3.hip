@@ -337,6 +337,8 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
       s1[nt] += __shfl_xor(s1[nt], 32, 64);
       mw[nt] = nw > 0.f ? s1[nt] / nw : 0.f;
     }
+    // squared deviations about the rounded wave mean, corrected by (sum d)^2 / n
+    float sd[2] = {0.f, 0.f};
     if (wave_active) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -347,6 +349,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
           for (int nt = 0; nt < 2; ++nt) {
             const float d = acc[mt][nt][e] + bias_l[nt] - mw[nt];
             s2[nt] += d * d;
+            sd[nt] += d;
           }
         }
     }
@@ -355,6 +358,8 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       s2[nt] += __shfl_xor(s2[nt], 32, 64);
+      sd[nt] += __shfl_xor(sd[nt], 32, 64);
+      if (nw > 0.f) s2[nt] -= sd[nt] * sd[nt] / nw;
       if (hsel == 0) {
         float* rp = red + (wave * 64 + nt * 32 + r_lane) * 3;
         rp[0] = s1[nt];
@@ -371,15 +376,17 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
         Nn += red[(w * 64 + tid) * 3 + 2];
       }
       const float m = Nn > 0.f ? S / Nn : 0.f;
-      float M2 = 0.f;
+      float M2 = 0.f, sdd = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
         const float c = red[(w * 64 + tid) * 3 + 2];
         if (c > 0.f) {
           const float d = red[(w * 64 + tid) * 3 + 0] / c - m;
           M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+          sdd += c * d;
         }
       }
+      if (Nn > 0.f) M2 -= sdd * sdd / Nn;
       float* st = p.stats + ((long)blockIdx.x * p.Cout + co_base + tid) * 2;
       st[0] = S;
       st[1] = M2;
@@ -765,11 +772,14 @@ Box fwd_box(int D, int H, int W) {
 constexpr int kStemSteps = 14;                    // 28 taps (27 + 1 zero) / 2
 constexpr int kStemWBytes = kStemSteps * 64 * 16 * 2;  // packed weights [14][64][16] bf16
 
-// master W[64][cin_w][27] fp32 -> [14][64][16] bf16, k = h * 8 + c <-> (tap 2s + h, c)
+// master W[64][cin_w][27] fp32 -> [14][64][16] bf16, k = h * 8 + c <-> (tap 2s + h, c);
+// the 64 output columns are ordered (nt, j) -> channel 2 j + nt so that a lane's two MFMA
+// tiles hold an adjacent channel pair (one packed bf16x2 LDS write per row)
 __global__ void stem_pack_kernel(const float* w, bf16_t* out, int cin_w) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= kStemSteps * 64 * 16) return;
-  const int k = i & 15, co = (i >> 4) & 63, s = i >> 10;
+  const int k = i & 15, col = (i >> 4) & 63, s = i >> 10;
+  const int co = 2 * (col & 31) + (col >> 5);  // MFMA column (nt, j) <-> channel 2 j + nt
   const int tap = 2 * s + (k >> 3), c = k & 7;
   float v = 0.f;
   if (tap < 27 && c < cin_w) v = w[((long)co * cin_w + c) * 27 + tap];
@@ -789,7 +799,7 @@ __device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
 // issued before them, is retired by s_waitcnt vmcnt(kStemStores).
 constexpr int kStemThreads = 512;
 constexpr int kStemHaloBytes = kHaloMax * 16;                 // 18 KiB
-constexpr int kStemCtOff = kStemWBytes + 2 * kStemHaloBytes;   // C tile offset
+constexpr int kStemCtOff = 2 * kStemHaloBytes;                 // C tile offset
 constexpr int kStemLds = kStemCtOff + 512 * 64 * 2 + 6144;     // + stats reduction [8][64][3]
 constexpr int kStemStores = 512 * 8 / kStemThreads;            // 16-B stores per thread per box
 __device__ __attribute__((aligned(16))) uint32_t g_sink[4 * 512];
@@ -798,7 +808,6 @@ template <int LBD, int LBH, int LBW>
 __global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p, int nbox) {
   const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* wl = lds;
   bf16_t* ct = reinterpret_cast<bf16_t*>(lds + kStemCtOff);
   float* red = reinterpret_cast<float*>(lds + kStemCtOff + 512 * 64 * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -821,7 +830,7 @@ __global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p
   }
   const bool wave_active = wave * 64 < boxvol;
   float bias_l[2] = {0.f, 0.f};
-  if (p.bias) { bias_l[0] = p.bias[r_lane]; bias_l[1] = p.bias[32 + r_lane]; }
+  if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
 
   auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
     int bwi = b % p.nbw; b /= p.nbw;
@@ -845,95 +854,124 @@ __global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p
       __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(hl + base * 16), 16, 0, 0);
     }
   };
-  // prologue: weights + first halo
+  // prologue: the B fragments of all 14 k-steps stay in registers for the whole kernel
+  // (28 x 16 B per lane, loaded once); first halo
+  s16x8_t wb[kStemSteps][2];
+  {
+    const bf16_t* wg = (const bf16_t*)p.w;
+#pragma unroll
+    for (int st = 0; st < kStemSteps; ++st) {
+      wb[st][0] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + r_lane) * 16 + hsel * 8);
+      wb[st][1] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
+    }
+  }
   int b = blockIdx.x;
-  for (int base = wave * 64; base < kStemWBytes / 16; base += kStemThreads)
-    __builtin_amdgcn_global_load_lds((const char*)p.w + (base + lane) * 16, (LDS_AS void*)(wl + base * 16), 16, 0, 0);
-  if (b < nbox) stage_halo(b, lds + kStemWBytes);
+  if (b < nbox) stage_halo(b, lds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int it = 0; b < nbox; b += gridDim.x, ++it) {
-    char* hl = lds + kStemWBytes + (it & 1) * kStemHaloBytes;
+    char* hl = lds + (it & 1) * kStemHaloBytes;
     const int bn = b + gridDim.x;
-    if (bn < nbox) stage_halo(bn, lds + kStemWBytes + ((it + 1) & 1) * kStemHaloBytes);
+    if (bn < nbox) stage_halo(bn, lds + ((it + 1) & 1) * kStemHaloBytes);
     f32x16_t acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];  // bias folded into the accumulator
     if (wave_active) {
+      // lane half hsel reads tap 2 st + hsel: constant base offset + hsel * constant delta.
+      // A fragments are prefetched one k-step ahead; sched_barrier keeps the compiler from
+      // hoisting every step's LDS reads (register pressure: the weights live in VGPRs).
+      // (hs16 is opaque so the 28 per-step lane addresses are formed in the loop, not
+      // hoisted out of it into spilled registers)
+      int hs16 = hsel * 16;
+      asm volatile("" : "+v"(hs16));
+      auto load_a = [&](int st, s16x8_t (&a)[2]) {
+        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
+        const int off16 = o0 * 16 + hs16 * (o1 - o0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb[mt] * 16 + off16);
+      };
+      s16x8_t abuf[2][2];
+      load_a(0, abuf[0]);
 #pragma unroll
       for (int st = 0; st < kStemSteps; ++st) {
-        const int off = hsel ? tap_off(2 * st + 1, HH, HW) : tap_off(2 * st, HH, HW);
-        s16x8_t b0 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + r_lane) * 16 + hsel * 8) * 2);
-        s16x8_t b1 = *reinterpret_cast<const s16x8_t*>(wl + ((st * 64 + 32 + r_lane) * 16 + hsel * 8) * 2);
+        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          s16x8_t a = *reinterpret_cast<const s16x8_t*>(hl + (hb[mt] + off) * 16);
-          acc[mt][0] = mfma(a, b0, acc[mt][0]);
-          acc[mt][1] = mfma(a, b1, acc[mt][1]);
+          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
+          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     int n, d0, h0, w0;
     origin(b, n, d0, h0, w0);
     const bool interior = d0 + bd <= p.D && h0 + bh <= p.H && w0 + bw <= p.W;
-    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
-    uint32_t vmask = 0;  // bit mt * 16 + e: row valid
-    if (wave_active) {
+    // Epilogue: C tile -> LDS as packed bf16 channel pairs; BatchNorm partials single-pass,
+    // shifted by the wave's row-0 value K of each channel: per wave S1 = sum d + n K,
+    // M2 = sum d^2 - (sum d)^2 / n (d = v - K), waves merged with Chan's formula below.
+    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
-          const int r = wave * 64 + mt * 32 + (w16 ? perm32(rr) : rr);
-          bool valid = r < boxvol;
-          if (valid && !interior) {
-            const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
-            valid = d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
-          }
-          if (valid) vmask |= 1u << (mt * 16 + e);
-        }
-    }
+    for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(acc[0][nt][0], r_lane, 64);
+    float nw = 0.f;
     __syncthreads();  // previous box's C-tile reads (stores) are done in every wave
     if (wave_active) {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
-          const int r = wave * 64 + mt * 32 + (w16 ? perm32(rr) : rr);
-          const bool valid = (vmask >> (mt * 16 + e)) & 1;
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const float v = acc[mt][nt][e] + bias_l[nt];
-            ct[r * 64 + nt * 32 + r_lane] = f2bf(v);
-            if (valid) s1[nt] += v;
-          }
-        }
-      }
-    }
-    if (p.stats) {
-      // per-wave mean, then squared deviations (see conv3_fwd_kernel's epilogue)
-      const float nw = (float)(__popc(vmask) + __shfl_xor(__popc(vmask), 32, 64));
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        s1[nt] += __shfl_xor(s1[nt], 32, 64);
-        const float mw = nw > 0.f ? s1[nt] / nw : 0.f;
+      // row of (mt, e) = perm32((e & 3) + 8 (e >> 2) + 4 hsel) as constant + (+-16 hsel); the
+      // opaque hp keeps the per-row indices from being hoisted out of the box loop (they
+      // would pin ~100 VGPRs)
+      int hp = hsel * 16;
+      asm volatile("" : "+v"(hp));
+      auto row_of = [&](int mt, int e) {
+        const int g = e >> 2;
+        const int base = wave * 64 + mt * 32 + (e & 3);
+        if (w16) return base + (g == 0 ? hp : g == 1 ? 20 - hp : g == 2 ? 24 - hp : 12 + hp);
+        return base + 8 * g + (hp >> 2);
+      };
+      if (interior && boxvol == 512) {  // every row valid: no per-row tests
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            const float d = acc[mt][nt][e] + bias_l[nt] - mw;
-            if ((vmask >> (mt * 16 + e)) & 1) s2[nt] += d * d;
+            const int r = row_of(mt, e);
+            const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
+            *reinterpret_cast<uint32_t*>(ct + r * 64 + 2 * r_lane) = pack_bf16x2(v0, v1);
+            const float e0 = v0 - K[0], e1 = v1 - K[1];
+            s1[0] += e0; s2[0] += e0 * e0;
+            s1[1] += e1; s2[1] += e1 * e1;
           }
+        nw = 64.f;
+      } else {
+        int cnt = 0;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int r = row_of(mt, e);
+            const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
+            *reinterpret_cast<uint32_t*>(ct + r * 64 + 2 * r_lane) = pack_bf16x2(v0, v1);
+            const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+            const bool valid = r < boxvol && d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
+            const float e0 = valid ? v0 - K[0] : 0.f, e1 = valid ? v1 - K[1] : 0.f;
+            s1[0] += e0; s2[0] += e0 * e0;
+            s1[1] += e1; s2[1] += e1 * e1;
+            cnt += valid ? 1 : 0;
+          }
+        nw = (float)(cnt + __shfl_xor(cnt, 32, 64));
+      }
+    }
+    if (p.stats) {
+      const float inv = nw > 0.f ? 1.f / nw : 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        s1[nt] += __shfl_xor(s1[nt], 32, 64);
         s2[nt] += __shfl_xor(s2[nt], 32, 64);
         if (hsel == 0) {
-          float* rp = red + (wave * 64 + nt * 32 + r_lane) * 3;
-          rp[0] = s1[nt];
-          rp[1] = s2[nt];
+          float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
+          rp[0] = s1[nt] + nw * K[nt];
+          rp[1] = s2[nt] - s1[nt] * s1[nt] * inv;
           rp[2] = nw;
         }
       }
@@ -944,15 +982,17 @@ __global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p
 #pragma unroll
       for (int w = 0; w < kStemThreads / 64; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
       const float m = Nn > 0.f ? S / Nn : 0.f;
-      float M2 = 0.f;
+      float M2 = 0.f, sdd = 0.f;
 #pragma unroll
       for (int w = 0; w < kStemThreads / 64; ++w) {
         const float c = red[(w * 64 + tid) * 3 + 2];
         if (c > 0.f) {
           const float d = red[(w * 64 + tid) * 3] / c - m;
           M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+          sdd += c * d;
         }
       }
+      if (Nn > 0.f) M2 -= sdd * sdd / Nn;
       float* stp = p.stats + ((long)b * 64 + tid) * 2;
       stp[0] = S;
       stp[1] = M2;
@@ -972,6 +1012,230 @@ __global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p
     // the next halo's LDS-DMA (issued before the stores) has landed; make it visible
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStemStores) : "memory");
     __syncthreads();
+  }
+}
+
+// Persistent stem forward, direct-store variant for 16-wide 512-voxel boxes (bd x bh = 32).
+// No C tile: the weight columns are ordered so that lane r_lane of a wave holds channels
+// (2 r_lane, 2 r_lane + 1) of each of its rows, so the 32 lanes of a half-wave write one
+// voxel's 64 channels (128 contiguous bytes) with ONE buffer_store_dword, addressed by a
+// per-lane voffset (2 variants), a wave-uniform soffset and an immediate offset: no VALU
+// address math, no LDS round trip, one barrier per box.  The halo arrives by buffer LDS-DMA
+// (out-of-range voffset = zero padding); weights stay in VGPRs; BatchNorm partials are
+// accumulated over all boxes of the workgroup (shifted sums) and written as ONE stats row
+// per workgroup (rows >= gridDim.x are zeroed: count 0).
+constexpr int kSDThreads = 512;
+constexpr int kSDHaloRows = kHaloMax;                         // 1152 rows (18 x 64)
+constexpr int kSDHaloBytes = kSDHaloRows * 16;
+constexpr int kSDLds = 2 * kSDHaloBytes + 8 * 64 * 3 * 4;     // halo x2 + stats reduction
+constexpr uint32_t kOOB = 0x80000000u;                         // voffset past num_records
+
+template <int LBD, int LBH>
+__global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
+                                                                        uint32_t xbytes, uint32_t ybytes) {
+  static_assert(LBD + LBH == 5, "512-voxel boxes");
+  constexpr int bd = 1 << LBD, bh = 1 << LBH, bw = 16;
+  constexpr int HH = bh + 2, HW = bw + 2, HV = (bd + 2) * HH * HW;
+  constexpr int NP = (HV + kSDThreads - 1) / kSDThreads;  // halo pieces per thread
+  static_assert(HV <= kSDHaloRows, "halo fits");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* red = reinterpret_cast<float*>(lds + 2 * kSDHaloBytes);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR math)
+  const int r_lane = lane & 31, hsel = lane >> 5;
+  const int D = p.D, H = p.H, W = p.W;
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x0, 0, xbytes, 0x00020000);
+  const auto yr = __builtin_amdgcn_make_buffer_rsrc(p.y0, 0, ybytes, 0x00020000);
+
+  // weights: B fragments of all 14 k-steps in registers
+  s16x8_t wb[kStemSteps][2];
+  {
+    const bf16_t* wg = (const bf16_t*)p.w;
+#pragma unroll
+    for (int st = 0; st < kStemSteps; ++st) {
+      wb[st][0] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + r_lane) * 16 + hsel * 8);
+      wb[st][1] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
+    }
+  }
+  float bias_l[2] = {0.f, 0.f};
+  if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
+  // halo rows of the two 32-row MFMA tiles (perm32 layout)
+  int hb16[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int r = wave * 64 + mt * 32 + perm32(r_lane);
+    const int rd = r >> (LBH + 4), rh = (r >> 4) & (bh - 1), rw = r & 15;
+    hb16[mt] = ((rd * HH + rh) * HW + rw) * 16;
+  }
+  // halo pieces of this thread: relative source offset (bytes) and packed coordinates
+  int prel[NP], pco[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int hv = tid + i * kSDThreads;
+    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+    prel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
+    pco[i] = hv < HV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
+  }
+  // store voffsets: rows x = perm32((e & 3) + 8 g + 4 hsel) have x & 15 = 4 g + (e & 3) and
+  // x >> 4 = (g in {1, 2}) ^ hsel
+  const uint32_t vb0 = r_lane * 4, vb1 = r_lane * 4 + (uint32_t)W * 128;
+  const uint32_t vA = hsel ? vb1 : vb0;  // g = 0, 3
+  const uint32_t vB = hsel ? vb0 : vb1;  // g = 1, 2
+
+  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    const int nbw = p.nbw, nbh = p.nbh, nbd = p.nbd;
+    int q = b;
+    const int bwi = q % nbw; q /= nbw;
+    const int bhi = q % nbh; q /= nbh;
+    const int bdi = q % nbd;
+    n = q / nbd;
+    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
+  };
+  auto stage = [&](int b, int buf) {
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const int base16 = ((((n * D + d0) * H + h0) * W) + w0) * 16;
+    const bool inner = d0 >= 1 && d0 + bd < D && h0 >= 1 && h0 + bh < H && w0 >= 1 && w0 + bw < W;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      if (wave * 64 + i * kSDThreads >= HV) break;  // whole wave past the halo (uniform)
+      uint32_t voff = (uint32_t)(base16 + prel[i]);
+      const int c = pco[i];
+      if (c < 0) {
+        voff = kOOB;
+      } else if (!inner) {
+        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
+        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (LDS_AS void*)(lds + buf * kSDHaloBytes + (wave * 64 + i * kSDThreads) * 16),
+                                           16, voff, 0, 0, 0);
+    }
+  };
+
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2] = {0.f, 0.f};
+  float cnt = 0.f;
+  bool first = true;
+  int b = blockIdx.x;
+  if (b < nbox) stage(b, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
+    // halo(b) has landed for this wave (vmcnt above / at the loop end); barrier: for all
+    // waves, and every wave is done reading the buffer the next DMA overwrites
+    __syncthreads();
+    const int bn = b + gridDim.x;
+    if (bn < nbox) stage(bn, (it + 1) & 1);
+    const char* hl = lds + (it & 1) * kSDHaloBytes;
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];
+    {
+      int hs16 = hsel * 16;
+      asm volatile("" : "+v"(hs16));
+      auto load_a = [&](int st, s16x8_t (&a)[2]) {
+        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
+        const int off16 = o0 * 16 + hs16 * (o1 - o0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + off16);
+      };
+      s16x8_t abuf[2][2];
+      load_a(0, abuf[0]);
+#pragma unroll
+      for (int st = 0; st < kStemSteps; ++st) {
+        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
+          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // ---- epilogue: direct stores + shifted BN sums ----
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const bool full = d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
+    if (first) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(acc[0][nt][0], r_lane, 64);
+      first = false;
+    }
+    const int bv = ((n * D + d0) * H + h0) * W + w0;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int R0 = wave * 4 + mt * 2;          // even (rd, rh) linear index of the tile
+      const int rd0 = R0 >> LBH, rh0 = R0 & (bh - 1);
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (rd0 * H + rh0) * W) * 128u);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int g = e >> 2, rw = 4 * g + (e & 3);
+        const bool gB = (g == 1 || g == 2);
+        const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
+        uint32_t voff = gB ? vB : vA;
+        float e0 = v0 - K[0], e1 = v1 - K[1];
+        if (!full) {  // uniform branch: boundary boxes only
+          const int xh = (gB ? 1 : 0) ^ hsel;
+          const bool valid = (d0 + rd0 < D) & (h0 + rh0 + xh < H) & (w0 + rw < W);
+          voff = valid ? voff : kOOB;
+          e0 = valid ? e0 : 0.f;
+          e1 = valid ? e1 : 0.f;
+          cnt += valid ? 1.f : 0.f;
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so + rw * 128, 0);
+        s1[0] += e0; s2[0] += e0 * e0;
+        s1[1] += e1; s2[1] += e1 * e1;
+      }
+    }
+    if (full) cnt += 32.f;
+    // the next halo's DMA was issued before this box's 32 stores
+    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  }
+  if (!p.stats) return;
+  // per wave (lanes r_lane and r_lane + 32 share channels and K): S = sum d + n K,
+  // M2 = sum d^2 - (sum d)^2 / n; then Chan across the 8 waves
+  const float nw = cnt + __shfl_xor(cnt, 32, 64);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    s1[nt] += __shfl_xor(s1[nt], 32, 64);
+    s2[nt] += __shfl_xor(s2[nt], 32, 64);
+    if (hsel == 0) {
+      float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
+      rp[0] = s1[nt] + nw * K[nt];
+      rp[1] = nw > 0.f ? s2[nt] - s1[nt] * s1[nt] / nw : 0.f;
+      rp[2] = nw;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float S = 0.f, Nn = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
+    const float m = Nn > 0.f ? S / Nn : 0.f;
+    float M2 = 0.f, sdd = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const float c = red[(w * 64 + tid) * 3 + 2];
+      if (c > 0.f) {
+        const float d = red[(w * 64 + tid) * 3] / c - m;
+        M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+        sdd += c * d;
+      }
+    }
+    if (Nn > 0.f) M2 -= sdd * sdd / Nn;
+    float* st = p.stats + ((long)blockIdx.x * 64 + tid) * 2;
+    st[0] = S;
+    st[1] = M2;
+    float* cnts = p.stats + (long)mrows * 128;  // row counts after the [mrows][64][2] block
+    if (tid == 0) cnts[blockIdx.x] = Nn;
+    // zero this workgroup's share of the rows past gridDim.x
+    for (int r = blockIdx.x + gridDim.x; r < mrows; r += gridDim.x) {
+      p.stats[((long)r * 64 + tid) * 2] = 0.f;
+      p.stats[((long)r * 64 + tid) * 2 + 1] = 0.f;
+      if (tid == 0) cnts[r] = 0.f;
+    }
   }
 }
 
@@ -1220,6 +1484,16 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const long xbytes = (long)N * D * H * W * 16, ybytes = (long)N * D * H * W * 128;
+  const bool direct = b.lbw == 4 && b.lbd + b.lbh == 5 && (b.lbd == 2 || b.lbd == 3) && ybytes < (long)kOOB;
+  if (direct) {
+    const int grid = std::min(nbox, ncu);
+    auto kern = b.lbd == 2 ? stem_fwd_direct_kernel<2, 3> : stem_fwd_direct_kernel<3, 2>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSDLds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThreads), kSDLds, s, p, nbox, nbox, (uint32_t)xbytes,
+                       (uint32_t)ybytes);
+    PCMS_CHECK_LAUNCH();
   }
   if (b.lbd == 2 && b.lbh == 3 && b.lbw == 4) {
     (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<2, 3, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kStemLds);

@@ -498,9 +498,11 @@ __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, c
   }
   if (!stats) return;
   const float m = cntv ? s1 / cntv : 0.f;
+  float sd = 0.f;
 #pragma unroll
   for (int i = 0; i < KPT; ++i)
-    if (v0 + vl + i * NV < nvox) s2 += (xs[i] - m) * (xs[i] - m);
+    if (v0 + vl + i * NV < nvox) { s2 += (xs[i] - m) * (xs[i] - m); sd += xs[i] - m; }
+  if (cntv) s2 -= sd * sd / cntv;  // deviations about the rounded mean
   red[vl][cl][0] = s1;
   red[vl][cl][1] = s2;
   red[vl][cl][2] = (float)cntv;
@@ -509,14 +511,16 @@ __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, c
     float S = 0.f, Nn = 0.f;
     for (int k = 0; k < NV; ++k) { S += red[k][cl][0]; Nn += red[k][cl][2]; }
     const float mb = Nn > 0.f ? S / Nn : 0.f;
-    float M2 = 0.f;
+    float M2 = 0.f, sdd = 0.f;
     for (int k = 0; k < NV; ++k) {
       const float n = red[k][cl][2];
       if (n > 0.f) {
         const float d = red[k][cl][0] / n - mb;
         M2 += red[k][cl][1] + n * d * d;
+        sdd += n * d;
       }
     }
+    if (Nn > 0.f) M2 -= sdd * sdd / Nn;
     stats[((long)blockIdx.x * C + c) * 2] = S;
     stats[((long)blockIdx.x * C + c) * 2 + 1] = M2;
     if (cl == 0 && blockIdx.y == 0) stats[(long)gridDim.x * C * 2 + blockIdx.x] = Nn;
