@@ -1,15 +1,26 @@
 #!/bin/bash
-# One GPU session: op tests, parity tests, bench, kernel profile.  Usage: tests/gpu_check.sh TAG
+# One GPU session: op + parity tests, smoke, bench, kernel-trace profile.
+# Usage: tests/gpu_check.sh TAG [--no-tests]
+# Every GPU step has its own time limit; the script stops at the first step that aborts,
+# faults or times out (exit status > 1), so nothing more runs on a sick GPU.
 TAG=${1:-run}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_ops.py tests/test_gpu_parity.py -q -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1
-rc=$?
-echo "tests_rc=$rc"; tail -3 gpurun_out/tests_$TAG.log
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench_$TAG.log 2>&1
-rc=$?
-echo "bench_rc=$rc"; tail -1 gpurun_out/bench_$TAG.log
-if [ $rc -ne 0 ]; then exit $rc; fi
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 5 > gpurun_out/prof_$TAG.log 2>&1
-echo "prof_rc=$?"
+stop_if_bad() {  # $1 = step name, $2 = status
+  if [ "$2" -gt 1 ]; then echo "$1 ended with status $2: stopping"; exit "$2"; fi
+}
+if [ "$2" != "--no-tests" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1
+  rc=$?
+  echo "tests_rc=$rc"; grep -E "passed|failed|error" gpurun_out/tests_$TAG.log | tail -3
+  stop_if_bad tests $rc
+fi
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
+rc=$?; echo "smoke_rc=$rc"; tail -1 gpurun_out/smoke_$TAG.log; stop_if_bad smoke $rc
+timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.log 2>&1
+rc=$?; echo "bench_rc=$rc"; tail -1 gpurun_out/bench_$TAG.log; stop_if_bad bench $rc
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run \
+  --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline \
+  > gpurun_out/prof_$TAG.log 2>&1
+rc=$?; echo "prof_rc=$rc"; tail -1 gpurun_out/prof_$TAG.log
