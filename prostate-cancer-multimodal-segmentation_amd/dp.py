@@ -1,0 +1,114 @@
+"""Data parallelism for the U-Net step: one process per GPU, ``torch.distributed`` with
+the "nccl" (= RCCL on ROCm) backend; gloo on CPU for the tests.
+
+The reference has no multi-GPU code.  The semantics chosen are those of
+``DistributedDataParallel(model, broadcast_buffers=True)`` around the reference step
+(utils/trainer.py:183-192), restated for the tests by
+``oracle.unet3d_cpu.dp_step_simulated``:
+
+* rank 0's BatchNorm running buffers are broadcast before every forward (ONE broadcast of
+  the engine's flat BN buffer);
+* every rank runs forward / loss / backward on its own volumes (per-replica BN statistics
+  and per-replica global Dice);
+* the flat fp32 gradient is summed over ranks; the 1/world mean is folded into Adam.
+
+The gradient all-reduce is bucketed and overlapped with the backward: the engine reports
+each module's gradient range as soon as its backward has written it (decoder first, the
+stem last) and a bucket is launched asynchronously (``async_op=True``: the RCCL kernel is
+ordered after the producing kernels of the compute stream, then runs beside the rest of
+the backward).  ``finish()`` makes the compute stream wait for every bucket before Adam.
+Buckets are contiguous slices of the flat gradient, so every collective is one large
+message: xGMI rings are per-link bound, so few large transfers beat many small ones.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+# top-level modules in the order the engine's backward finishes their gradients
+BACKWARD_ORDER = ("outc", "up4", "up3", "up2", "up1", "down4", "down3", "down2", "down1", "inc")
+
+
+def module_grad_ranges(model) -> Dict[str, Tuple[int, int]]:
+    """Element range [lo, hi) of each top-level module's parameters in the flat buffer
+    (``model.parameters()`` order = the engine's flat layout).  ``model``: a module, or
+    an iterable of (name, tensor) pairs in parameter order."""
+    named = model.named_parameters() if hasattr(model, "named_parameters") else model
+    ranges: Dict[str, List[int]] = {}
+    off = 0
+    for name, p in named:
+        top = name.split(".", 1)[0]
+        r = ranges.setdefault(top, [off, off])
+        if r[1] != off:
+            raise ValueError(f"parameters of {top} are not contiguous in the flat buffer")
+        off += p.numel()
+        r[1] = off
+    return {k: (v[0], v[1]) for k, v in ranges.items()}
+
+
+class GradSync:
+    """Bucketed, backward-overlapped all-reduce (sum) of a flat gradient buffer.
+
+    ``ready(lo, hi)`` declares flat_g[lo:hi] final.  Ranges arrive in descending order
+    and tile the buffer (hi == the previous range's lo), as the U-Net backward produces
+    them (outc and up4 sit at the end of the buffer, inc at offset 0).  Pending ranges are
+    launched once they reach ``bucket_elems`` (default 16 Mi elements = 64 MB fp32);
+    ``finish()`` launches the rest, waits, and returns the 1/world scale Adam applies.
+    """
+
+    def __init__(self, flat_g: torch.Tensor, group=None, bucket_elems: int = 16 << 20, overlap: bool = True):
+        self.flat_g = flat_g
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.bucket_elems = int(bucket_elems)
+        self.overlap = overlap
+        self._works: List = []
+        self._lo: Optional[int] = None   # pending range [lo, hi)
+        self._hi: Optional[int] = None
+        self._next_hi = flat_g.numel()   # the next ready range must end here
+        self.launched: List[Tuple[int, int]] = []   # buckets of the current step (tests / logs)
+
+    def broadcast_buffers(self, flat_bn: torch.Tensor):
+        """DDP broadcast_buffers: every rank takes rank 0's BatchNorm running statistics."""
+        dist.broadcast(flat_bn, src=0, group=self.group)
+
+    def _fresh_step(self):
+        if self._next_hi == self.flat_g.numel() and not self._works:
+            self.launched = []
+
+    def ready(self, lo: int, hi: int):
+        if hi != self._next_hi or not 0 <= lo <= hi:
+            raise RuntimeError(f"gradient range [{lo}, {hi}) out of order (expected one ending at {self._next_hi})")
+        self._fresh_step()
+        self._next_hi = lo
+        if self._hi is None:
+            self._hi = hi
+        self._lo = lo
+        if self.overlap and self._hi - self._lo >= self.bucket_elems:
+            self._launch()
+
+    def _launch(self):
+        if self._hi is not None and self._hi > self._lo:
+            lo, hi = self._lo, self._hi
+            self._works.append(dist.all_reduce(self.flat_g[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
+            self.launched.append((lo, hi))
+        self._lo = self._hi = None
+
+    def finish(self) -> float:
+        """Launch what is pending (a range the backward did not report is reduced too),
+        make the caller wait for every bucket, reset for the next step."""
+        self._fresh_step()
+        if self._next_hi != 0:
+            if self._hi is None:
+                self._hi = self._next_hi
+            self._lo = 0
+            self._next_hi = 0
+        self._launch()
+        for w in self._works:
+            w.wait()
+        self._works = []
+        self._next_hi = self.flat_g.numel()
+        return 1.0 / self.world

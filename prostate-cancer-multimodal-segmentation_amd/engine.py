@@ -24,6 +24,7 @@ import torch
 
 from . import _lib
 from ._lib import BF16, F32, call, query
+from .dp import module_grad_ranges
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
@@ -108,6 +109,7 @@ class UNetEngine:
         self.saved_epoch = -1
         self.act_ckpt = False
         self.wgrad_target = 512
+        self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
         self._flatten()
         for bn in self.bns:
             c = bn.c
@@ -147,6 +149,12 @@ class UNetEngine:
         self.flat_p, self.flat_g, self.flat_bn = flat, gflat, bflat
         self._flat_ptrs = [p.data_ptr() for p in params]
         self._dirty = True
+        self.grad_ranges = module_grad_ranges(self.model)
+
+    def _grads_done(self, module: str):
+        """Report a finished module gradient range to the data-parallel hook (dp.GradSync)."""
+        if self.grad_ready is not None:
+            self.grad_ready(*self.grad_ranges[module])
 
     def sync_params(self):
         """Re-flatten if a module op (``.to()``, ``.cuda()``, param reassignment) replaced
@@ -405,6 +413,7 @@ class UNetEngine:
         D, H, W = S[0]
         call("pcms_head_bwd", self.code, b["d0_a2"], dlogits, oc.weight, b["gH"], oc.weight.grad, oc.bias.grad,
              D * H * W, N, self.ncls)
+        self._grads_done("outc")
         g = b["gH"]
         # decoder, last block first
         for i in reversed(range(4)):
@@ -424,6 +433,7 @@ class UNetEngine:
             dx_ = (S[l][2] - 2 * S[l + 1][2]) // 2
             call("pcms_box_channel_sum", self.code, gu, up.bias.grad, N, *S[l], C[l], dz, dy_, dx_,
                  2 * S[l + 1][0], 2 * S[l + 1][1], 2 * S[l + 1][2])
+            self._grads_done(f"up{i + 1}")
             gnext = b["gx4"] if i == 0 else b[f"gA{l + 1}"]
             call("pcms_convt_dgrad", self.code, gu, dpack, gnext, N, *S[l + 1], up.in_channels, up.out_channels,
                  *S[l])
@@ -434,9 +444,11 @@ class UNetEngine:
             acts = {"y1": b[f"e{l}_y1"], "a1": b[f"e{l}_a1"], "y2": b[f"e{l}_y2"]}
             if l == 0:
                 self._block_bwd(blk, b["gx0"], acts, b["xin"], self.cp, None, 0, None, None, 0, N, S[0], 0)
+                self._grads_done("inc")
             else:
                 gp = b[f"gU{l}"]
                 self._block_bwd(blk, b[f"gx{l}"], acts, b[f"pool{l}"], C[l - 1], None, 0, gp, None, C[l - 1], N,
                                 S[l], l)
+                self._grads_done(f"down{l}")
                 call("pcms_maxpool_bwd", self.code, b[f"e{l - 1}_x"], gp, b[f"gx{l - 1}"], N, *S[l - 1], C[l - 1])
         self.saved_epoch = -1

@@ -13,7 +13,9 @@ The per-batch step of utils/trainer.py:179-195 becomes ``Trainer.step(batch) -> 
 Data parallel (one process per GPU, ``torch.distributed`` with the "nccl" = RCCL backend):
 every rank runs the step on its shard; rank 0's BatchNorm running buffers are broadcast
 before the forward (DistributedDataParallel(broadcast_buffers=True) semantics) and the
-flat fp32 gradient is summed with ONE all-reduce, the 1/world mean folded into Adam.
+flat fp32 gradient is summed by a few large bucketed all-reduces that run beside the
+backward as it finishes each module (``pcms_amd.dp.GradSync``), the 1/world mean folded
+into Adam.
 BatchNorm statistics and the global Dice stay per replica (plain BatchNorm3d).
 
 Config keys follow utils/trainer.py:40-49 (``device``, ``learning_rate``, ``batch_size``,
@@ -29,6 +31,7 @@ from typing import Iterable, Optional
 import torch
 import torch.distributed as dist
 
+from ..dp import GradSync
 from ..models.unet3d import UNet3D
 from ..optim import FlatAdam
 from .losses import BCEDiceLoss, DiceLoss
@@ -53,6 +56,7 @@ class BaseTrainer:
         if self.val_loader is None and config.get("validation", False):
             self.val_loader = self._create_dataloader("test")
         self._copy_stream = None
+        self._sync = None
         if self.distributed:
             self._broadcast_params()
         if config.get("save_dir"):
@@ -89,6 +93,13 @@ class BaseTrainer:
         loss = self.step_async(batch)
         return loss.item()
 
+    def _grad_sync(self):
+        eng = self.model.engine()
+        if self._sync is None or self._sync.flat_g is not eng.flat_g:
+            self._sync = GradSync(eng.flat_g, bucket_elems=self.config.get("dp_bucket_elems", 16 << 20),
+                                  overlap=self.config.get("dp_overlap", True))
+        return eng, self._sync
+
     def step_async(self, batch) -> torch.Tensor:
         """One training step; returns the loss as a device tensor (no host sync)."""
         images = batch["image"].to(self.device, non_blocking=True)
@@ -96,14 +107,18 @@ class BaseTrainer:
         self.model.train()
         self.optimizer.zero_grad()
         if self.distributed:
-            dist.broadcast(self.model.engine().flat_bn, src=0)
-        outputs = self.model(images)
-        loss = self.criterion(outputs, labels)
-        loss.backward()
+            eng, sync = self._grad_sync()
+            sync.broadcast_buffers(eng.flat_bn)
+            eng.grad_ready = sync.ready   # buckets launch as the backward finishes each module
+        try:
+            outputs = self.model(images)
+            loss = self.criterion(outputs, labels)
+            loss.backward()
+        finally:
+            if self.distributed:
+                eng.grad_ready = None
         if self.distributed:
-            eng = self.model.engine()
-            dist.all_reduce(eng.flat_g, op=dist.ReduceOp.SUM)
-            self.optimizer.grad_scale = 1.0 / self.world_size
+            self.optimizer.grad_scale = sync.finish()
         self.optimizer.step()
         return loss.detach()
 
