@@ -60,7 +60,7 @@ def stem_roofline(tr, N, spatial, reps):
     rows = L.query("pcms_conv3_mblocks", N, D, H, W)
     stats = torch.empty(rows * (64 * 2 + 1), device="cuda")
     dw = torch.zeros(64 * 5 * 27, device="cuda")
-    dwt = torch.empty(27 * 64 * eng.cp, device="cuda")
+    dwt = torch.empty(max(27 * 64 * eng.cp, L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5)), device="cuda")
 
     eng._ensure_packs()
 
@@ -73,7 +73,7 @@ def stem_roofline(tr, N, spatial, reps):
 
     def wgrad(s):
         if eng.stem_fast:
-            L.call("pcms_stem_wgrad", s[0], s[2], dw, 5, N, D, H, W, 256)
+            L.call("pcms_stem_wgrad", s[0], s[2], dw, dwt, 5, N, D, H, W, 256)
         else:
             L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
 

@@ -55,8 +55,12 @@ int pcms_stem_pack_elems(void);
 int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
                   int N, int D, int H, int W, hipStream_t s);
-int pcms_stem_wgrad(const void* x, const void* dy, float* dw, int cin_w, int N, int D, int H, int W,
-                    int target_wgs, hipStream_t s);
+/* dw [64][cin_w][27] += stem weight gradient.  D % 4 == H % 4 == W % 16 == 0: streaming
+ * kernel (one partial row per CU in ws, then a fixed-order sum), ws =
+ * pcms_stem_wgrad_ws_floats(...) floats; other shapes: tiled kernel (ws unused).          */
+int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w);
+int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H,
+                    int W, int target_wgs, hipStream_t s);
 /* stats layout as pcms_conv3_fwd with rows = pcms_split_epilogue_rows(nvox)              */
 int pcms_split_epilogue_rows(long nvox);
 int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0,

@@ -25,7 +25,8 @@ SIGNATURES = {
     "pcms_stem_pack_elems": "",
     "pcms_stem_pack": "ppis",
     "pcms_stem_fwd": "pppppiiiis",
-    "pcms_stem_wgrad": "pppiiiiiis",
+    "pcms_stem_wgrad_ws_floats": "iiiii",
+    "pcms_stem_wgrad": "ppppiiiiiis",
     "pcms_split_epilogue_rows": "l",
     "pcms_split_epilogue": "ippppipils",
     "pcms_bn_ws_doubles": "i",

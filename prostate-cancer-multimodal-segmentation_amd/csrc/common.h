@@ -82,6 +82,34 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Raw buffer descriptor (4 SGPRs): base, stride 0, num_records bytes (out-of-range offsets
+// read 0), dword3 as __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000) builds it.
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+__device__ __forceinline__ i32x4_t buffer_desc(const void* base, uint32_t num_bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4_t d;
+  d[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  d[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xffff);
+  d[2] = __builtin_amdgcn_readfirstlane((int)num_bytes);
+  d[3] = 0x00020000;
+  return d;
+}
+
+// 16-byte LDS-DMA (buffer_load_dwordx4 ... lds): lane l's 16 bytes from rsrc at
+// voff + soff land at LDS byte lds_base + 16 l (lds_base wave-uniform).  Issued from inline
+// asm so the compiler's waitcnt pass does not see it: it would otherwise wait vmcnt(0)
+// before the next LDS read of ANY buffer (killing a multi-stage ring).  The caller retires
+// these with explicit s_waitcnt vmcnt(N) + a barrier before reading the data.
+__device__ __forceinline__ void dma16(i32x4_t rsrc, uint32_t lds_base, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rsrc), "s"(soff)
+               : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 #define PCMS_CHECK_LAUNCH() return (int)hipGetLastError()
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

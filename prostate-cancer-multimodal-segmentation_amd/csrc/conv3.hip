@@ -1391,6 +1391,203 @@ __global__ void __launch_bounds__(256, 1) stem_wgrad_kernel(const bf16_t* x, con
   }
 }
 
+// Streaming stem weight gradient (the HBM-bound hot case: D % 4 == H % 4 == W % 16 == 0).
+// dW[co][c][t] = sum_v dy[v][co] x[v + t][c]: GEMM with M = 64 co, N = 224 (tap, channel)
+// columns, K = voxels.  Persistent: one 4-wave workgroup per CU walks 4x4x16 voxel boxes
+// b = blockIdx.x + k gridDim.x.  Each box's dy tile (256 voxels x 128 B) and x halo
+// (6x6x18 rows x 16 B) arrive by buffer LDS-DMA (inline asm, see dma16) into a 3-slot ring:
+// two boxes in flight while one computes, counted vmcnt + raw s_barrier, every source
+// offset a per-thread constant + the box base.  Wave w owns k-steps w, w + 4, w + 8, w + 12
+// of every box and ALL 14 output tiles (2 co x 7 column tiles, accumulators in AGPRs), so
+// each A / B fragment is read from LDS exactly once per box (ds_read_b64_tr_b16 transposes
+// both operands) and the next k-step's fragments are read during this one's 14 MFMAs.
+// Flush: one fp32 partial row [64][cin_w][27] per workgroup (plain stores), summed into dw
+// by stem_wgrad_reduce_kernel (deterministic, no atomics).
+constexpr int kSWT = 256;                                  // 4 waves, one per SIMD
+constexpr int kSWBV = 256;                                 // 4 x 4 x 16 voxels
+constexpr int kSWHV = 6 * 6 * 18;                          // 648 halo rows
+constexpr int kSWHRows = 704;                              // halo rows written (11 x 64)
+constexpr int kSWBuf = kSWBV * 128 + kSWHRows * 16;        // 43 KiB per ring slot
+constexpr int kSWLds = 3 * kSWBuf;                         // 129 KiB
+static_assert(kSWLds >= 64 * 224 * 4, "flush tile fits in the ring");
+
+__global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t* x, const bf16_t* dy, float* part,
+                                                                    int N, int D, int H, int W, int cin_w,
+                                                                    uint32_t xbytes, uint32_t dybytes) {
+  constexpr int BD = 4, BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
+  extern __shared__ __attribute__((aligned(16))) char swl[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hsel = lane >> 5;
+  const int nbw = W / BW, nbh = H / BH, nbd = D / BD;
+  const int nbox = N * nbd * nbh * nbw;
+  const i32x4_t xr = buffer_desc(x, xbytes);
+  const i32x4_t dr = buffer_desc(dy, dybytes);
+
+  // per-thread DMA source offsets relative to the box origin (constant over boxes)
+  uint32_t dyrel[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int pc = tid + i * kSWT;
+    const int r = pc >> 3, q = pc & 7;
+    const int ql = q ^ (((r >> 1) & 1) << 2);  // dy_off_bf16: 64-B halves swapped on odd row pairs
+    const int rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
+    dyrel[i] = (uint32_t)(((rd * H + rh) * W + rw) * 128 + ql * 16);
+  }
+  const int nxp = wave < 3 ? 3 : 2;  // halo pieces of this wave: rows wave*64 + lane + 256 i
+  int xrel[3], xco[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int hv = wave * 64 + lane + i * kSWT;
+    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+    xrel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
+    xco[i] = hv < kSWHV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
+  }
+  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    int q = b;
+    const int bwi = q % nbw; q /= nbw;
+    const int bhi = q % nbh; q /= nbh;
+    const int bdi = q % nbd;
+    n = q / nbd;
+    d0 = bdi * BD; h0 = bhi * BH; w0 = bwi * BW;
+  };
+  auto stage = [&](int b, int slot) {
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const int vb = ((n * D + d0) * H + h0) * W + w0;
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(swl) + slot * kSWBuf + wave * 64 * 16);
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)vb * 128u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
+    const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= nxp) break;
+      uint32_t voff = (uint32_t)(vb * 16 + xrel[i]);
+      const int c = xco[i];
+      if (c < 0) {
+        voff = kOOB;
+      } else if (!inner) {
+        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
+        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
+      }
+      dma16(xr, lb + kSWBV * 128 + i * kSWT * 16, voff, 0);
+    }
+  };
+
+  const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+  f32x16_t acc[2][7];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // lane offsets of the tr reads, with the wave's k-step offset folded in (k-step s = wave +
+  // 4 i is box row (rd = i, rh = wave): dy rows at s * 2048, halo rows at (i HH + wave) HW)
+  const int aoff0 = dy_off_bf16(8 * hsel + qq, g * 16 + pp * 4) + wave * 2048;
+  const int aoff1 = dy_off_bf16(8 * hsel + qq, 32 + g * 16 + pp * 4) + wave * 2048;
+  int boff[7];  // column tile j: taps 4 j + 2 g + (pp >> 1), channels 4 (pp & 1) .. + 3
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+    boff[j] = kSWBV * 128 + (8 * hsel + qq + tap_off(4 * j + 2 * g + (pp >> 1), HH, HW) + wave * HW) * 16 + (pp & 1) * 8;
+  auto compute = [&](const char* buf) {
+    uint32_t pa0 = lds_addr(buf) + aoff0, pa1 = lds_addr(buf) + aoff1, pb[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) pb[j] = lds_addr(buf) + boff[j];
+    asm volatile("" : "+v"(pa0), "+v"(pa1), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]),
+                 "+v"(pb[5]), "+v"(pb[6]));
+    auto tr = [](uint32_t p, int off) {
+      return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(uintptr_t)(p + off));
+    };
+    auto cat = [](s16x4_t lo, s16x4_t hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); };
+    auto load = [&](int i, s16x8_t (&a)[2], s16x8_t (&bq)[7]) {
+      const int dyb = i * 4 * 2048;
+      const int hrb = i * HH * HW * 16;
+      a[0] = cat(tr(pa0, dyb), tr(pa0, dyb + 512));
+      a[1] = cat(tr(pa1, dyb), tr(pa1, dyb + 512));
+#pragma unroll
+      for (int j = 0; j < 7; ++j) bq[j] = cat(tr(pb[j], hrb), tr(pb[j], hrb + 64));
+    };
+    s16x8_t a[2][2], bq[2][7];
+    load(0, a[0], bq[0]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i + 1 < 4) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct][j] = mfma(a[i & 1][ct], bq[i & 1][j], acc[ct][j]);
+    }
+  };
+
+  int b = blockIdx.x;
+  if (b < nbox) stage(b, 0);
+  if (b + (int)gridDim.x < nbox) stage(b + gridDim.x, 1);
+  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
+    // retire box b's DMA (box b + G may stay in flight), then barrier: every wave's share
+    // of box b has landed and every wave is done reading the slot refilled below
+    if (b + (int)gridDim.x < nbox) {
+      if (wave < 3) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int b2 = b + 2 * gridDim.x;
+    if (b2 < nbox) stage(b2, (it + 2) % 3);
+    compute(swl + (it % 3) * kSWBuf);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // flush: the 4 waves' partial tiles summed in LDS [co][224 cols] (fixed order)
+  float* red = reinterpret_cast<float*>(swl);
+  for (int pass = 0; pass < 4; ++pass) {
+    if (wave == pass) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int co = ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+            float* dst = red + co * 224 + j * 32 + (lane & 31);
+            if (pass == 0) *dst = acc[ct][j][e];
+            else *dst += acc[ct][j][e];
+          }
+    }
+    __syncthreads();
+  }
+  const int total = 64 * cin_w * 27;
+  float* prow = part + (long)blockIdx.x * total;
+  for (int i = tid; i < total; i += kSWT) {
+    const int t = i % 27, c = (i / 27) % cin_w, co = i / (27 * cin_w);
+    prow[i] = red[co * 224 + t * 8 + c];
+  }
+}
+
+// dw[o] += sum over the workgroup partial rows (fixed order).  Block = 32 outputs x 8 row
+// groups: 32 independent 128-B row segments in flight per thread group, LDS combine.
+__global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* part, int rows, int total, float* dw) {
+  __shared__ float red[8][32];
+  const int ol = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int o = blockIdx.x * 32 + ol;
+  float s = 0.f;
+  if (o < total) {
+#pragma unroll 8
+    for (int r = rg; r < rows; r += 8) s += part[(long)r * total + o];
+  }
+  red[rg][ol] = s;
+  __syncthreads();
+  if (rg == 0 && o < total) {
+    float t = 0.f;
+#pragma unroll
+    for (int g2 = 0; g2 < 8; ++g2) t += red[g2][ol];
+    dw[o] += t;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1505,10 +1702,47 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
   PCMS_CHECK_LAUNCH();
 }
 
-// dw [64][cin_w][27] fp32 += stem weight gradient (x: 8-channel bf16 input, dy: 64 ch)
-int pcms_stem_wgrad(const void* x, const void* dy, float* dw, int cin_w, int N, int D, int H, int W,
+static int device_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
+
+static bool stem_wgrad_streams(int N, int D, int H, int W) {
+  return D % 4 == 0 && H % 4 == 0 && W % 16 == 0 && (long)N * D * H * W * 128 < (1L << 31);
+}
+
+// fp32 workspace floats pcms_stem_wgrad needs (0: none)
+int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w) {
+  if (!stem_wgrad_streams(N, D, H, W)) return 0;
+  const int nbox = N * (D / 4) * (H / 4) * (W / 16);
+  return std::min(nbox, device_cus()) * 64 * cin_w * 27;
+}
+
+// dw [64][cin_w][27] fp32 += stem weight gradient (x: 8-channel bf16 input, dy: 64 ch);
+// ws: pcms_stem_wgrad_ws_floats(...) floats
+int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H, int W,
                     int target_wgs, hipStream_t s) {
-  if (cin_w > 8) return -1;
+  if (cin_w > 8 || cin_w < 1) return -1;
+  if (stem_wgrad_streams(N, D, H, W)) {
+    if (ws == nullptr) return -2;
+    const int nbox = N * (D / 4) * (H / 4) * (W / 16);
+    const int grid = std::min(nbox, device_cus());
+    const long xbytes = (long)N * D * H * W * 16, dybytes = (long)N * D * H * W * 128;
+    (void)hipFuncSetAttribute((const void*)stem_wgrad_stream_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kSWLds);
+    hipLaunchKernelGGL(stem_wgrad_stream_kernel, dim3(grid), dim3(kSWT), kSWLds, s, (const bf16_t*)x,
+                       (const bf16_t*)dy, ws, N, D, H, W, cin_w, (uint32_t)xbytes, (uint32_t)dybytes);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    const int total = 64 * cin_w * 27;
+    hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, (const float*)ws, grid,
+                       total, dw);
+    PCMS_CHECK_LAUNCH();
+  }
   Box b = choose_box(D, H, W, kSBV, kSHalo, 4, 16);
   const int nbd = cdiv(D, 1 << b.lbd), nbh = cdiv(H, 1 << b.lbh), nbw = cdiv(W, 1 << b.lbw);
   const int nbox = N * nbd * nbh * nbw;

@@ -373,7 +373,7 @@ class UNetEngine:
         # BN0/ReLU backward -> dy1 (reuse gY)
         self._bn_bwd(blk.b0, gA, acts["y1"], gY, nvox)
         if blk is self.enc[0] and self.stem_fast:
-            call("pcms_stem_wgrad", x0, gY, blk.c0.mod.weight.grad, blk.c0.cin, N, *S, 256)
+            call("pcms_stem_wgrad", x0, gY, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S, 256)
         else:
             call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gY, blk.c0.mod.weight.grad, b["dwt"], N, *S,
                  blk.c0.cout, blk.c0.cin, self.wgrad_target)

@@ -22,15 +22,18 @@ def main():
     bias = torch.zeros(64, device="cuda")
     stats = torch.empty(L.query("pcms_conv3_mblocks", N, D, H, W) * 129, device="cuda")
     dw = torch.zeros(64 * 5 * 27, device="cuda")
-    for name in ("fwd", "wgrad"):
-        if which not in ("both", name):
+    ws = torch.empty(max(1, L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5)), device="cuda")
+    for name in ("fwd", "wgrad", "calib"):
+        if which not in ("both", name) and not (which == "all"):
             continue
         def f(i):
             x, y, dy = sets[i % 3]
-            if name == "fwd":
+            if name == "calib":
+                y.copy_(dy)          # 268 MB read + 268 MB write (torch copy kernel)
+            elif name == "fwd":
                 L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W)
             else:
-                L.call("pcms_stem_wgrad", x, dy, dw, 5, N, D, H, W, 256)
+                L.call("pcms_stem_wgrad", x, dy, dw, ws, 5, N, D, H, W, 256)
         for i in range(3):
             f(i)
         torch.cuda.synchronize()
@@ -41,8 +44,22 @@ def main():
         e1.record()
         e1.synchronize()
         t = e0.elapsed_time(e1) / reps * 1e-3
-        byts = nvox * 5 * 2 + nvox * 64 * 2
+        byts = nvox * 5 * 2 + nvox * 64 * 2 if name != "calib" else 2 * nvox * 64 * 2
         print(f"stem {name}: {t * 1e6:.1f} us  {byts / t / 1e9:.0f} GB/s algorithmic", flush=True)
+    if which in ("all", "calib"):
+        x, y, dy = sets[0]
+        for i in range(3):
+            s = sets[i % 3][2].float().sum()
+        torch.cuda.synchronize()
+        src = [torch.empty(nvox * 64 // 2, dtype=torch.float32, device="cuda").fill_(1.0) for _ in range(3)]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            s = src[i % 3].sum()
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1) / reps * 1e-3
+        print(f"calib read-only sum of 268 MB: {t * 1e6:.1f} us  {nvox * 128 / t / 1e9:.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -22,7 +22,7 @@ def load(dirs, flt):
                     name = row["Kernel_Name"]
                     if flt and flt not in name:
                         continue
-                    short = name.split("(")[0][-60:]
+                    short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:70]
                     vals[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return vals
 

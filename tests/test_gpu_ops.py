@@ -419,7 +419,8 @@ def test_pack_input(dt, code):
     close(out.cpu(), exp.to(dt), 0, "pack input")
 
 
-@pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (1, (9, 10, 11)), (2, (8, 8, 4)), (1, (6, 20, 33))])
+@pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (1, (9, 10, 11)), (2, (8, 8, 4)), (1, (6, 20, 33)),
+                                 (1, (8, 12, 48)), (3, (4, 4, 16)), (1, (32, 32, 32))])
 def test_stem_fwd_wgrad_bf16(N, S):
     """Dedicated stem kernels (tap-pair packed K) vs torch conv3d on the bf16-rounded input."""
     L = _lib()
@@ -443,7 +444,8 @@ def test_stem_fwd_wgrad_bf16(N, S):
     ref.backward(dy.double())
     guard = 4096
     dw = torch.zeros(64 * 5 * 27 + guard, device=DEV)
-    L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, 5, N, *S, 64)
+    ws = torch.empty(max(1, L.query("pcms_stem_wgrad_ws_floats", N, *S, 5)), device=DEV)
+    L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, ws, 5, N, *S, 64)
     torch.cuda.synchronize()
     close(ncdhw(y.cpu()), ref.detach(), 1e-2, "stem fwd")
     mean, var = bn_moments(stats, rows, 64, N * S[0] * S[1] * S[2])
