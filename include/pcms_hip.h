@@ -30,7 +30,13 @@ int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long 
 
 /* ---- Conv3d(k=3, padding=1): models/unet3d.py:29,35 ------------------------------- */
 int pcms_conv3_chunk(int dtype);                  /* input channels per K-chunk        */
-int pcms_conv3_mblocks(int N, int D, int H, int W);/* rows of the BN partial buffer     */
+int pcms_conv3_mblocks(int N, int D, int H, int W);/* general-kernel M blocks (an upper
+                                                      bound on the BN partial rows)      */
+/* BN partial rows an unsplit pcms_conv3_fwd over sources (c0, c1) writes: the big-box
+ * bf16 kernel (8x8x16 boxes, 16-channel chunks, >= pcms_conv3_big_min_boxes boxes) writes
+ * one row per box, the general kernel pcms_conv3_mblocks rows                           */
+int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1);
+int pcms_conv3_big_min_boxes(int v);               /* set (v > 0) / query; returns old */
 /* master W [Cout][Cin][3][3][3] fp32 -> kernel pack; flip=1 builds the dgrad pack      */
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s);
 /* Y = conv(X) + bias, X = channel-concat(x0[:, :c0], x1[:, :c1]) (Up3D cat, :156),
@@ -53,6 +59,9 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
  * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32).                  */
 int pcms_stem_pack_elems(void);
 int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
+/* y = stem conv(x) + bias; BatchNorm partial moments into stats, laid out as pcms_conv3_fwd
+ * with rows = pcms_stem_fwd_rows(N, D, H, W) (one row per workgroup on the hot shapes)   */
+int pcms_stem_fwd_rows(int N, int D, int H, int W);
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
                   int N, int D, int H, int W, hipStream_t s);
 /* dw [64][cin_w][27] += stem weight gradient.  D % 4 == H % 4 == W % 16 == 0: streaming

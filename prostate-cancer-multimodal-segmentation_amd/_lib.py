@@ -19,11 +19,14 @@ SIGNATURES = {
     "pcms_pack_input": "ippiilis",
     "pcms_conv3_chunk": "i",
     "pcms_conv3_mblocks": "iiii",
+    "pcms_conv3_fwd_rows": "iiiiiii",
+    "pcms_conv3_big_min_boxes": "i",
     "pcms_conv3_pack": "ippiiis",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
     "pcms_conv3_wgrad": "ipipipppiiiiiiis",
     "pcms_stem_pack_elems": "",
     "pcms_stem_pack": "ppis",
+    "pcms_stem_fwd_rows": "iiii",
     "pcms_stem_fwd": "pppppiiiis",
     "pcms_stem_wgrad_ws_floats": "iiiii",
     "pcms_stem_wgrad": "ppppiiiiiis",

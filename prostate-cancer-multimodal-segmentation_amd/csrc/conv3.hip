@@ -19,6 +19,13 @@
 #include "common.h"
 #include "pcms_hip.h"
 #include <algorithm>
+#include <utility>
+
+// PCMS_ABL: ablation switches for the stem kernels, set only by the test-tooling build
+// (tests/kexp/Makefile) to time their parts separately; 0 in the product build.
+#ifndef PCMS_ABL
+#define PCMS_ABL 0
+#endif
 
 namespace {
 
@@ -679,15 +686,20 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
 }
 
 // dwt [27][Cout][Cin] (fp32 workspace, Cin = stored channels) -> dw [Cout][Cw][27] (+=),
-// torch OIDHW layout with the weight's own input-channel count Cw <= Cin (stem: 5 of 8)
-__global__ void wgrad_permute_kernel(const float* dwt, float* dw, int Cout, int Cin, int Cw) {
-  const long total = (long)Cout * Cw * 27;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int t = i % 27;
-    const long oc = i / 27;
-    const int ci = oc % Cw, co = oc / Cw;
-    dw[i] += dwt[((long)t * Cout + co) * Cin + ci];
+// torch OIDHW layout with the weight's own input-channel count Cw <= Cin (stem: 5 of 8).
+// Block = (co, 32 input channels): the [27][32] source tile is read as 27 coalesced 128-B
+// rows, transposed through LDS, and added to the contiguous 32 x 27 run of dw.
+__global__ void __launch_bounds__(256) wgrad_permute_kernel(const float* dwt, float* dw, int Cout, int Cin, int Cw) {
+  __shared__ float tile[27][33];
+  const int co = blockIdx.x, ci0 = blockIdx.y * 32;
+  for (int e = threadIdx.x; e < 27 * 32; e += 256) {
+    const int t = e >> 5, c = e & 31, ci = ci0 + c;
+    tile[t][c] = ci < Cw ? dwt[((long)t * Cout + co) * Cin + ci] : 0.f;
   }
+  __syncthreads();
+  float* dst = dw + ((long)co * Cw + ci0) * 27;
+  const int n = min(32, Cw - ci0) * 27;
+  for (int e = threadIdx.x; e < n; e += 256) dst[e] += tile[e % 27][e / 27];
 }
 
 // master fp32 W[Cout][Cin][27] -> packed T [chunk][27][J][CK]
@@ -1123,7 +1135,7 @@ __global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Par
     // waves, and every wave is done reading the buffer the next DMA overwrites
     __syncthreads();
     const int bn = b + gridDim.x;
-    if (bn < nbox) stage(bn, (it + 1) & 1);
+    if (bn < nbox && !(PCMS_ABL & 4)) stage(bn, (it + 1) & 1);
     const char* hl = lds + (it & 1) * kSDHaloBytes;
     f32x16_t acc[2][2];
 #pragma unroll
@@ -1132,7 +1144,7 @@ __global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Par
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];
-    {
+    if (!(PCMS_ABL & 1)) {
       int hs16 = hsel * 16;
       asm volatile("" : "+v"(hs16));
       auto load_a = [&](int st, s16x8_t (&a)[2]) {
@@ -1184,7 +1196,7 @@ __global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Par
           e1 = valid ? e1 : 0.f;
           cnt += valid ? 1.f : 0.f;
         }
-        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so + rw * 128, 0);
+        if (!(PCMS_ABL & 2)) __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so + rw * 128, 0);
         s1[0] += e0; s2[0] += e0 * e0;
         s1[1] += e1; s2[1] += e1 * e1;
       }
@@ -1236,6 +1248,211 @@ __global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Par
       p.stats[((long)r * 64 + tid) * 2 + 1] = 0.f;
       if (tid == 0) cnts[r] = 0.f;
     }
+  }
+}
+
+// Wave-independent persistent stem forward: the hot case D % 2 == H % 2 == 0, W % 16 == 0.
+// Every wave owns a private stream of 2x2x16-voxel boxes (64 voxels = two 32-row MFMA
+// tiles) with its own 3-slot LDS ring of halos (4x4x18 rows, buffer LDS-DMA, prefetch
+// distance 2): no barrier inside the box loop, so the two waves sharing a SIMD drift apart
+// and one's MFMAs cover the other's epilogue.  MFMA row r of tile mt is voxel
+// (rd, rh, rw) = (mt, r >> 4, 2 (r & 3) + ((r >> 2) & 1) + 8 ((r >> 3) & 1)), so an
+// accumulator register of the 32x32 layout holds two ADJACENT voxels (lane halves) and each
+// buffer_store_dword writes 256 contiguous bytes with a per-lane constant voffset, a
+// per-(mt, row pair) soffset and an immediate offset.  Weights stay in VGPRs; BatchNorm
+// partials (shifted sums) are merged over the workgroup once at the end: ONE stats row per
+// workgroup (pcms_stem_fwd_rows).  Box order is XCD-aware (8 consecutive logical
+// workgroups' neighbouring boxes share one L2).
+constexpr int kSWvThreads = 512;
+constexpr int kSWvHalo = 4 * 4 * 18;                           // 288 halo rows
+constexpr int kSWvPieces = 5;                                  // DMA instructions per box (320 rows)
+constexpr int kSWvSlot = kSWvPieces * 64 * 16;                 // 5 KiB per ring slot
+constexpr int kSWvLds = 8 * 3 * kSWvSlot + 8 * 64 * 3 * 4;     // 120 KiB rings + stats merge
+
+__global__ void __launch_bounds__(kSWvThreads, 1) stem_fwd_wave_kernel(const bf16_t* x, const bf16_t* wpack,
+                                                                      const float* bias, bf16_t* y, float* stats,
+                                                                      int N, int D, int H, int W,
+                                                                      uint32_t xbytes, uint32_t ybytes) {
+  constexpr int HH = 4, HW = 18;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* red = reinterpret_cast<float*>(lds + 8 * 3 * kSWvSlot);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r_lane = lane & 31, hsel = lane >> 5;
+  const i32x4_t xr = buffer_desc(x, xbytes);
+  const auto yr = __builtin_amdgcn_make_buffer_rsrc(y, 0, ybytes, 0x00020000);
+  const int nbw = W >> 4, nbh = H >> 1, nbd = D >> 1;
+  const int nwb = N * nbd * nbh * nbw;
+  // logical workgroup: consecutive logical ids on one XCD (dispatch is round-robin over 8)
+  const int G = gridDim.x;
+  const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int stride = G * 8;
+
+  s16x8_t wb[kStemSteps][2];
+#pragma unroll
+  for (int st = 0; st < kStemSteps; ++st) {
+    wb[st][0] = *reinterpret_cast<const s16x8_t*>(wpack + (st * 64 + r_lane) * 16 + hsel * 8);
+    wb[st][1] = *reinterpret_cast<const s16x8_t*>(wpack + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
+  }
+  const float bias0 = bias ? bias[2 * r_lane] : 0.f, bias1 = bias ? bias[2 * r_lane + 1] : 0.f;
+  // A rows: halo row of this lane's voxel in tile mt
+  int hb16[2];
+  {
+    const int q = r_lane & 15;
+    const int rw = 2 * (q & 3) + ((q >> 2) & 1) + 8 * ((q >> 3) & 1);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) hb16[mt] = ((mt * HH + (r_lane >> 4)) * HW + rw) * 16;
+  }
+  // halo pieces: row hv = 64 j + lane of the 4x4x18 halo; source offset relative to the box
+  // origin voxel, packed halo coordinates (-1: past the halo)
+  int prel[kSWvPieces], pco[kSWvPieces];
+#pragma unroll
+  for (int j = 0; j < kSWvPieces; ++j) {
+    const int hv = j * 64 + lane;
+    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+    prel[j] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
+    pco[j] = hv < kSWvHalo ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
+  }
+  const uint32_t ring = lds_addr(lds) + wave * 3 * kSWvSlot;
+  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    int q = b;
+    const int bwi = q % nbw; q /= nbw;
+    const int bhi = q % nbh; q /= nbh;
+    const int bdi = q % nbd;
+    n = q / nbd;
+    d0 = bdi * 2; h0 = bhi * 2; w0 = bwi * 16;
+  };
+  // exactly kSWvPieces DMA instructions per call (b >= nwb: all out of range -> zeros), so
+  // the vmcnt arithmetic below is the same for every iteration
+  auto stage = [&](int b, int slot) {
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(ring + slot * kSWvSlot);
+    if (b >= nwb) {
+#pragma unroll
+      for (int j = 0; j < kSWvPieces; ++j) dma16(xr, lb + j * 1024, kOOB, 0);
+      return;
+    }
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const int base16 = (((n * D + d0) * H + h0) * W + w0) * 16;
+    const bool inner = d0 >= 1 && d0 + 2 < D && h0 >= 1 && h0 + 2 < H && w0 >= 1 && w0 + 16 < W;
+#pragma unroll
+    for (int j = 0; j < kSWvPieces; ++j) {
+      uint32_t voff = (uint32_t)(base16 + prel[j]);
+      const int c = pco[j];
+      if (c < 0) {
+        voff = kOOB;
+      } else if (!inner) {
+        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
+        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
+      }
+      dma16(xr, lb + j * 1024, voff, 0);
+    }
+  };
+
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2] = {0.f, 0.f};
+  float cnt = 0.f;
+  const uint32_t vlane = r_lane * 4 + hsel * 128;  // store voffset: channel pair + odd voxel
+  int b = lg * 8 + wave;
+  stage(b, 0);
+  stage(b + stride, 1);
+  for (int it = 0; b < nwb; b += stride, ++it) {
+    // this box's halo has landed (issued after it: DMA of the next box + the stores of the
+    // previous two; capped at the 6-bit counter)
+    if (it == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if (it == 1) asm volatile("s_waitcnt vmcnt(37)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    stage(b + 2 * stride, (it + 2) % 3);
+    const char* hl = lds + wave * 3 * kSWvSlot + (it % 3) * kSWvSlot;
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { acc[mt][0][e] = bias0; acc[mt][1][e] = bias1; }
+    if (!(PCMS_ABL & 1)) {
+      int hs16 = hsel * 16;
+      asm volatile("" : "+v"(hs16));
+      auto load_a = [&](int st, s16x8_t (&a)[2]) {
+        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
+        const int off16 = o0 * 16 + hs16 * (o1 - o0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + off16);
+      };
+      s16x8_t abuf[2][2];
+      load_a(0, abuf[0]);
+#pragma unroll
+      for (int st = 0; st < kStemSteps; ++st) {
+        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
+          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (it == 0) {
+      K[0] = __shfl(acc[0][0][0], r_lane, 64);
+      K[1] = __shfl(acc[0][1][0], r_lane, 64);
+    }
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const int bv = ((n * D + d0) * H + h0) * W + w0;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int gh = 0; gh < 2; ++gh) {
+        const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (mt * H + gh) * W) * 128u);
+#pragma unroll
+        for (int gl = 0; gl < 2; ++gl)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int e = (2 * gh + gl) * 4 + i;  // g = e >> 2: gh = g >> 1, gl = g & 1
+            const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
+            if (!(PCMS_ABL & 2))
+              __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, vlane + (2 * i + 8 * gl) * 128, so, 0);
+            const float e0 = v0 - K[0], e1 = v1 - K[1];
+            s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
+            s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
+          }
+      }
+    cnt += 32.f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!stats) return;
+  // per wave: S = sum d + n K, M2 = sum d^2 - (sum d)^2 / n; Chan merge over the 8 waves
+  const float nw = 2.f * cnt;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    s1[nt] += __shfl_xor(s1[nt], 32, 64);
+    s2[nt] += __shfl_xor(s2[nt], 32, 64);
+    if (hsel == 0) {
+      float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
+      rp[0] = s1[nt] + nw * K[nt];
+      rp[1] = nw > 0.f ? s2[nt] - s1[nt] * s1[nt] / nw : 0.f;
+      rp[2] = nw;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float S = 0.f, Nn = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
+    const float m = Nn > 0.f ? S / Nn : 0.f;
+    float M2 = 0.f, sdd = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const float c = red[(w * 64 + tid) * 3 + 2];
+      if (c > 0.f) {
+        const float d = red[(w * 64 + tid) * 3] / c - m;
+        M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+        sdd += c * d;
+      }
+    }
+    if (Nn > 0.f) M2 -= sdd * sdd / Nn;
+    float* st = stats + ((long)blockIdx.x * 64 + tid) * 2;
+    st[0] = S;
+    st[1] = M2;
+    if (tid == 0) stats[(long)gridDim.x * 128 + blockIdx.x] = Nn;
   }
 }
 
@@ -1536,8 +1753,8 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const int b2 = b + 2 * gridDim.x;
-    if (b2 < nbox) stage(b2, (it + 2) % 3);
-    compute(swl + (it % 3) * kSWBuf);
+    if (b2 < nbox && !(PCMS_ABL & 16)) stage(b2, (it + 2) % 3);
+    if (!(PCMS_ABL & 8)) compute(swl + (it % 3) * kSWBuf);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1588,15 +1805,322 @@ __global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* par
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Big-box forward / dgrad (bf16; the level-0/1 hot case: D % 8 == H % 8 == 0, W % 16 == 0,
+// input channels in 16-channel chunks).  One 4-wave workgroup per CU computes an
+// 8 x 8 x 16 = 1024-voxel box x 64 output channels.  Wave w owns voxel rows
+// [256 w, 256 w + 256) = 8 M-tiles, so every B fragment (weights, L2-resident) feeds 8 MFMAs,
+// half the weight traffic per MFMA of conv3_fwd_kernel.  The 10 x 10 x 18 halo of a chunk
+// (32-B rows; the two 16-B halves swapped on odd row octets, so 16 consecutive rows hit 16
+// distinct bank groups) is double-buffered: the next chunk's halo streams in by buffer
+// LDS-DMA, one piece per thread and tap over the first 15 taps of the current chunk, and A
+// fragments of tap t + 1 are read while tap t's 16 MFMAs run.  Output columns are channel
+// pairs (column j of N-tile nt = channel 2 j + nt): each accumulator register pair stores as
+// one packed bf16x2, a store instruction writes two 128-B voxel rows.  BatchNorm partials:
+// one stats row per box (sum, M2 about the row mean; counts after the [rows][Cout][2] block).
+// ------------------------------------------------------------------------------------
+constexpr int kBgThreads = 256;
+constexpr int kBgHH = 10, kBgHW = 18;
+// BD = box depth: 8 (1024 voxels, 8 M-tiles per wave, one workgroup per CU) or 4 (512
+// voxels, 4 M-tiles per wave, two workgroups per CU that cover each other's prologue,
+// chunk barriers and store tail)
+template <int BD> struct BgGeom {
+  static constexpr int MT = BD;                                           // M-tiles per wave
+  static constexpr int Halo = (BD + 2) * kBgHH * kBgHW;                   // rows x 32 B
+  static constexpr int Pieces = (2 * Halo + kBgThreads - 1) / kBgThreads; // DMA pieces / thread
+  static constexpr int Buf = Pieces * kBgThreads * 16;                    // (tail pad)
+  static constexpr int Lds = 2 * Buf + 4 * 64 * 3 * 4;                    // + stats merge
+  static constexpr int PerCU = BD == 8 ? 1 : 2;
+  static constexpr int Dist = BD == 8 ? 8 : 2;  // B prefetch distance (taps); (Dist + 1) | 27
+  static_assert(27 % (Dist + 1) == 0, "B ring index must continue across chunks");
+};
+constexpr int kBgBD = (PCMS_ABL & 1024) ? 4 : 8;  // product box depth (depth 4 measured slower)
+
+// hidden 16-B global load (the compiler's waitcnt pass does not count it): retired by
+// vm_wait2<N>, which also orders the register's readers after the wait
+__device__ __forceinline__ void gload16(s16x8_t& dst, const void* ptr) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(ptr) : "memory");
+}
+template <int N> __device__ __forceinline__ void vm_wait2(s16x8_t& a, s16x8_t& b) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F> __device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+// vector-memory ops issued after B(t)'s second load by the time tap t waits for it: every
+// tap s issues B(s + D) x 2 then piece(s) (s < 15, chunk-relative, every chunk alike)
+template <int P> constexpr int bg_piece(int s) { return ((s % 27) + 27) % 27 < P ? 1 : 0; }
+template <int P, int Dist> constexpr int bg_wait(int t) {
+  int n = bg_piece<P>(t - Dist);
+  for (int s = t - Dist + 1; s <= t; ++s) n += 2 + bg_piece<P>(s);
+  return n;
+}
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+
+template <int BD>
+__global__ void __launch_bounds__(kBgThreads, BgGeom<BD>::PerCU) conv3_fwd_big_kernel(Conv3Params p, uint32_t x0bytes,
+                                                                                     uint32_t x1bytes) {
+  typedef BgGeom<BD> Gm;
+  constexpr int MT = Gm::MT;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r_lane = lane & 31, hsel = lane >> 5;
+  const int Cout = p.Cout, ncob = Cout >> 6;
+  // logical workgroup id: consecutive ids on one XCD (dispatch is round-robin over 8), output
+  // channel block fastest, so the workgroups sharing a halo (and neighbouring boxes) share L2
+  const int G = gridDim.x;
+  const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int cob = lg % ncob, box = lg / ncob, nbox = G / ncob;
+  int q = box;
+  const int bwi = q % p.nbw; q /= p.nbw;
+  const int bhi = q % p.nbh; q /= p.nbh;
+  const int bdi = q % p.nbd;
+  const int n = q / p.nbd;
+  const int d0 = bdi * BD, h0 = bhi * 8, w0 = bwi * 16;
+  const int co_base = cob * 64;
+
+  // this thread's halo pieces: (voxel << 1 | logical 16-B half), -1 = zero (padding, tail)
+  int pv[Gm::Pieces];
+#pragma unroll
+  for (int j = 0; j < Gm::Pieces; ++j) {
+    const int pc = tid + j * kBgThreads;
+    const int hv = pc >> 1;
+    int e = -1;
+    if (hv < Gm::Halo) {
+      const int hw_ = hv % kBgHW, t_ = hv / kBgHW, hh_ = t_ % kBgHH, hd_ = t_ / kBgHH;
+      const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+      if ((unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H && (unsigned)gw < (unsigned)p.W)
+        e = ((((n * p.D + gd) * p.H + gh) * p.W + gw) << 1) | ((pc & 1) ^ ((hw_ >> 3) & 1));
+    }
+    pv[j] = e;
+  }
+  const i32x4_t xr0 = buffer_desc(p.x0, x0bytes);
+  const i32x4_t xr1 = buffer_desc(p.x1 ? p.x1 : p.x0, x1bytes);
+  const uint32_t lds0 = lds_addr(lds);
+  // live = false (past the last chunk): the piece is still issued (the vmcnt arithmetic is
+  // the same for every chunk) but reads out of range = zeros into the idle buffer
+  auto stage_piece = [&](int chunk, int buf, int j, bool live) {
+    const int c = chunk * 16;
+    const bool first = c < p.c0;  // workgroup-uniform: the chunk lies in x0 or in x1
+    const uint32_t stride = first ? p.c0 : p.c1;
+    const uint32_t cofs = first ? c : c - p.c0;
+    const int e = pv[j];
+    const uint32_t voff = (e < 0 || !live) ? kOOB
+                                           : ((uint32_t)(e >> 1) * stride + cofs + (uint32_t)(e & 1) * 8u) * 2u;
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds0 + buf * Gm::Buf + (wave * 64 + j * kBgThreads) * 16);
+    dma16(first ? xr0 : xr1, lb, voff, 0);
+  };
+
+  // A fragment byte offsets in a halo buffer: MFMA row r = 256 wave + 32 mt + perm32(lane)
+  // is box voxel (2 wave + mt / 4, 2 (mt % 4) + prow / 16, prow % 16).  The half swizzle
+  // depends on the halo w coordinate only, so for each kw the (kd, kh) part of a tap is a
+  // constant row offset (kd * 10 + kh) * 18 * 32 bytes folded into the ds_read immediate.
+  const int prow = perm32(r_lane);
+  int hb32[MT], swk[3];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int rd = (BD / 4) * wave + (mt >> 2), rh = 2 * (mt & 3) + (prow >> 4);
+    hb32[mt] = ((rd * kBgHH + rh) * kBgHW + (prow & 15)) * 32;
+  }
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) swk[kw] = kw * 32 + ((hsel ^ ((((prow & 15) + kw) >> 3) & 1)) << 4);
+  // B fragment: packed [Cin/32][27][Cout][32]; 16-channel chunk c = half (c & 1) of c >> 1
+  // B fragments (weights, packed [Cin/32][27][Cout][32]; 16-channel chunk c = half c & 1 of
+  // 32-chunk c >> 1) come through hidden loads Dist taps ahead: vector-memory returns are
+  // in order, so a wait on B(t) also retires every halo piece issued before it; the pieces
+  // get >= Dist taps to arrive from HBM before anything waits on them.
+  const bf16_t* wp = (const bf16_t*)p.w;
+  const int nchunk = p.Cin >> 4;
+  auto load_b = [&](s16x8_t (&dst)[2], int chunk, int tap) {
+    chunk = min(chunk, nchunk - 1);  // past the last chunk: a harmless reload (fixed counts)
+    const bf16_t* wt = wp + ((long)((chunk >> 1) * 27 + tap) * Cout + co_base + 2 * r_lane) * 32 + (chunk & 1) * 16 +
+                       hsel * 8;
+    gload16(dst[0], wt);
+    gload16(dst[1], wt + 32);
+  };
+
+  f32x16_t acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+#pragma unroll
+  for (int j = 0; j < Gm::Pieces; ++j) stage_piece(0, 0, j, true);
+  s16x8_t bset[Gm::Dist + 1][2];
+#pragma unroll
+  for (int t = 0; t < Gm::Dist; ++t) load_b(bset[t], 0, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int chunk = 0; chunk < nchunk; ++chunk) {
+    const int buf = chunk & 1;
+    const bool more = chunk + 1 < nchunk;
+    const char* hl = lds + buf * Gm::Buf;
+    auto read_a = [&](s16x8_t (&dst)[MT], int tap) {
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      const char* base = hl + swk[kw] + (kd * kBgHH + kh) * kBgHW * 32;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) dst[mt] = *reinterpret_cast<const s16x8_t*>(base + hb32[mt]);
+    };
+    s16x8_t a[2][MT];
+    read_a(a[0], 0);
+    // per tap: B(tap + D) (the set index runs on across chunks: (D + 1) | 27), one halo piece
+    // of the next chunk (taps < 15), A of tap + 1; wait for B(tap); this tap's 16 MFMAs
+    static_for<27>([&](auto tc) {
+      constexpr int tap = decltype(tc)::value;
+      constexpr int tn = tap + Gm::Dist;
+      if constexpr (!(PCMS_ABL & 64)) {
+        if constexpr (tn < 27) load_b(bset[tn % (Gm::Dist + 1)], chunk, tn);
+        else load_b(bset[tn % (Gm::Dist + 1)], chunk + 1, tn - 27);
+      }
+      if constexpr (tap < Gm::Pieces && !(PCMS_ABL & 32)) stage_piece(chunk + 1, buf ^ 1, tap, more);
+      constexpr int cur = tap & 1;
+      if constexpr (tap + 1 < 27) {
+        if constexpr (!(PCMS_ABL & 256)) read_a(a[cur ^ 1], tap + 1);
+        else if constexpr (tap == 0) read_a(a[1], 1);
+      }
+      s16x8_t(&b)[2] = bset[tap % (Gm::Dist + 1)];
+      if constexpr (!(PCMS_ABL & 128)) vm_wait2<bg_wait<Gm::Pieces, Gm::Dist>(tap)>(b[0], b[1]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[cur][mt], b[nt], acc[mt][nt]);
+    });
+    // the next chunk's halo has landed (the newest piece is followed by the B loads of the
+    // remaining taps) and every wave is done with buf; after the last chunk retire everything
+    if (more) vm_wait<2 * (27 - Gm::Pieces)>();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: + bias, packed channel-pair stores (two-pointer output split at cy0)
+  const int cpair = co_base + 2 * r_lane;
+  float bias0 = 0.f, bias1 = 0.f;
+  if (p.bias) {
+    bias0 = p.bias[cpair];
+    bias1 = p.bias[cpair + 1];
+  }
+  const bool to0 = co_base < p.cy0;
+  bf16_t* yb = to0 ? (bf16_t*)p.y0 : (bf16_t*)p.y1;
+  const long ys = to0 ? p.cy0 : Cout - p.cy0;
+  const int yc = to0 ? cpair : cpair - p.cy0;
+  const long plane = (long)p.H * p.W;
+  const long vbase = (((long)n * p.D + d0) * p.H + h0) * p.W + w0;
+  float s1[2] = {0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int pr = perm32((e & 3) + 8 * (e >> 2) + 4 * hsel);
+    const long vrow = vbase + (long)(pr >> 4) * p.W + (pr & 15);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int rd = (BD / 4) * wave + (mt >> 2), rh = 2 * (mt & 3);
+      const long vox = vrow + (long)rd * plane + (long)rh * p.W;
+      const float v0 = acc[mt][0][e] + bias0, v1 = acc[mt][1][e] + bias1;
+      if (!(PCMS_ABL & 512)) *reinterpret_cast<uint32_t*>(yb + vox * ys + yc) = pack_bf16x2(v0, v1);
+      s1[0] += v0;
+      s1[1] += v1;
+    }
+  }
+  if (!p.stats) return;
+  // BatchNorm partials: per-wave mean, squared deviations about it (corrected by
+  // (sum d)^2 / n), Chan merge over the 4 waves
+  constexpr float nw = 32.f * MT;
+  float mw[2], s2[2] = {0.f, 0.f}, sd[2] = {0.f, 0.f};
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    s1[nt] += __shfl_xor(s1[nt], 32, 64);
+    mw[nt] = s1[nt] / nw;
+  }
+  const float sh[2] = {bias0 - mw[0], bias1 - mw[1]};  // d = acc + bias - mean
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const float d = acc[mt][nt][e] + sh[nt];
+        s2[nt] = fmaf(d, d, s2[nt]);
+        sd[nt] += d;
+      }
+  float* red = reinterpret_cast<float*>(lds + 2 * Gm::Buf);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    s2[nt] += __shfl_xor(s2[nt], 32, 64);
+    sd[nt] += __shfl_xor(sd[nt], 32, 64);
+    s2[nt] -= sd[nt] * sd[nt] / nw;
+    if (hsel == 0) {
+      float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
+      rp[0] = s1[nt];
+      rp[1] = s2[nt];
+      rp[2] = nw;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float S = 0.f, Nn = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      S += red[(w * 64 + tid) * 3];
+      Nn += red[(w * 64 + tid) * 3 + 2];
+    }
+    const float m = S / Nn;
+    float M2 = 0.f, sdd = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float c = red[(w * 64 + tid) * 3 + 2];
+      const float d = red[(w * 64 + tid) * 3] / c - m;
+      M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+      sdd += c * d;
+    }
+    M2 -= sdd * sdd / Nn;
+    float* st = p.stats + ((long)box * Cout + co_base + tid) * 2;
+    st[0] = S;
+    st[1] = M2;
+    if (tid == 0 && cob == 0) p.stats[(long)nbox * Cout * 2 + box] = Nn;
+  }
+}
+
 }  // namespace
+
+// big-box forward: bf16, whole 8x8x16 boxes, 16-channel chunks of both sources, enough boxes
+// to give every CU one (pcms_conv3_big_min_boxes), every byte offset inside a 32-bit voffset
+static int g_big_min_boxes = 256;
+static bool big_fwd_ok(int dtype, int N, int D, int H, int W, int c0, int c1) {
+  if (dtype != PCMS_BF16 || D % kBgBD || H % 8 || W % 16 || c0 % 16 || c1 % 16 || c0 < 16) return false;
+  const long nvox = (long)N * D * H * W;
+  if ((long)N * (D / kBgBD) * (H / 8) * (W / 16) < g_big_min_boxes) return false;
+  return nvox < (1L << 30) && nvox * std::max(c0, c1) * 2 < (long)kOOB;
+}
 
 extern "C" {
 
-// Returns the m-block count (workgroups along M) the fwd launch will use for a grid;
-// callers size the BatchNorm partial buffer [mblocks][Cout][2] from it.
+// Returns the m-block count (workgroups along M) of the general fwd kernel for a grid
+// (an upper bound on every fwd path's BatchNorm row count; sizes the split decision).
 int pcms_conv3_mblocks(int N, int D, int H, int W) {
   Box b = fwd_box(D, H, W);
   return N * cdiv(D, 1 << b.lbd) * cdiv(H, 1 << b.lbh) * cdiv(W, 1 << b.lbw);
+}
+
+// BatchNorm partial rows an unsplit pcms_conv3_fwd with these sources writes
+int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1) {
+  if (big_fwd_ok(dtype, N, D, H, W, c0, c1)) return N * (D / kBgBD) * (H / 8) * (W / 16);
+  return pcms_conv3_mblocks(N, D, H, W);
+}
+
+// Minimum box count for the big-box forward (tests lower it to reach small grids);
+// v <= 0 only queries.  Returns the previous value.
+int pcms_conv3_big_min_boxes(int v) {
+  const int old = g_big_min_boxes;
+  if (v > 0) g_big_min_boxes = v;
+  return old;
 }
 
 int pcms_conv3_chunk(int dtype) { return dtype == PCMS_BF16 ? Traits<bf16_t>::CK : Traits<float>::CK; }
@@ -1642,6 +2166,16 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
   p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
   if (splits > 1) p.yacc = yacc;
+  if (splits == 1 && !accumulate && big_fwd_ok(dtype, N, D, H, W, c0, c1)) {
+    p.nbd = D / kBgBD; p.nbh = H / 8; p.nbw = W / 16;
+    const int nbox = N * p.nbd * p.nbh * p.nbw;
+    const long nvox = (long)N * D * H * W;
+    constexpr int lds = BgGeom<kBgBD>::Lds;
+    (void)hipFuncSetAttribute((const void*)conv3_fwd_big_kernel<kBgBD>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(conv3_fwd_big_kernel<kBgBD>, dim3(nbox * (Cout / 64)), dim3(kBgThreads), lds, s, p,
+                       (uint32_t)(nvox * c0 * 2), (uint32_t)(nvox * c1 * 2));
+    PCMS_CHECK_LAUNCH();
+  }
   dim3 grid(N * p.nbd * p.nbh * p.nbw, Cout / 64, splits);
   const bool hot = b.lbd == 2 && b.lbh == 3 && b.lbw == 4;
   if (dtype == PCMS_BF16) {
@@ -1662,7 +2196,24 @@ int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s) {
 }
 int pcms_stem_pack_elems(void) { return kStemSteps * 64 * 16; }
 
-// x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_conv3_mblocks
+static int device_cus();
+// the wave-independent stem forward measured slower than the direct kernel (110 vs 97 us at
+// config 2): kept for tuning behind an ablation switch
+static bool stem_fwd_wave_shape(int N, int D, int H, int W) {
+  return (PCMS_ABL & 2048) && D % 2 == 0 && H % 2 == 0 && W % 16 == 0 && (long)N * D * H * W * 128 < (long)kOOB;
+}
+static int stem_fwd_wave_grid(int N, int D, int H, int W) {
+  const long nwb = (long)N * (D / 2) * (H / 2) * (W / 16);
+  return (int)std::max(1L, std::min((long)device_cus(), (nwb + 7) / 8));
+}
+
+// BatchNorm statistics rows pcms_stem_fwd writes
+int pcms_stem_fwd_rows(int N, int D, int H, int W) {
+  if (stem_fwd_wave_shape(N, D, H, W)) return stem_fwd_wave_grid(N, D, H, W);
+  return pcms_conv3_mblocks(N, D, H, W);
+}
+
+// x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_stem_fwd_rows
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
                   int N, int D, int H, int W, hipStream_t s) {
   Box b = fwd_box(D, H, W);
@@ -1683,6 +2234,13 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
   const long xbytes = (long)N * D * H * W * 16, ybytes = (long)N * D * H * W * 128;
+  if (stem_fwd_wave_shape(N, D, H, W)) {
+    const int grid = stem_fwd_wave_grid(N, D, H, W);
+    (void)hipFuncSetAttribute((const void*)stem_fwd_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kSWvLds);
+    hipLaunchKernelGGL(stem_fwd_wave_kernel, dim3(grid), dim3(kSWvThreads), kSWvLds, s, (const bf16_t*)x,
+                       (const bf16_t*)wpack, bias, (bf16_t*)y, stats, N, D, H, W, (uint32_t)xbytes, (uint32_t)ybytes);
+    PCMS_CHECK_LAUNCH();
+  }
   const bool direct = b.lbw == 4 && b.lbd + b.lbh == 5 && (b.lbd == 2 || b.lbd == 3) && ybytes < (long)kOOB;
   if (direct) {
     const int grid = std::min(nbox, ncu);
@@ -1799,9 +2357,8 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   }
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const long total = 27L * Cout * cin_w;
-  hipLaunchKernelGGL(wgrad_permute_kernel, dim3((int)std::min<long>(4096, (total + 255) / 256)), dim3(256), 0, s,
-                     (const float*)dwt, dw, Cout, Cin, cin_w);
+  hipLaunchKernelGGL(wgrad_permute_kernel, dim3(Cout, cdiv(cin_w, 32)), dim3(256), 0, s, (const float*)dwt, dw,
+                     Cout, Cin, cin_w);
   PCMS_CHECK_LAUNCH();
 }
 

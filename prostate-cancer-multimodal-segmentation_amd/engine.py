@@ -252,7 +252,8 @@ class UNetEngine:
             b[f"gU{l}"] = act(l, C[l])      # grad of up output / pooled input (scratch)
         b["gH"] = act(0, C[0])              # grad of the decoder output (head input)
         # workspaces
-        rows_f = max(query("pcms_conv3_mblocks", N, *S[l]) for l in range(5))
+        rows_f = max(max(query("pcms_conv3_mblocks", N, *S[l]) for l in range(5)),
+                     query("pcms_stem_fwd_rows", N, *S[0]))
         rows_s = max(query("pcms_split_epilogue_rows", nv[l]) for l in range(5))
         rows_b = max(query("pcms_bn_bwd_rows", self.code, C[l], nv[l]) for l in range(5))
         # BN partials [rows][C][2] + [rows] voxel counts
@@ -284,11 +285,11 @@ class UNetEngine:
         st = b["stats"] if training else None
         if cs is self.convs[0] and self.stem_fast:
             call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2])
-            rows = query("pcms_conv3_mblocks", N, *S)
+            rows = query("pcms_stem_fwd_rows", N, *S)
         elif splits == 1:
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
-            rows = query("pcms_conv3_mblocks", N, *S)
+            rows = query("pcms_conv3_fwd_rows", self.code, N, *S, c0, c1)
         else:
             acc = b["yacc"][: nvox * cs.cout]
             acc.zero_()

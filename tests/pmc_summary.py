@@ -1,54 +1,29 @@
-"""Summarise rocprofv3 --pmc counter CSVs per kernel (mean over dispatches).
+"""Average rocprofv3 PMC counters per dispatch for kernels matching a substring (test tooling).
 
-    python tests/pmc_summary.py gpurun_out/pmcX [filter-substring]
-
-Reads every */*counter_collection.csv under the given directories, keeps kernels whose
-name contains the filter, and prints counter means plus derived figures (VALU per MFMA,
-wait fractions, HBM bytes with the gfx950 FETCH_SIZE x2 correction).
+    python tests/pmc_summary.py <run_counter_collection.csv> [...] --kernel conv3_fwd_big
 """
-import collections
+import argparse
 import csv
-import glob
-import os
 import sys
 
-
-def load(dirs, flt):
-    vals = collections.defaultdict(lambda: collections.defaultdict(list))
-    for d in dirs:
-        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    name = row["Kernel_Name"]
-                    if flt and flt not in name:
-                        continue
-                    short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:70]
-                    vals[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return vals
+csv.field_size_limit(sys.maxsize)
 
 
 def main():
-    args = sys.argv[1:]
-    flt = ""
-    dirs = [a for a in args if os.path.isdir(a)]
-    rest = [a for a in args if not os.path.isdir(a)]
-    if rest:
-        flt = rest[0]
-    for k, cs in load(dirs, flt).items():
-        m = {c: sum(v) / len(v) for c, v in cs.items()}
-        print(f"== {k}  (dispatches/counter: {max(len(v) for v in cs.values())})")
-        for c in sorted(m):
-            print(f"   {c:32s} {m[c]:.4g}")
-        if "SQ_INSTS_VALU" in m and "SQ_INSTS_VALU_MFMA_BF16" in m and m["SQ_INSTS_VALU_MFMA_BF16"]:
-            print(f"   -> VALU per MFMA {(m['SQ_INSTS_VALU'] - m['SQ_INSTS_VALU_MFMA_BF16']) / m['SQ_INSTS_VALU_MFMA_BF16']:.2f}")
-        if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
-            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
-                if c in m:
-                    print(f"   -> {c}/WAVE_CYCLES {m[c] / m['SQ_WAVE_CYCLES']:.3f}")
-        if "FETCH_SIZE" in m:
-            print(f"   -> HBM read (FETCH_SIZE x2) {2 * m['FETCH_SIZE'] * 1024 / 1e6:.1f} MB")
-        if "WRITE_SIZE" in m:
-            print(f"   -> HBM write {m['WRITE_SIZE'] * 1024 / 1e6:.1f} MB")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("files", nargs="+")
+    ap.add_argument("--kernel", required=True)
+    a = ap.parse_args()
+    for fn in a.files:
+        per = {}
+        for r in csv.DictReader(open(fn)):
+            if a.kernel not in r["Kernel_Name"]:
+                continue
+            d = per.setdefault(r["Counter_Name"], {})
+            d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+        for name, d in sorted(per.items()):
+            vals = list(d.values())
+            print(f"{name:32s} dispatches={len(vals):3d} mean={sum(vals) / len(vals):.4g}")
 
 
 if __name__ == "__main__":

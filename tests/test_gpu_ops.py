@@ -88,7 +88,7 @@ def test_conv3_fwd(dt, code, tol, N, cin, cout, S, split):
     L.call("pcms_conv3_pack", code, w.to(DEV), wpack, cout, cin_real, 0)
     y = torch.empty(N, *S, cout, dtype=dt, device=DEV)
     nvox = N * S[0] * S[1] * S[2]
-    rows = L.query("pcms_conv3_mblocks", N, *S)
+    rows = L.query("pcms_conv3_fwd_rows", code, N, *S, cin, 0)
     stats = torch.zeros(max(rows, L.query("pcms_split_epilogue_rows", nvox)) * (cout * 2 + 1), device=DEV)
     if split == 1:
         L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, None, stats, 0,
@@ -179,6 +179,50 @@ def test_conv3_dual_source_and_dgrad_split_output(dt, code, tol):
     torch.cuda.synchronize()
     close(ncdhw(gs.cpu()), xr.grad[:, :cs], tol, "dgrad skip part")
     close(ncdhw(gu.cpu()), xr.grad[:, cs:], tol, "dgrad up part")
+
+
+@pytest.mark.parametrize("N,c0,c1,cout,cy0,S", [
+    (1, 64, 0, 64, 64, (8, 8, 16)),         # one box
+    (2, 32, 32, 128, 64, (16, 8, 32)),      # dual source, two-pointer output, 2 channel blocks
+    (1, 16, 48, 64, 64, (8, 16, 16)),       # chunks split unevenly between the sources
+    (1, 128, 0, 192, 128, (16, 16, 16)),    # odd number of 64-channel blocks, split output
+])
+def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S):
+    """Big-box bf16 forward (8x8x16 boxes, 16-channel chunks, channel-pair stores) vs
+    torch conv3d on the same bf16 inputs; BN partial moments; the min-box threshold is
+    lowered so these small grids reach it."""
+    L = _lib()
+    old = L.query("pcms_conv3_big_min_boxes", 1)
+    try:
+        dt = torch.bfloat16
+        g = torch.Generator().manual_seed(c0 + 5 * c1 + cout)
+        x0 = torch.randn(N, c0, *S, generator=g).to(dt)
+        x1 = torch.randn(N, c1, *S, generator=g).to(dt)
+        cin = c0 + c1
+        w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+        b = torch.randn(cout, generator=g)
+        ref = F.conv3d(torch.cat([x0, x1], 1).double(), w.to(dt).double(), b.double(), padding=1)
+        wp = torch.empty(-(-cin // 32) * 27 * cout * 32, dtype=dt, device=DEV)
+        L.call("pcms_conv3_pack", 1, w.to(DEV), wp, cout, cin, 0)
+        y0 = torch.empty(N, *S, cy0, dtype=dt, device=DEV)
+        y1 = torch.empty(N, *S, max(cout - cy0, 8), dtype=dt, device=DEV)
+        nvox = N * S[0] * S[1] * S[2]
+        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, c0, c1)
+        assert rows in [N * (S[0] // bd) * (S[1] // 8) * (S[2] // 16) for bd in (4, 8)]  # big-box path taken
+        stats = torch.zeros(rows * (cout * 2 + 1), device=DEV)
+        L.call("pcms_conv3_fwd", 1, ndhwc(x0).to(DEV), c0, ndhwc(x1).to(DEV) if c1 else None, c1, wp, b.to(DEV),
+               y0, y1 if cout > cy0 else None, cy0, None, stats, 0, N, *S, cout, 1)
+        torch.cuda.synchronize()
+        got = ncdhw(y0.cpu())
+        if cout > cy0:
+            got = torch.cat([got, ncdhw(y1.cpu())], 1)
+        close(got, ref, 1e-2, "big-box fwd")
+        mean, var = bn_moments(stats, rows, cout, nvox)
+        yref = ref.transpose(0, 1).reshape(cout, -1)
+        close(mean, yref.mean(1), 1e-3, "big-box stats mean")
+        close(var, yref.var(1, unbiased=False), 1e-3, "big-box stats var")
+    finally:
+        L.query("pcms_conv3_big_min_boxes", old)
 
 
 @pytest.mark.parametrize("dt,code,tol", DTS)
@@ -420,7 +464,8 @@ def test_pack_input(dt, code):
 
 
 @pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (1, (9, 10, 11)), (2, (8, 8, 4)), (1, (6, 20, 33)),
-                                 (1, (8, 12, 48)), (3, (4, 4, 16)), (1, (32, 32, 32))])
+                                 (1, (8, 12, 48)), (3, (4, 4, 16)), (1, (32, 32, 32)), (1, (48, 64, 64)),
+                                 (2, (32, 64, 64))])
 def test_stem_fwd_wgrad_bf16(N, S):
     """Dedicated stem kernels (tap-pair packed K) vs torch conv3d on the bf16-rounded input."""
     L = _lib()
@@ -434,7 +479,7 @@ def test_stem_fwd_wgrad_bf16(N, S):
     wp = torch.empty(L.query("pcms_stem_pack_elems"), dtype=torch.bfloat16, device=DEV)
     L.call("pcms_stem_pack", w.to(DEV), wp, 5)
     y = torch.empty(N, *S, 64, dtype=torch.bfloat16, device=DEV)
-    rows = L.query("pcms_conv3_mblocks", N, *S)
+    rows = L.query("pcms_stem_fwd_rows", N, *S)
     stats = torch.zeros(rows * (64 * 2 + 1), device=DEV)
     L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y, stats, N, *S)
     xr = x.double()
