@@ -60,7 +60,8 @@ def stem_roofline(tr, N, spatial, reps):
     rows = L.query("pcms_conv3_mblocks", N, D, H, W)
     stats = torch.empty(rows * (64 * 2 + 1), device="cuda")
     dw = torch.zeros(64 * 5 * 27, device="cuda")
-    dwt = torch.empty(max(27 * 64 * eng.cp, L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5)), device="cuda")
+    dwt = torch.empty(max(L.query("pcms_conv3_wgrad_ws_floats", code, N, D, H, W, eng.cp, 0, 64, 512),
+                          L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5)), device="cuda")
 
     eng._ensure_packs()
 

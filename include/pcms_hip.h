@@ -51,7 +51,9 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    float* yacc, float* stats, int accumulate,
                    int N, int D, int H, int W, int Cout, int splits, hipStream_t s);
 /* dw [Cout][cin_w][27] fp32 += sum_v dy[v, co] * x[v + tap, ci] (ci < cin_w <= c0 + c1);
- * dwt = 27*Cout*(c0+c1) fp32 workspace                                                   */
+ * dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (one partial row per voxel split,
+ * summed in a fixed order: deterministic)                                               */
+int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout, int target_wgs);
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, hipStream_t s);

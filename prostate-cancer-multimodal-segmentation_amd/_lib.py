@@ -23,6 +23,7 @@ SIGNATURES = {
     "pcms_conv3_big_min_boxes": "i",
     "pcms_conv3_pack": "ippiiis",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
+    "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiis",
     "pcms_stem_pack_elems": "",
     "pcms_stem_pack": "ppis",

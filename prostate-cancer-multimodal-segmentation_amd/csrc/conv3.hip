@@ -34,6 +34,7 @@ constexpr int kRowBytes = 64;      // one halo row = one LDS row of the current 
 constexpr int kHaloMax = 1152;     // halo voxels per workgroup (72 KiB LDS, 2 WG / CU)
 
 __device__ __attribute__((aligned(16))) uint32_t g_zero16[4];  // zero page for LDS-DMA padding
+constexpr uint32_t kOOB = 0x80000000u;  // buffer voffset past num_records: reads zeros
 
 template <typename T> struct Traits;
 template <> struct Traits<bf16_t> {
@@ -431,10 +432,13 @@ template <> struct WTraits<float> {
 struct WgradParams {
   const void* x0; const void* x1; int c0; int c1;
   const void* dy;
-  float* dwt;            // fp32 workspace [27][Cout][Cin] (atomic accumulate)
+  float* dwt;            // fp32 workspace: one [27][Cout][Cin] partial row per split
   int N, D, H, W, Cin, Cout;
   int lbd, lbh, lbw, nbd, nbh, nbw;
   int nbox, boxes_per_split;
+  int nco, nci;          // 64-channel output blocks, 32-channel input blocks
+  int dma;               // bf16: stage by buffer LDS-DMA (byte sizes below < 2^31)
+  uint32_t x0bytes, x1bytes, dybytes;
 };
 
 // dy tile: 128-B (bf16) rows, 64-B halves swizzled by row bit 1 (conflict-free tr reads).
@@ -462,8 +466,14 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   const int cot = wave & 1;           // co tile (32 rows of the 64-wide dy tile)
   const int tg = wave >> 1;           // taps tg, tg+4, ...
   const int ntap = (tg == 3) ? 6 : 7;
-  const int co_base = blockIdx.y * 64;
-  const int ci_base = blockIdx.z * 32;
+  // 1-D grid, logical id XCD-aware (dispatch is round-robin over 8 XCDs: consecutive logical
+  // ids land on one XCD at about the same time), tile (co block, ci block) fastest: the
+  // workgroups of one split that share its dy boxes (and its halos) share an L2
+  const int G = gridDim.x, ntile = p.nco * p.nci;
+  const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int tile = lg % ntile, split = lg / ntile;
+  const int co_base = (tile % p.nco) * 64;
+  const int ci_base = (tile / p.nco) * 32;
   const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
   const int HH = bh + 2, HW = bw + 2;
   const int HV = (bd + 2) * HH * HW;
@@ -473,7 +483,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   const T* x1 = (const T*)p.x1;
   const T* dy = (const T*)p.dy;
 
-  const int b_beg = blockIdx.x * p.boxes_per_split;
+  const int b_beg = split * p.boxes_per_split;
   const int b_end = min(p.nbox, b_beg + p.boxes_per_split);
 
   f32x16_t acc[7];
@@ -500,8 +510,11 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     box_origin(b, n, d0, h0, w0);
 #pragma unroll
     for (int i = 0; i < MAXP; ++i) {
+      // one unconditional 16-B load per piece (invalid pieces read the zero page): a
+      // conditional load merged with a zero default makes the compiler drain vmcnt before
+      // the merge, serialising the prefetch with the compute it should overlap
       const int pc = tid + i * kWThreads;
-      u32x4_t v = {0u, 0u, 0u, 0u};
+      const void* src = g_zero16;
       if (pc < DYP) {
         const int r = pc / (Tr::DYROW / 16), q = pc % (Tr::DYROW / 16);
         if (r < boxvol) {
@@ -509,7 +522,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
           if (gd < p.D && gh < p.H && gw < p.W) {
             const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
-            v = *reinterpret_cast<const u32x4_t*>(dy + vox * p.Cout + co_base + q * Tr::VEC);
+            src = dy + vox * p.Cout + co_base + q * Tr::VEC;
           }
         }
       } else if (pc < DYP + XP) {
@@ -520,11 +533,10 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         const int c = ci_base + q * Tr::VEC;
         if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
           const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
-          const T* src = (c < p.c0) ? x0 + vox * p.c0 + c : x1 + vox * p.c1 + (c - p.c0);
-          v = *reinterpret_cast<const u32x4_t*>(src);
+          src = (c < p.c0) ? (const void*)(x0 + vox * p.c0 + c) : (const void*)(x1 + vox * p.c1 + (c - p.c0));
         }
       }
-      stg[i] = v;
+      stg[i] = *reinterpret_cast<const u32x4_t*>(src);
     }
   };
   auto stage_store = [&](char* buf) {
@@ -634,16 +646,69 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     }
   };
 
-  if (b_beg < b_end) {
+  // bf16 hot path: both tiles arrive by buffer LDS-DMA (no register staging); the next box
+  // streams in while this one computes.  The dy tile keeps dy_off_bf16's half swap (applied
+  // to the source address); each wave instruction is all-dy or all-halo (2048 dy pieces);
+  // out-of-range pieces read zeros.
+  auto stage_dma = [&](char* buf, int b) {
+    int n, d0, h0, w0;
+    box_origin(b, n, d0, h0, w0);
+    const uint32_t lb0 = lds_addr(buf);
+    const bool first = ci_base < p.c0;  // a 32-channel block lies in one source
+    const i32x4_t xr = buffer_desc(first ? p.x0 : p.x1, first ? p.x0bytes : p.x1bytes);
+    const i32x4_t dr = buffer_desc(p.dy, p.dybytes);
+    const int xs = first ? p.c0 : p.c1, xc = first ? ci_base : ci_base - p.c0;
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int pc0 = (tid & ~63) + i * kWThreads;  // wave-uniform first piece
+      if (pc0 >= DYP + XP) break;
+      const int pc = pc0 + lane;
+      uint32_t voff = kOOB;
+      if (pc0 < DYP) {
+        const int r = pc >> 3, q = pc & 7;
+        const int ql = q ^ (((r >> 1) & 1) << 2);
+        if (r < boxvol) {
+          const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+          const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+          if (gd < p.D && gh < p.H && gw < p.W)
+            voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * p.Cout + co_base + ql * 8) * 2);
+        }
+        dma16(dr, __builtin_amdgcn_readfirstlane(lb0 + pc0 * 16), voff, 0);
+      } else {
+        const int hp = pc - DYP;
+        const int hv = hp >> 2, q = hp & 3;
+        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+        if (hp < XP && gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && xc + q * 8 < xs)
+          voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * xs + xc + q * 8) * 2);
+        dma16(xr, __builtin_amdgcn_readfirstlane(lb0 + DYBYTES + (pc0 - DYP) * 16), voff, 0);
+      }
+    }
+  };
+
+  if (b_beg < b_end && p.dma) {
+    if constexpr (Tr::NBUF == 2) {
+      stage_dma(wlds, b_beg);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int b = b_beg; b < b_end; ++b) {
+        const int cur = (b - b_beg) & 1;
+        if (b + 1 < b_end) stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
+        compute(wlds + cur * BUFBYTES);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else if (b_beg < b_end) {
     if constexpr (Tr::NBUF == 2) {
       stage_load(b_beg);
       stage_store(wlds);
       __syncthreads();
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
-        if (b + 1 < b_end) stage_load(b + 1);
-        compute(wlds + cur * BUFBYTES);
-        if (b + 1 < b_end) stage_store(wlds + (cur ^ 1) * BUFBYTES);
+        if (b + 1 < b_end && !(PCMS_ABL & 4096)) stage_load(b + 1);
+        if (!(PCMS_ABL & 8192)) compute(wlds + cur * BUFBYTES);
+        if (b + 1 < b_end && !(PCMS_ABL & 4096)) stage_store(wlds + (cur ^ 1) * BUFBYTES);
         __syncthreads();
       }
     } else {
@@ -670,7 +735,12 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     }
   }
 
-  // flush: C[row = co][col = ci] of tap -> dwt[tap][co][ci] (coalesced along ci)
+  // flush: C[row = co][col = ci] of tap -> this split's partial row dwt[split][tap][co][ci]
+  // with plain stores (two 128-B row segments per instruction); the splits are summed in a
+  // fixed order by wgrad_group_sum_kernel / wgrad_reduce_kernel.  (fp32 atomics from every
+  // split into one [27][Cout][Cin] image serialised on the contended addresses: 2-4x the
+  // kernel's own time at level 0.)
+  float* prow = p.dwt + (long)split * 27 * p.Cout * p.Cin;
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
     if (j >= ntap) continue;
@@ -679,22 +749,40 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     for (int e = 0; e < 16; ++e) {
       const int co = co_base + cot * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
       const int ci = ci_base + (lane & 31);
-      if (co < p.Cout && ci < p.Cin)
-        atomicAdd(p.dwt + ((long)tap * p.Cout + co) * p.Cin + ci, acc[j][e]);
+      if (co < p.Cout && ci < p.Cin) prow[((long)tap * p.Cout + co) * p.Cin + ci] = acc[j][e];
     }
   }
 }
 
-// dwt [27][Cout][Cin] (fp32 workspace, Cin = stored channels) -> dw [Cout][Cw][27] (+=),
-// torch OIDHW layout with the weight's own input-channel count Cw <= Cin (stem: 5 of 8).
-// Block = (co, 32 input channels): the [27][32] source tile is read as 27 coalesced 128-B
-// rows, transposed through LDS, and added to the contiguous 32 x 27 run of dw.
-__global__ void __launch_bounds__(256) wgrad_permute_kernel(const float* dwt, float* dw, int Cout, int Cin, int Cw) {
+// Weight-gradient split reduction (deterministic, fixed order).  part: S rows of
+// E = 27 * Cout * Cin floats ([split][tap][co][ci], Cin = stored channels).
+// Stage 1 (S > 16): rows r*16 .. r*16+15 summed in place into row r*16.
+__global__ void __launch_bounds__(256) wgrad_group_sum_kernel(float* part, int S, long E) {
+  const long e = blockIdx.x * 256L + threadIdx.x;
+  if (e >= E) return;
+  const int r0 = blockIdx.y * 16, r1 = min(S, r0 + 16);
+  float* src = part + (long)r0 * E + e;
+  float sum = 0.f;
+  for (int r = r0; r < r1; ++r, src += E) sum += *src;
+  part[(long)r0 * E + e] = sum;
+}
+// Stage 2: dw [Cout][Cw][27] (torch OIDHW, the weight's own input-channel count Cw <= Cin;
+// stem: 5 of 8) += sum of R rows spaced `stride` rows apart.  Block = (co, 32 channels): the
+// [27][32] tiles are read as 128-B rows, transposed through LDS, added to the contiguous
+// 32 x 27 run of dw.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, int R, int stride, float* dw,
+                                                           int Cout, int Cin, int Cw) {
   __shared__ float tile[27][33];
   const int co = blockIdx.x, ci0 = blockIdx.y * 32;
+  const long rstep = (long)stride * 27 * Cout * Cin;
   for (int e = threadIdx.x; e < 27 * 32; e += 256) {
     const int t = e >> 5, c = e & 31, ci = ci0 + c;
-    tile[t][c] = ci < Cw ? dwt[((long)t * Cout + co) * Cin + ci] : 0.f;
+    float sum = 0.f;
+    if (ci < Cw) {
+      const float* src = part + ((long)t * Cout + co) * Cin + ci;
+      for (int r = 0; r < R; ++r, src += rstep) sum += *src;
+    }
+    tile[t][c] = sum;
   }
   __syncthreads();
   float* dst = dw + ((long)co * Cw + ci0) * 27;
@@ -730,6 +818,43 @@ __global__ void __launch_bounds__(256) pack_conv3_kernel(const float* w, T* out,
     if (j0 + jj >= J) continue;
     const float v = flip ? tile[jj][k][26 - t] : tile[jj][k][t];
     out[(((long)chunk * 27 + t) * J + j0 + jj) * CK + k] = Elem<T>::cvt(v);
+  }
+}
+
+// bf16 fast path (Kdim % 32 == 0, J % 8 == 0: every layer but the stem): the same block, read
+// as 16-B vectors (the block's source is 8 contiguous 864-float runs (fwd) or 32 contiguous
+// 216-float runs (dgrad)) and written as 16-B vectors of 8 packed k.
+__global__ void __launch_bounds__(256) pack_conv3_bf16_kernel(const float* w, bf16_t* out, int Cout, int Cin,
+                                                              int flip) {
+  __shared__ float tile[8][32][27];
+  const int J = flip ? Cin : Cout;
+  const int chunk = blockIdx.y;
+  const int j0 = blockIdx.x * 8;
+  for (int e = threadIdx.x; e < 1728; e += 256) {
+    int base, run, q;
+    if (!flip) {  // w[j0 + jj][chunk*32 .. +32][27]: run jj of 864 floats
+      run = e / 216; q = e % 216;
+      base = ((j0 + run) * Cin + chunk * 32) * 27;
+    } else {      // w[chunk*32 + k][j0 .. j0+8][27]: run k of 216 floats
+      run = e / 54; q = e % 54;
+      base = ((chunk * 32 + run) * Cin + j0) * 27;
+    }
+    const f32x4_t v = *reinterpret_cast<const f32x4_t*>(w + base + 4 * q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = 4 * q + i;
+      if (!flip) tile[run][idx / 27][idx % 27] = v[i];
+      else tile[idx / 27][run][idx % 27] = v[i];
+    }
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < 864; g += 256) {
+    const int t = g >> 5, jj = (g >> 2) & 7, k8 = (g & 3) * 8;
+    const int ts = flip ? 26 - t : t;
+    u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(tile[jj][k8 + 2 * i][ts], tile[jj][k8 + 2 * i + 1][ts]);
+    *reinterpret_cast<u32x4_t*>(out + (((long)chunk * 27 + t) * J + j0 + jj) * 32 + k8) = o;
   }
 }
 
@@ -1040,7 +1165,6 @@ constexpr int kSDThreads = 512;
 constexpr int kSDHaloRows = kHaloMax;                         // 1152 rows (18 x 64)
 constexpr int kSDHaloBytes = kSDHaloRows * 16;
 constexpr int kSDLds = 2 * kSDHaloBytes + 8 * 64 * 3 * 4;     // halo x2 + stats reduction
-constexpr uint32_t kOOB = 0x80000000u;                         // voffset past num_records
 
 template <int LBD, int LBH>
 __global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
@@ -2130,7 +2254,9 @@ int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int
   const int J = flip ? Cin : Cout;
   const int Kdim = flip ? Cout : Cin;
   dim3 grid(cdiv(J, 8), cdiv(Kdim, CK));
-  if (dtype == PCMS_BF16)
+  if (dtype == PCMS_BF16 && Kdim % 32 == 0 && J % 8 == 0)
+    hipLaunchKernelGGL(pack_conv3_bf16_kernel, grid, dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip);
+  else if (dtype == PCMS_BF16)
     hipLaunchKernelGGL((pack_conv3_kernel<bf16_t, 32>), grid, dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip);
   else
     hipLaunchKernelGGL((pack_conv3_kernel<float, 16>), grid, dim3(256), 0, s, w, (float*)out, Cout, Cin, flip);
@@ -2316,9 +2442,33 @@ int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin
   PCMS_CHECK_LAUNCH();
 }
 
+// Weight-gradient launch plan: box geometry, boxes per split, split count (shared by the
+// launch and its workspace query)
+struct WgradPlan { Box b; int nbd, nbh, nbw, nbox, bps, splits; };
+static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int Cout, int target_wgs) {
+  WgradPlan q;
+  const int bv = dtype == PCMS_BF16 ? WTraits<bf16_t>::BV : WTraits<float>::BV;
+  q.b = choose_box(D, H, W, bv, kWHaloMax, 4, 16);
+  q.nbd = cdiv(D, 1 << q.b.lbd); q.nbh = cdiv(H, 1 << q.b.lbh); q.nbw = cdiv(W, 1 << q.b.lbw);
+  q.nbox = N * q.nbd * q.nbh * q.nbw;
+  const int tiles = (Cout / 64) * cdiv(Cin, 32);
+  if (target_wgs <= 0) target_wgs = 512;
+  const int splits = std::max(1, std::min(q.nbox, cdiv(target_wgs, tiles)));
+  q.bps = cdiv(q.nbox, splits);
+  q.splits = cdiv(q.nbox, q.bps);
+  return q;
+}
+
+// fp32 workspace floats pcms_conv3_wgrad needs: one [27][Cout][c0+c1] partial row per split
+int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout, int target_wgs) {
+  const int Cin = c0 + c1;
+  return wgrad_plan(dtype, N, D, H, W, Cin, Cout, target_wgs).splits * 27 * Cout * Cin;
+}
+
 // Weight gradient: dw (torch layout [Cout][cin_w][27], fp32) += sum_v dy (x) x, where
 // cin_w <= c0 + c1 is the weight's input-channel count (the stored input may be padded).
-// dwt: fp32 workspace of 27*Cout*Cin floats (zeroed here).
+// dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (per-split partial rows, summed in a
+// fixed order: the result is deterministic).
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w, int target_wgs,
                      hipStream_t s) {
@@ -2326,28 +2476,29 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   if (cin_w <= 0 || cin_w > Cin) return -4;
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0) return -1;
-  const int bv = dtype == PCMS_BF16 ? WTraits<bf16_t>::BV : WTraits<float>::BV;
-  Box b = choose_box(D, H, W, bv, kWHaloMax, 4, 16);
+  const WgradPlan q = wgrad_plan(dtype, N, D, H, W, Cin, Cout, target_wgs);
   WgradParams p;
   p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1; p.dy = dy; p.dwt = dwt;
   p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
-  p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
-  p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
-  p.nbox = N * p.nbd * p.nbh * p.nbw;
-  const int tiles = (Cout / 64) * cdiv(Cin, 32);
-  if (target_wgs <= 0) target_wgs = 512;
-  int splits = std::max(1, std::min(p.nbox, cdiv(target_wgs, tiles)));
-  p.boxes_per_split = cdiv(p.nbox, splits);
-  splits = cdiv(p.nbox, p.boxes_per_split);
-  hipError_t e = hipMemsetAsync(dwt, 0, sizeof(float) * 27L * Cout * Cin, s);
-  if (e != hipSuccess) return (int)e;
-  dim3 grid(splits, Cout / 64, cdiv(Cin, 32));
+  p.lbd = q.b.lbd; p.lbh = q.b.lbh; p.lbw = q.b.lbw;
+  p.nbd = q.nbd; p.nbh = q.nbh; p.nbw = q.nbw;
+  p.nbox = q.nbox;
+  p.boxes_per_split = q.bps;
+  const long nvox = (long)N * D * H * W;
+  p.dma = dtype == PCMS_BF16 && (c1 == 0 || c0 % 32 == 0) && nvox * std::max(Cout, std::max(c0, c1)) * 2 < (long)kOOB;
+  p.x0bytes = (uint32_t)(nvox * c0 * 2);
+  p.x1bytes = (uint32_t)(nvox * c1 * 2);
+  p.dybytes = (uint32_t)(nvox * Cout * 2);
+  const int splits = q.splits;
+  p.nco = Cout / 64;
+  p.nci = cdiv(Cin, 32);
+  dim3 grid(splits * p.nco * p.nci);
   size_t lds;
   if (dtype == PCMS_BF16) {
     lds = (size_t)WTraits<bf16_t>::NBUF * (WTraits<bf16_t>::BV * WTraits<bf16_t>::DYROW + kWHaloMax * WTraits<bf16_t>::XROW);
     auto kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1>;
-    if (b.lbd == 2 && b.lbh == 2 && b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
-    else if (b.lbd == 1 && b.lbh == 3 && b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
+    if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
+    else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
   } else {
@@ -2355,10 +2506,20 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
     (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<float, -1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((conv3_wgrad_kernel<float, -1, -1, -1>), grid, dim3(kWThreads), lds, s, p);
   }
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(wgrad_permute_kernel, dim3(Cout, cdiv(cin_w, 32)), dim3(256), 0, s, (const float*)dwt, dw,
-                     Cout, Cin, cin_w);
+  const long E = 27L * Cout * Cin;
+  int R = splits, stride = 1;
+  if (splits > 16) {
+    hipLaunchKernelGGL(wgrad_group_sum_kernel, dim3((unsigned)cdiv(E, 256), cdiv(splits, 16)), dim3(256), 0, s, dwt,
+                       splits, E);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    R = cdiv(splits, 16);
+    stride = 16;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(Cout, cdiv(cin_w, 32)), dim3(256), 0, s, (const float*)dwt, R, stride,
+                     dw, Cout, Cin, cin_w);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -260,7 +260,14 @@ class UNetEngine:
         b["stats"] = torch.empty(max(rows_f, rows_s, rows_b) * (1024 * 2 + 1), dtype=torch.float32, device=dev)
         b["coef"] = torch.empty(3 * 1024, dtype=torch.float32, device=dev)
         b["bnws"] = torch.empty(query("pcms_bn_ws_doubles", 1024), dtype=torch.float64, device=dev)
-        b["dwt"] = torch.empty(27 * 1024 * 1024, dtype=torch.float32, device=dev)
+        # weight-gradient workspace: per-split partial rows of the largest conv (and the stem)
+        ws = [query("pcms_stem_wgrad_ws_floats", N, *S[0], self.nmod)] if self.stem_fast else []
+        for blk, l in [(bk, i) for i, bk in enumerate(self.enc)] + [(bk, 3 - i) for i, bk in enumerate(self.dec)]:
+            for cs, c1 in ((blk.c0, C[l] if blk in self.dec else 0), (blk.c1, 0)):
+                c0 = cs.cin_store - c1
+                ws.append(query("pcms_conv3_wgrad_ws_floats", self.code, N, *S[l], c0, c1, cs.cout,
+                                self.wgrad_target))
+        b["dwt"] = torch.empty(max(ws), dtype=torch.float32, device=dev)
         # split-K accumulators only where a level can be split (few workgroups along M)
         split_lv = [l for l in range(5) if query("pcms_conv3_mblocks", N, *S[l]) * (C[l] // 64) < 192]
         b["yacc"] = torch.empty(max([nv[l] * 2 * C[l] for l in split_lv] + [1]), dtype=torch.float32, device=dev)

@@ -67,7 +67,7 @@ def main():
         stats = torch.empty(rows * (cout * 2 + 1), device="cuda")
         bias = torch.zeros(cout, device="cuda")
         dw = torch.zeros(cout * cin * 27, device="cuda")
-        dwt = torch.empty(27 * cout * cin, device="cuda")
+        dwt = torch.empty(L.query("pcms_conv3_wgrad_ws_floats", code, N, D, H, W, cin, 0, cout, 512), device="cuda")
         acc = torch.empty(nvox * max(cin, cout), device="cuda") if l >= 3 else None
         out = []
         if not only or "fwd" in only:

@@ -248,7 +248,7 @@ def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
     # the stored input may carry zero pad channels (stem: 5 of 8); dw has the weight's Cin
     guard = 4096
     dw_full = torch.zeros(cout * cin_real * 27 + guard, device=DEV)
-    ws = torch.empty(27 * cout * cin, device=DEV)
+    ws = torch.empty(L.query("pcms_conv3_wgrad_ws_floats", code, N, *S, c0, c1, cout, 256), device=DEV)
     xs = ndhwc(x).to(DEV)
     if c1:
         L.call("pcms_conv3_wgrad", code, ndhwc(x[:, :c0]).to(DEV), c0, ndhwc(x[:, c0:]).to(DEV), c1,
