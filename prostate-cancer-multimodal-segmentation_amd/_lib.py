@@ -44,6 +44,7 @@ SIGNATURES = {
     "pcms_convt_pack": "ippiiis",
     "pcms_convt_fwd": "ippppiiiiiiiiis",
     "pcms_convt_dgrad": "ipppiiiiiiiiis",
+    "pcms_convt_wgrad_ws_floats": "iiiiiii",
     "pcms_convt_wgrad": "ippppiiiiiiiiiis",
     "pcms_box_channel_sum": "ippiiiiiiiiiiis",
     "pcms_head_fwd": "ippppliis",

@@ -1745,17 +1745,30 @@ __global__ void __launch_bounds__(256, 1) stem_wgrad_kernel(const bf16_t* x, con
 // Flush: one fp32 partial row [64][cin_w][27] per workgroup (plain stores), summed into dw
 // by stem_wgrad_reduce_kernel (deterministic, no atomics).
 constexpr int kSWT = 256;                                  // 4 waves, one per SIMD
-constexpr int kSWBV = 256;                                 // 4 x 4 x 16 voxels
-constexpr int kSWHV = 6 * 6 * 18;                          // 648 halo rows
-constexpr int kSWHRows = 704;                              // halo rows written (11 x 64)
-constexpr int kSWBuf = kSWBV * 128 + kSWHRows * 16;        // 43 KiB per ring slot
-constexpr int kSWLds = 3 * kSWBuf;                         // 129 KiB
+// BD = box depth (boxes BD x 4 x 16), NS = ring slots (NS - 1 boxes in flight).  The load
+// pipeline is latency-bound (bytes in flight per CU), so the product ring uses 2-deep boxes
+// in 6 slots (115 KB in flight) rather than 4-deep boxes in 3 slots (86 KB).
+template <int BD> struct SWGeom {
+  static constexpr int BV = BD * 64;                            // voxels per box
+  static constexpr int HV = (BD + 2) * 6 * 18;                  // halo rows (16 B)
+  static constexpr int HRows = (HV + 63) / 64 * 64;             // rows written
+  static constexpr int Buf = BV * 128 + HRows * 16;             // bytes per ring slot
+  static constexpr int DYP = BV * 8 / kSWT;                     // dy DMA pieces per thread
+  static constexpr int XI = (HRows / 64 + 3) / 4;               // halo DMA rounds per wave
+};
+constexpr int kSWBD = (PCMS_ABL & 4096) ? 2 : 4;  // 2-deep x 6 slots measured slower
+constexpr int kSWNS = kSWBD == 4 ? 3 : 6;
+constexpr int kSWLds = kSWNS * SWGeom<kSWBD>::Buf;
 static_assert(kSWLds >= 64 * 224 * 4, "flush tile fits in the ring");
+static_assert(kSWLds <= 160 * 1024, "ring fits in LDS");
 
+template <int BD, int NS>
 __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t* x, const bf16_t* dy, float* part,
                                                                     int N, int D, int H, int W, int cin_w,
                                                                     uint32_t xbytes, uint32_t dybytes) {
-  constexpr int BD = 4, BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
+  typedef SWGeom<BD> Gm;
+  constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
+  constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
   extern __shared__ __attribute__((aligned(16))) char swl[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1766,19 +1779,20 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   const i32x4_t dr = buffer_desc(dy, dybytes);
 
   // per-thread DMA source offsets relative to the box origin (constant over boxes)
-  uint32_t dyrel[8];
+  uint32_t dyrel[Gm::DYP];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < Gm::DYP; ++i) {
     const int pc = tid + i * kSWT;
     const int r = pc >> 3, q = pc & 7;
     const int ql = q ^ (((r >> 1) & 1) << 2);  // dy_off_bf16: 64-B halves swapped on odd row pairs
     const int rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
     dyrel[i] = (uint32_t)(((rd * H + rh) * W + rw) * 128 + ql * 16);
   }
-  const int nxp = wave < 3 ? 3 : 2;  // halo pieces of this wave: rows wave*64 + lane + 256 i
-  int xrel[3], xco[3];
+  // halo pieces of this wave: rows wave*64 + lane + 256 i < HRows (XI or XI - 1 of them)
+  const int nxp = (Gm::HRows / 64 - wave + 3) / 4;
+  int xrel[Gm::XI], xco[Gm::XI];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < Gm::XI; ++i) {
     const int hv = wave * 64 + lane + i * kSWT;
     const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
     xrel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
@@ -1799,10 +1813,10 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(swl) + slot * kSWBuf + wave * 64 * 16);
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)vb * 128u);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
+    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
     const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < Gm::XI; ++i) {
       if (i >= nxp) break;
       uint32_t voff = (uint32_t)(vb * 16 + xrel[i]);
       const int c = xco[i];
@@ -1853,8 +1867,8 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     s16x8_t a[2][2], bq[2][7];
     load(0, a[0], bq[0]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i + 1 < 4) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
+    for (int i = 0; i < BD; ++i) {
+      if (i + 1 < BD) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
 #pragma unroll
       for (int j = 0; j < 7; ++j)
 #pragma unroll
@@ -1862,23 +1876,26 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     }
   };
 
+  const int G = gridDim.x;
   int b = blockIdx.x;
-  if (b < nbox) stage(b, 0);
-  if (b + (int)gridDim.x < nbox) stage(b + gridDim.x, 1);
-  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
-    // retire box b's DMA (box b + G may stay in flight), then barrier: every wave's share
-    // of box b has landed and every wave is done reading the slot refilled below
-    if (b + (int)gridDim.x < nbox) {
-      if (wave < 3) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (b + k * G < nbox) stage(b + k * G, k);
+  for (int it = 0; b < nbox; b += G, ++it) {
+    // retire box b's DMA (the NS - 2 boxes after it may stay in flight), then barrier:
+    // every wave's share of box b has landed and every wave is done reading the slot
+    // refilled below
+    if (b + (NS - 2) * G < nbox) {
+      if (nxp == Gm::XI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI - 1)) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const int b2 = b + 2 * gridDim.x;
-    if (b2 < nbox && !(PCMS_ABL & 16)) stage(b2, (it + 2) % 3);
-    if (!(PCMS_ABL & 8)) compute(swl + (it % 3) * kSWBuf);
+    const int b2 = b + (NS - 1) * G;
+    if (b2 < nbox) stage(b2, (it + NS - 1) % NS);
+    compute(swl + (it % NS) * kSWBuf);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -2397,13 +2414,13 @@ static int device_cus() {
 }
 
 static bool stem_wgrad_streams(int N, int D, int H, int W) {
-  return D % 4 == 0 && H % 4 == 0 && W % 16 == 0 && (long)N * D * H * W * 128 < (1L << 31);
+  return D % kSWBD == 0 && H % 4 == 0 && W % 16 == 0 && (long)N * D * H * W * 128 < (1L << 31);
 }
 
 // fp32 workspace floats pcms_stem_wgrad needs (0: none)
 int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w) {
   if (!stem_wgrad_streams(N, D, H, W)) return 0;
-  const int nbox = N * (D / 4) * (H / 4) * (W / 16);
+  const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
   return std::min(nbox, device_cus()) * 64 * cin_w * 27;
 }
 
@@ -2414,11 +2431,12 @@ int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin
   if (cin_w > 8 || cin_w < 1) return -1;
   if (stem_wgrad_streams(N, D, H, W)) {
     if (ws == nullptr) return -2;
-    const int nbox = N * (D / 4) * (H / 4) * (W / 16);
+    const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
     const int grid = std::min(nbox, device_cus());
     const long xbytes = (long)N * D * H * W * 16, dybytes = (long)N * D * H * W * 128;
-    (void)hipFuncSetAttribute((const void*)stem_wgrad_stream_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kSWLds);
-    hipLaunchKernelGGL(stem_wgrad_stream_kernel, dim3(grid), dim3(kSWT), kSWLds, s, (const bf16_t*)x,
+    auto kern = stem_wgrad_stream_kernel<kSWBD, kSWNS>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSWLds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT), kSWLds, s, (const bf16_t*)x,
                        (const bf16_t*)dy, ws, N, D, H, W, cin_w, (uint32_t)xbytes, (uint32_t)dybytes);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;

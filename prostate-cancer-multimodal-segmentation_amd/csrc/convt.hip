@@ -57,8 +57,10 @@ __global__ void __launch_bounds__(256) convt_fwd_kernel(const T* x, const T* wt,
   if (m0 >= M) return;
   const long ma = std::min<long>(m0 + r, M - 1);
   const T* arow = x + ma * Cin;
-  const T* b0 = wt + (long)(q0 + r) * Cin;
-  const T* b1 = wt + (long)(q0 + 32 + r) * Cin;
+  // MFMA column r of N-tile j is output column q0 + 2 r + j: a lane holds a channel pair, so
+  // the bf16 build stores packed bf16x2 (two 128-B row segments per store instruction)
+  const T* b0 = wt + (long)(q0 + 2 * r) * Cin;
+  const T* b1 = b0 + Cin;
   f32x16_t acc0, acc1;
   for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
   for (int k = 0; k < Cin; k += GT<T>::KS) {
@@ -66,16 +68,19 @@ __global__ void __launch_bounds__(256) convt_fwd_kernel(const T* x, const T* wt,
     acc0 = mfma(a, ldfrag(b0 + k, h), acc0);
     acc1 = mfma(a, ldfrag(b1 + k, h), acc1);
   }
+  const int q = q0 + 2 * r;             // Cout % 64 == 0: the pair shares one tap
+  const int t = q / Cout, co = q % Cout;
+  const float bias0 = bias[co], bias1 = bias[co + 1];
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
     if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int q = q0 + j * 32 + r;
-      const int t = q / Cout, co = q % Cout;
-      const float v = (j ? acc1[e] : acc0[e]) + bias[co];
-      Elem<T>::st(out + child_vox(g, m, t) * Cout + co, v);
+    T* dst = out + child_vox(g, m, t) * Cout + co;
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<uint32_t*>(dst) = pack_bf16x2(acc0[e] + bias0, acc1[e] + bias1);
+    } else {
+      Elem<T>::st(dst, acc0[e] + bias0);
+      Elem<T>::st(dst + 1, acc1[e] + bias1);
     }
   }
 }
@@ -128,84 +133,139 @@ __device__ __forceinline__ s16x4_t tr_read(const char* lds, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + off));
 }
 
+// Workgroup tile: 64 ci x (8 taps x 64 co) over a voxel split.  A block of VB input voxels
+// stages x [VB][64 ci] once and the 8 taps' dout child rows [8][VB][64 co], so the x tile
+// feeds all 8 taps: 8 waves = (ci half, co half, tap half), 4 tap tiles each (16 MFMAs per
+// 64 voxels between barriers).  All of a thread's 16-B pieces of a block are loaded into
+// registers before any is written to LDS (the loads overlap instead of each waiting alone).
+template <typename T> struct CW { static constexpr int VB = sizeof(T) == 2 ? 64 : 32; };
+
 template <typename T>
-__global__ void __launch_bounds__(256) convt_wgrad_kernel(const T* x, const T* dout, float* ws, UpGeom g,
+__global__ void __launch_bounds__(512, 1) convt_wgrad_kernel(const T* x, const T* dout, float* ws, UpGeom g,
                                                           int Cin, int Cout, int vox_per_split) {
+  constexpr int VB = CW<T>::VB;
   constexpr int ROW = 64 * (int)sizeof(T);
-  __shared__ __attribute__((aligned(16))) char lds[2 * kVB * ROW];
-  char* P = lds;
-  char* Q = lds + kVB * ROW;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int PPR = 64 / VEC;                  // 16-B pieces per row
+  constexpr int NP = 9 * VB * PPR;               // pieces per block: x + 8 taps
+  constexpr int PT = NP / 512;                   // per thread
+  static_assert(NP % 512 == 0, "whole pieces per thread");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* P = lds;                                 // x tile [VB][64]
+  char* Q = lds + VB * ROW;                      // dout tiles [8][VB][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int wp = wave & 1, wq = wave >> 1;
+  const int wp = wave & 1, wq = (wave >> 1) & 1, t0 = (wave >> 2) * 4;  // ci half, co half, taps t0..t0+3
   const int p0 = blockIdx.z * 64;     // ci tile
-  const int qt = blockIdx.y;          // (t, co) tile: q = t*Cout + co
-  const int t = (qt * 64) / Cout, co0 = (qt * 64) % Cout;
+  const int co0 = blockIdx.y * 64;    // co tile
   const long M = (long)g.N * g.Din * g.Hin * g.Win;
   const long vbeg = (long)blockIdx.x * vox_per_split;
   const long vend = std::min<long>(M, vbeg + vox_per_split);
-  constexpr int VEC = 16 / (int)sizeof(T);
-  constexpr int PPR = 64 / VEC;       // pieces per row
-  f32x16_t acc, macc;
-  for (int e = 0; e < 16; ++e) { acc[e] = 0.f; macc[e] = 0.f; }
-  for (long vb = vbeg; vb < vend; vb += kVB) {
+  f32x16_t acc[4], macc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { acc[t][e] = 0.f; macc[t][e] = 0.f; }
+  for (long vb = vbeg; vb < vend; vb += VB) {
     if constexpr (sizeof(T) == 4) {  // fp32 build: per-block chains summed (two-level)
-      macc += acc;
-      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-    }
-    __syncthreads();
-    for (int pc = tid; pc < 2 * kVB * PPR; pc += 256) {
-      const int which = pc / (kVB * PPR), rem = pc % (kVB * PPR);
-      const int v = rem / PPR, q = rem % PPR;
-      const long m = vb + v;
-      u32x4_t val = {0u, 0u, 0u, 0u};
-      if (m < vend) {
-        const T* src = which == 0 ? x + m * Cin + p0 + q * VEC : dout + child_vox(g, m, t) * Cout + co0 + q * VEC;
-        val = *reinterpret_cast<const u32x4_t*>(src);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        macc[t] += acc[t];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
       }
-      char* base = which == 0 ? P : Q;
+    }
+    u32x4_t stg[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int pc = tid + i * 512;
+      const int which = pc / (VB * PPR), rem = pc % (VB * PPR);   // 0: x, 1 + t: dout tap t
+      const int v = rem / PPR, q = rem % PPR;
+      const long m = std::min<long>(vb + v, vend - 1);             // clamped (zeroed below)
+      const T* src = which == 0 ? x + m * Cin + p0 + q * VEC : dout + child_vox(g, m, which - 1) * Cout + co0 + q * VEC;
+      stg[i] = *reinterpret_cast<const u32x4_t*>(src);
+      if (vb + v >= vend) stg[i] = (u32x4_t){0u, 0u, 0u, 0u};
+    }
+    __syncthreads();  // every wave is done with the previous block's tiles
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int pc = tid + i * 512;
+      const int which = pc / (VB * PPR), rem = pc % (VB * PPR);
+      const int v = rem / PPR, q = rem % PPR;
       const int off = sizeof(T) == 2 ? half_swz(v, q * VEC) : v * ROW + q * 16;
-      *reinterpret_cast<u32x4_t*>(base + off) = val;
+      *reinterpret_cast<u32x4_t*>((which == 0 ? P : Q + (which - 1) * VB * ROW) + off) = stg[i];
     }
     __syncthreads();
     if constexpr (sizeof(T) == 2) {
       const int gg = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-      for (int k0 = 0; k0 < kVB; k0 += 16) {
+      const int ca = wp * 32 + gg * 16 + pp * 4, cb = wq * 32 + gg * 16 + pp * 4;
+#pragma unroll
+      for (int k0 = 0; k0 < VB; k0 += 16) {
         const int v = k0 + 8 * h + qq;
-        const int ca = wp * 32 + gg * 16 + pp * 4, cb = wq * 32 + gg * 16 + pp * 4;
         s16x4_t a0 = tr_read(P, half_swz(v, ca)), a1 = tr_read(P, half_swz(v + 4, ca));
-        s16x4_t b0 = tr_read(Q, half_swz(v, cb)), b1 = tr_read(Q, half_swz(v + 4, cb));
         s16x8_t a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        s16x8_t b = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-        acc = mfma(a, b, acc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const char* Qt = Q + (t0 + t) * VB * ROW;
+          s16x4_t b0 = tr_read(Qt, half_swz(v, cb)), b1 = tr_read(Qt, half_swz(v + 4, cb));
+          s16x8_t b = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+          acc[t] = mfma(a, b, acc[t]);
+        }
       }
     } else {
-      for (int k0 = 0; k0 < kVB; k0 += 2) {
+      for (int k0 = 0; k0 < VB; k0 += 2) {
         const int v = k0 + h;
         float a = *reinterpret_cast<const float*>(P + v * ROW + (wp * 32 + (lane & 31)) * 4);
-        float b = *reinterpret_cast<const float*>(Q + v * ROW + (wq * 32 + (lane & 31)) * 4);
-        acc = mfma(a, b, acc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float b = *reinterpret_cast<const float*>(Q + (t0 + t) * VB * ROW + v * ROW + (wq * 32 + (lane & 31)) * 4);
+          acc[t] = mfma(a, b, acc[t]);
+        }
       }
     }
   }
-  if constexpr (sizeof(T) == 4) acc += macc;
-  // C[row = ci][col = co]; ws layout [Cin][8][Cout]
+  if constexpr (sizeof(T) == 4) {
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int ci = p0 + wp * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-    const int co = co0 + wq * 32 + (lane & 31);
-    atomicAdd(ws + ((long)ci * 8 + t) * Cout + co, acc[e]);
+    for (int t = 0; t < 4; ++t) acc[t] += macc[t];
   }
+  // C[row = ci][col = co] per tap -> this split's partial row ws[split][Cin][8][Cout] (plain
+  // stores; fp32 atomics from every split into one image serialise on contended addresses)
+  float* prow = ws + (long)blockIdx.x * 8 * Cin * Cout;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int ci = p0 + wp * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int co = co0 + wq * 32 + (lane & 31);
+      prow[((long)ci * 8 + t0 + t) * Cout + co] = acc[t][e];
+    }
 }
 
-// ws [Cin][8][Cout] -> dw [Cin][Cout][8] (+=), torch ConvTranspose3d layout
-__global__ void convt_wgrad_permute(const float* ws, float* dw, int Cin, int Cout) {
-  const long total = (long)Cin * Cout * 8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int t = i & 7;
-    const long r = i >> 3;
-    const int co = r % Cout, ci = r / Cout;
-    dw[i] += ws[((long)ci * 8 + t) * Cout + co];
-  }
+// split reduction, fixed order.  Stage 1 (S > 16): rows r*16 .. r*16+15 summed in place into
+// row r*16 (E floats per row).
+__global__ void __launch_bounds__(256) convt_group_sum(float* ws, int S, long E) {
+  const long e = blockIdx.x * 256L + threadIdx.x;
+  if (e >= E) return;
+  const int r0 = blockIdx.y * 16, r1 = min(S, r0 + 16);
+  float* src = ws + (long)r0 * E + e;
+  float sum = 0.f;
+  for (int r = r0; r < r1; ++r, src += E) sum += *src;
+  ws[(long)r0 * E + e] = sum;
+}
+// Stage 2: dw [Cin][Cout][8] (torch ConvTranspose3d layout, +=) = sum of R rows of
+// [Cin][8][Cout] spaced `stride` rows apart.  Block = (ci, 32 co): [8][32] tiles read as
+// 128-B rows, transposed through LDS, added to the contiguous 32 x 8 run of dw.
+__global__ void __launch_bounds__(256) convt_wgrad_reduce(const float* ws, int R, int stride, float* dw, int Cin,
+                                                          int Cout) {
+  __shared__ float tile[8][33];
+  const int ci = blockIdx.x, co0 = blockIdx.y * 32;
+  const long rstep = (long)stride * 8 * Cin * Cout;
+  const int e = threadIdx.x, t = e >> 5, c = e & 31;
+  const float* src = ws + ((long)ci * 8 + t) * Cout + co0 + c;
+  float sum = 0.f;
+  for (int r = 0; r < R; ++r, src += rstep) sum += *src;
+  tile[t][c] = sum;
+  __syncthreads();
+  dw[((long)ci * Cout + co0) * 8 + e] += tile[e & 7][e >> 3];
 }
 
 // master W[Cin][Cout][8] fp32 ->  fwd pack [8][Cout][Cin]  /  dgrad pack [Cin][8][Cout]
@@ -274,30 +334,56 @@ int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
   PCMS_CHECK_LAUNCH();
 }
 
-// dw (torch layout [Cin][Cout][2][2][2], fp32) += ...; ws: Cin*8*Cout floats (zeroed here)
+static int convt_wgrad_splits(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs, int* vps) {
+  const long M = (long)N * Din * Hin * Win;
+  const int tiles = (Cout / 64) * (Cin / 64);
+  if (target_wgs <= 0) target_wgs = 512;
+  const long nvb = (M + kVB - 1) / kVB;
+  int splits = (int)std::max<long>(1, std::min<long>(nvb, cdiv(target_wgs, tiles)));
+  *vps = (int)(cdiv(nvb, splits) * kVB);
+  return (int)((M + *vps - 1) / *vps);
+}
+
+// fp32 workspace floats pcms_convt_wgrad needs: one [Cin][8][Cout] partial row per split
+int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs) {
+  int vps;
+  return convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps) * 8 * Cin * Cout;
+}
+
+// dw (torch layout [Cin][Cout][2][2][2], fp32) += ...; ws: pcms_convt_wgrad_ws_floats(...)
+// floats (per-split partial rows summed in a fixed order: deterministic)
 int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
                      int target_wgs, hipStream_t s) {
   if (Cin % 64 || Cout % 64) return -1;
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
-  const long M = (long)N * Din * Hin * Win;
-  hipError_t e = hipMemsetAsync(ws, 0, sizeof(float) * 8L * Cin * Cout, s);
+  int vps;
+  const int splits = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps);
+  dim3 grid(splits, Cout / 64, Cin / 64);
+  if (dtype == PCMS_BF16) {
+    constexpr int lds = 9 * CW<bf16_t>::VB * 128;
+    (void)hipFuncSetAttribute((const void*)convt_wgrad_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(convt_wgrad_kernel<bf16_t>, grid, dim3(512), lds, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g,
+                       Cin, Cout, vps);
+  } else {
+    constexpr int lds = 9 * CW<float>::VB * 256;
+    (void)hipFuncSetAttribute((const void*)convt_wgrad_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(convt_wgrad_kernel<float>, grid, dim3(512), lds, s, (const float*)x, (const float*)dout, ws, g,
+                       Cin, Cout, vps);
+  }
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const int tiles = (8 * Cout / 64) * (Cin / 64);
-  if (target_wgs <= 0) target_wgs = 1024;
-  const long nvb = (M + kVB - 1) / kVB;
-  int splits = (int)std::max<long>(1, std::min<long>(nvb, cdiv(target_wgs, tiles)));
-  const int vps = (int)(cdiv(nvb, splits) * kVB);
-  splits = (int)((M + vps - 1) / vps);
-  dim3 grid(splits, 8 * Cout / 64, Cin / 64);
-  if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL(convt_wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g, Cin, Cout, vps);
-  else
-    hipLaunchKernelGGL(convt_wgrad_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (const float*)dout, ws, g, Cin, Cout, vps);
-  e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  const long total = 8L * Cin * Cout;
-  hipLaunchKernelGGL(convt_wgrad_permute, dim3((int)std::min<long>(4096, (total + 255) / 256)), dim3(256), 0, s, (const float*)ws, dw, Cin, Cout);
+  const long E = 8L * Cin * Cout;
+  int R = splits, stride = 1;
+  if (splits > 16) {
+    hipLaunchKernelGGL(convt_group_sum, dim3((unsigned)cdiv(E, 256), cdiv(splits, 16)), dim3(256), 0, s, ws, splits, E);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    R = cdiv(splits, 16);
+    stride = 16;
+  }
+  hipLaunchKernelGGL(convt_wgrad_reduce, dim3(Cin, Cout / 32), dim3(256), 0, s, (const float*)ws, R, stride, dw, Cin,
+                     Cout);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -271,7 +271,9 @@ class UNetEngine:
         # split-K accumulators only where a level can be split (few workgroups along M)
         split_lv = [l for l in range(5) if query("pcms_conv3_mblocks", N, *S[l]) * (C[l] // 64) < 192]
         b["yacc"] = torch.empty(max([nv[l] * 2 * C[l] for l in split_lv] + [1]), dtype=torch.float32, device=dev)
-        b["ctws"] = torch.empty(8 * 1024 * 512, dtype=torch.float32, device=dev)
+        ctws = [query("pcms_convt_wgrad_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels, 512)
+                for i, up in enumerate(self.ups)]
+        b["ctws"] = torch.empty(max(ctws), dtype=torch.float32, device=dev)
         self.bufs = b
         self.buf_key = key
 
@@ -435,7 +437,7 @@ class UNetEngine:
             _, dpack = self.convt_packs[i]
             hin = b["e4_x"] if i == 0 else b[f"d{l + 1}_a2"]
             call("pcms_convt_wgrad", self.code, hin, gu, up.weight.grad, b["ctws"], N, *S[l + 1], up.in_channels,
-                 up.out_channels, *S[l], 1024)
+                 up.out_channels, *S[l], 512)
             dz = (S[l][0] - 2 * S[l + 1][0]) // 2
             dy_ = (S[l][1] - 2 * S[l + 1][1]) // 2
             dx_ = (S[l][2] - 2 * S[l + 1][2]) // 2

@@ -363,7 +363,7 @@ def test_convt(dt, code, tol, Sin, Sout):
     dx = torch.empty(N, *Sin, cin, dtype=dt, device=DEV)
     L.call("pcms_convt_dgrad", code, god, dp, dx, N, *Sin, cin, cout, *Sout)
     dw = torch.zeros(cin, cout, 2, 2, 2, device=DEV)
-    ws = torch.empty(8 * cin * cout, device=DEV)
+    ws = torch.empty(L.query("pcms_convt_wgrad_ws_floats", N, *Sin, cin, cout, 64), device=DEV)
     L.call("pcms_convt_wgrad", code, ndhwc(x).to(DEV), god, dw, ws, N, *Sin, cin, cout, *Sout, 64)
     db = torch.zeros(cout, device=DEV)
     L.call("pcms_box_channel_sum", code, god, db, N, *Sout, cout, dz // 2, dyy // 2, dxx // 2,
