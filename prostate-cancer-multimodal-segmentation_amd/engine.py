@@ -108,7 +108,7 @@ class UNetEngine:
         self.epoch = 0
         self.saved_epoch = -1
         self.act_ckpt = False
-        self.wgrad_target = 512
+        self.wgrad_target = 256  # conv weight-gradient workgroups: one round of 1 WG per CU (fewer partial rows to reduce than 512)
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
         self._flatten()
         for bn in self.bns:

@@ -14,7 +14,7 @@ def short(name: str) -> str:
     name = re.sub(r"\(anonymous namespace\)::", "", name)
     name = re.sub(r"\(.*", "", name)
     name = re.sub(r"^void ", "", name)
-    return name[:70]
+    return name[:70].replace(",", ";")
 
 
 def main():
