@@ -1161,15 +1161,19 @@ __global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p
 // (out-of-range voffset = zero padding); weights stay in VGPRs; BatchNorm partials are
 // accumulated over all boxes of the workgroup (shifted sums) and written as ONE stats row
 // per workgroup (rows >= gridDim.x are zeroed: count 0).
-constexpr int kSDThreads = 512;
+// THR = 512: one 8-wave workgroup per CU, 512-voxel boxes; THR = 256: two independent
+// 4-wave workgroups per CU with 256-voxel boxes (each workgroup's barrier-synchronised
+// compute and store phases drift against the other's).
 constexpr int kSDHaloRows = kHaloMax;                         // 1152 rows (18 x 64)
 constexpr int kSDHaloBytes = kSDHaloRows * 16;
 constexpr int kSDLds = 2 * kSDHaloBytes + 8 * 64 * 3 * 4;     // halo x2 + stats reduction
+constexpr int kSDThr = (PCMS_ABL & 8192) ? 256 : 512;  // product variant (256: same time, 101 vs 102 us)
 
-template <int LBD, int LBH>
-__global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
-                                                                        uint32_t xbytes, uint32_t ybytes) {
-  static_assert(LBD + LBH == 5, "512-voxel boxes");
+template <int LBD, int LBH, int THR>
+__global__ void __launch_bounds__(THR, 512 / THR) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
+                                                                         uint32_t xbytes, uint32_t ybytes) {
+  constexpr int kSDThreads = THR, NWV = THR / 64;
+  static_assert((1 << (LBD + LBH + 4)) == NWV * 64, "box = 64 voxels per wave");
   constexpr int bd = 1 << LBD, bh = 1 << LBH, bw = 16;
   constexpr int HH = bh + 2, HW = bw + 2, HV = (bd + 2) * HH * HW;
   constexpr int NP = (HV + kSDThreads - 1) / kSDThreads;  // halo pieces per thread
@@ -1348,11 +1352,11 @@ __global__ void __launch_bounds__(kSDThreads, 1) stem_fwd_direct_kernel(Conv3Par
   if (tid < 64) {
     float S = 0.f, Nn = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
+    for (int w = 0; w < NWV; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
     const float m = Nn > 0.f ? S / Nn : 0.f;
     float M2 = 0.f, sdd = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
+    for (int w = 0; w < NWV; ++w) {
       const float c = red[(w * 64 + tid) * 3 + 2];
       if (c > 0.f) {
         const float d = red[(w * 64 + tid) * 3] / c - m;
@@ -2387,9 +2391,17 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
   const bool direct = b.lbw == 4 && b.lbd + b.lbh == 5 && (b.lbd == 2 || b.lbd == 3) && ybytes < (long)kOOB;
   if (direct) {
     const int grid = std::min(nbox, ncu);
-    auto kern = b.lbd == 2 ? stem_fwd_direct_kernel<2, 3> : stem_fwd_direct_kernel<3, 2>;
+    auto kern = b.lbd == 2 ? stem_fwd_direct_kernel<2, 3, 512> : stem_fwd_direct_kernel<3, 2, 512>;
+    int g2 = grid;
+    if (kSDThr == 256) {  // 4x4x16 boxes, two workgroups per CU; rows stay <= the caller's
+      p.lbd = 2; p.lbh = 2;
+      p.nbd = cdiv(D, 4); p.nbh = cdiv(H, 4);
+      g2 = std::min(std::min(p.N * p.nbd * p.nbh * p.nbw, 2 * ncu), nbox);
+      kern = stem_fwd_direct_kernel<2, 2, 256>;
+    }
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSDLds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThreads), kSDLds, s, p, nbox, nbox, (uint32_t)xbytes,
+    hipLaunchKernelGGL(kern, dim3(g2), dim3(kSDThr), kSDLds, s, p, kSDThr == 256 ? p.N * p.nbd * p.nbh * p.nbw : nbox,
+                       nbox, (uint32_t)xbytes,
                        (uint32_t)ybytes);
     PCMS_CHECK_LAUNCH();
   }
