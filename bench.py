@@ -98,8 +98,18 @@ def stem_roofline(tr, N, spatial, reps):
     wg_bytes = xb + yb + 64 * 5 * 27 * 4
     t = res["fwd"] + res["wgrad"]
     achieved = (fwd_bytes + wg_bytes) / t
+    # HBM bytes per fwd+wgrad pair from the PMC counters (FETCH_SIZE / WRITE_SIZE in separate
+    # rocprofv3 passes, gfx950 FETCH correction: tests/kexp/pmc_stem_traffic.sh), committed
+    # for the shape they were measured on; null for any other shape
+    traffic = None
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_stem_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            rec = json.load(f)
+        if rec.get("shape") == [N, D, H, W] and code == 1:
+            traffic = rec["traffic_bytes_per_pair"]
     return {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
             "kernel": "stem conv3d 5->64 fwd + wgrad (stem_fwd_kernel + stem_wgrad_kernel)",
             "algorithmic_bytes": fwd_bytes + wg_bytes, "t_fwd_us": round(res["fwd"] * 1e6, 1),
             "t_wgrad_us": round(res["wgrad"] * 1e6, 1)}
