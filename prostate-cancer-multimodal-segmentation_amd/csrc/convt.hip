@@ -37,13 +37,19 @@ struct UpGeom {
   int pz, py, px;           // pad-lo offsets
 };
 
-__device__ __forceinline__ long child_vox(const UpGeom& g, long m, int t) {
-  const int w = m % g.Win; long r = m / g.Win;
-  const int h = r % g.Hin; r /= g.Hin;
-  const int d = r % g.Din; const int n = r / g.Din;
-  const int od = 2 * d + (t >> 2) + g.pz, oh = 2 * h + ((t >> 1) & 1) + g.py, ow = 2 * w + (t & 1) + g.px;
-  return (((long)n * g.Do + od) * g.Ho + oh) * g.Wo + ow;
+// child voxel of input voxel m through tap t = (i, j, k) = (t >> 2, (t >> 1) & 1, t & 1).
+// 32-bit index math (the host checks M < 2^31): 64-bit division is a long software sequence.
+__device__ __forceinline__ long child_base(const UpGeom& g, long m) {
+  const uint32_t mm = (uint32_t)m;
+  const uint32_t w = mm % (uint32_t)g.Win; uint32_t r = mm / (uint32_t)g.Win;
+  const uint32_t h = r % (uint32_t)g.Hin; r /= (uint32_t)g.Hin;
+  const uint32_t d = r % (uint32_t)g.Din; const uint32_t n = r / (uint32_t)g.Din;
+  return (((long)n * g.Do + 2 * d + g.pz) * g.Ho + 2 * h + g.py) * g.Wo + 2 * w + g.px;
 }
+__device__ __forceinline__ long tap_delta(const UpGeom& g, int t) {
+  return ((long)(t >> 2) * g.Ho + ((t >> 1) & 1)) * g.Wo + (t & 1);
+}
+__device__ __forceinline__ long child_vox(const UpGeom& g, long m, int t) { return child_base(g, m) + tap_delta(g, t); }
 
 // wave tile 32 (M) x 64 (N); workgroup 4 waves stacked along M -> 128 x 64.
 template <typename T>
@@ -120,6 +126,136 @@ __global__ void __launch_bounds__(256) convt_dgrad_kernel(const T* dout, const T
     if (m >= M) continue;
     Elem<T>::st(dx + m * Cin + q0 + r, acc0[e]);
     Elem<T>::st(dx + m * Cin + q0 + 32 + r, acc1[e]);
+  }
+}
+
+// bf16 forward and dgrad, LDS-staged (the hot path).  The direct kernels above read each A
+// row 32 B per lane pair and instruction (the 32x32 A layout): ~25 % of each 128-B line per
+// request, ~1/5 of the HBM roofline.  Here a 512-thread workgroup owns 256 input voxels x 128
+// GEMM columns; per stage (a 64-channel chunk of K) it stages the 256 A rows (full 128-B
+// rows, 8 lanes per row) and the 128 x 64 weight tile into LDS (16-B slots XOR-swizzled by
+// row & 7), register-prefetching the next stage while 8 waves (32 voxels x 128 columns, 4
+// N-tiles) run their MFMAs.  Columns are channel pairs (packed bf16x2 stores).
+//   FWD:   A = x[m][Cin],                 K = Cin,      columns q = (t, co), out[child(m,t)][co] + b
+//   dgrad: A = dout[child(m, t)][Cout],   K = 8 Cout,   columns = ci,        dx[m][ci]
+constexpr int kCDM = 256, kCDN = 128;
+constexpr int kCDStage = kCDM * 128 + kCDN * 128;                 // 48 KiB per stage
+constexpr int kCDPieces = kCDStage / 16 / 512;                    // 6 per thread
+
+__device__ __forceinline__ int cd_slot(int row, int slot) { return row * 128 + ((slot ^ (row & 7)) << 4); }
+
+template <bool FWD>
+__global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, const bf16_t* wpk, const float* bias,
+                                                           bf16_t* out, UpGeom g, int Cin, int Cout) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r_lane = lane & 31, hsel = lane >> 5;
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  const long m0 = (long)blockIdx.x * kCDM;
+  const int q0 = blockIdx.y * kCDN;
+  const int K = FWD ? Cin : 8 * Cout, Ka = FWD ? Cin : Cout;  // K, A row pitch
+  const int nst = K / 64;
+  // staging pieces of this thread: j < 4: A rows (256 x 8 slots), j >= 4: weight rows (128 x 8)
+  long arow[4];  // FWD: input voxel; dgrad: its tap-0 child voxel
+  int aslot[4], aoff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pc = tid + j * 512, row = pc >> 3, sl = pc & 7;
+    const long m = std::min<long>(m0 + row, M - 1);  // clamped tail rows are computed, never stored
+    arow[j] = FWD ? m : child_base(g, m);
+    aslot[j] = sl;
+    aoff[j] = cd_slot(row, sl);
+  }
+  int brow[2], bslot[2], boff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pc = tid + j * 512, row = pc >> 3, sl = pc & 7;
+    // LDS weight row = MFMA column (nt, cl): GEMM column q0 + 64 (nt / 2) + 2 cl + nt % 2
+    const int nt = row >> 5, cl = row & 31;
+    brow[j] = q0 + 64 * (nt >> 1) + 2 * cl + (nt & 1);
+    bslot[j] = sl;
+    boff[j] = kCDM * 128 + cd_slot(row, sl);
+  }
+  u32x4_t stg[kCDPieces];
+  auto load = [&](int st) {
+    if constexpr (FWD) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        stg[j] = *reinterpret_cast<const u32x4_t*>(a_src + arow[j] * Ka + st * 64 + aslot[j] * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        stg[4 + j] = *reinterpret_cast<const u32x4_t*>(wpk + (long)brow[j] * K + st * 64 + bslot[j] * 8);
+    } else {
+      const int t = st % 8, kc = st / 8;
+      const long dt = tap_delta(g, t);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        stg[j] = *reinterpret_cast<const u32x4_t*>(a_src + (arow[j] + dt) * Ka + kc * 64 + aslot[j] * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        stg[4 + j] = *reinterpret_cast<const u32x4_t*>(wpk + (long)brow[j] * K + t * Cout + kc * 64 + bslot[j] * 8);
+    }
+  };
+  auto store = [&](char* buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4_t*>(buf + aoff[j]) = stg[j];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) *reinterpret_cast<u32x4_t*>(buf + boff[j]) = stg[4 + j];
+  };
+  f32x16_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+  const int arw = wave * 32 + r_lane;
+  load(0);
+  store(lds);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const char* buf = lds + (st & 1) * kCDStage;
+    if (st + 1 < nst) load(st + 1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const s16x8_t a = *reinterpret_cast<const s16x8_t*>(buf + cd_slot(arw, ks * 2 + hsel));
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const s16x8_t b = *reinterpret_cast<const s16x8_t*>(buf + kCDM * 128 + cd_slot(nt * 32 + r_lane, ks * 2 + hsel));
+        acc[nt] = mfma(a, b, acc[nt]);
+      }
+    }
+    if (st + 1 < nst) store(lds + ((st + 1) & 1) * kCDStage);
+    __syncthreads();
+  }
+  if constexpr (FWD) {
+    long dq[2];
+    int cq[2];
+    float b0[2], b1[2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int q = q0 + 64 * pr + 2 * r_lane;  // Cout even: the pair shares one tap
+      dq[pr] = tap_delta(g, q / Cout) * Cout;
+      cq[pr] = q % Cout;
+      b0[pr] = bias[cq[pr]];
+      b1[pr] = bias[cq[pr] + 1];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const long m = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+      if (m >= M) continue;
+      bf16_t* crow = out + child_base(g, m) * Cout;
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+        *reinterpret_cast<uint32_t*>(crow + dq[pr] + cq[pr]) =
+            pack_bf16x2(acc[2 * pr][e] + b0[pr], acc[2 * pr + 1][e] + b1[pr]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const long m = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+      if (m >= M) continue;
+      bf16_t* row = out + m * Cin + q0 + 2 * r_lane;
+      *reinterpret_cast<uint32_t*>(row) = pack_bf16x2(acc[0][e], acc[1][e]);
+      *reinterpret_cast<uint32_t*>(row + 64) = pack_bf16x2(acc[2][e], acc[3][e]);
+    }
   }
 }
 
@@ -307,12 +443,20 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
                    int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
   if (Cin % 16 || Cout % 64) return -1;
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
+  if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
   const size_t es = dtype == PCMS_BF16 ? 2 : 4;
   if (Do != 2 * Din || Ho != 2 * Hin || Wo != 2 * Win) {
     hipError_t e = hipMemsetAsync(out, 0, es * N * (size_t)Do * Ho * Wo * Cout, s);
     if (e != hipSuccess) return (int)e;
   }
   const long M = (long)N * Din * Hin * Win;
+  if (dtype == PCMS_BF16 && Cin % 64 == 0 && (8 * Cout) % kCDN == 0) {
+    (void)hipFuncSetAttribute((const void*)convt_lds_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * kCDStage);
+    hipLaunchKernelGGL(convt_lds_kernel<true>, dim3(cdiv(M, kCDM), 8 * Cout / kCDN), dim3(512), 2 * kCDStage, s,
+                       (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
+    PCMS_CHECK_LAUNCH();
+  }
   dim3 grid(cdiv(M, 128), 8 * Cout / 64);
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL(convt_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
@@ -325,7 +469,15 @@ int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
   if (Cin % 64 || Cout % 16) return -1;
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
+  if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
   const long M = (long)N * Din * Hin * Win;
+  if (dtype == PCMS_BF16 && Cin % kCDN == 0 && Cout % 64 == 0) {
+    (void)hipFuncSetAttribute((const void*)convt_lds_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * kCDStage);
+    hipLaunchKernelGGL(convt_lds_kernel<false>, dim3(cdiv(M, kCDM), Cin / kCDN), dim3(512), 2 * kCDStage, s,
+                       (const bf16_t*)dout, (const bf16_t*)wpack_d, nullptr, (bf16_t*)dx, g, Cin, Cout);
+    PCMS_CHECK_LAUNCH();
+  }
   dim3 grid(cdiv(M, 128), Cin / 64);
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL(convt_dgrad_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, (const bf16_t*)wpack_d, (bf16_t*)dx, g, Cin, Cout);
@@ -357,6 +509,7 @@ int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, floa
                      int target_wgs, hipStream_t s) {
   if (Cin % 64 || Cout % 64) return -1;
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
+  if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
   int vps;
   const int splits = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps);
   dim3 grid(splits, Cout / 64, Cin / 64);

@@ -336,11 +336,12 @@ def test_maxpool_fwd_bwd(dt, code, tol):
 
 
 @pytest.mark.parametrize("dt,code,tol", DTS)
-@pytest.mark.parametrize("Sin,Sout", [((4, 4, 2), (8, 8, 4)), ((2, 2, 3), (5, 4, 7))])
-def test_convt(dt, code, tol, Sin, Sout):
+@pytest.mark.parametrize("Sin,Sout,cin,cout", [((4, 4, 2), (8, 8, 4), 128, 64), ((2, 2, 3), (5, 4, 7), 128, 64),
+                                               ((8, 8, 6), (16, 16, 12), 256, 128)])  # > 1 tile, 2 co chunks
+def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     L = _lib()
     g = torch.Generator().manual_seed(9)
-    N, cin, cout = 2, 128, 64
+    N = 2
     x = torch.randn(N, cin, *Sin, generator=g).to(dt)
     w = (torch.randn(cin, cout, 2, 2, 2, generator=g) / math.sqrt(cin)).to(dt)
     b = torch.randn(cout, generator=g)
