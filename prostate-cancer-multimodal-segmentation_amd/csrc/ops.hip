@@ -220,7 +220,9 @@ __global__ void maxpool_fwd_kernel(const T* a, T* p, int N, int D, int H, int W,
   const int Do = D / 2, Ho = H / 2, Wo = W / 2, CV = C / VEC;
   const long total = (long)N * Do * Ho * Wo * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int cv = i % CV; long r = i / CV;
+    // 32-bit index decomposition (host: total < 2^31): 64-bit division is a long sequence
+    const uint32_t ii = (uint32_t)i;
+    const int cv = ii % CV; uint32_t r = ii / CV;
     const int wo = r % Wo; r /= Wo;
     const int ho = r % Ho; r /= Ho;
     const int d_o = r % Do; const long n = r / Do;
@@ -246,7 +248,8 @@ __global__ void maxpool_bwd_kernel(const T* a, const T* dp, T* da, int N, int D,
   const int Do = D / 2, Ho = H / 2, Wo = W / 2, CV = C / VEC;
   const long total = (long)N * Do * Ho * Wo * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int cv = i % CV; long r = i / CV;
+    const uint32_t ii = (uint32_t)i;  // 32-bit index decomposition (host: total < 2^31)
+    const int cv = ii % CV; uint32_t r = ii / CV;
     const int wo = r % Wo; r /= Wo;
     const int ho = r % Ho; r /= Ho;
     const int d_o = r % Do; const long n = r / Do;
@@ -290,7 +293,8 @@ __global__ void __launch_bounds__(TPB) box_channel_sum_kernel(const T* x, float*
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
   for (long i = (long)blockIdx.x * VL + vl; i < nv; i += (long)gridDim.x * VL) {
-    const int w = i % bw; long r = i / bw;
+    const uint32_t ii = (uint32_t)i;  // 32-bit index decomposition (host: nv < 2^31)
+    const int w = ii % bw; uint32_t r = ii / bw;
     const int h = r % bh; r /= bh;
     const int d = r % bd; const long n = r / bd;
     float v[VEC];
@@ -324,7 +328,7 @@ __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, floa
       load16<T>(a + v * 64 + sub * 8, x);
       load16<T>(a + v * 64 + sub * 8 + 4, x + 4);
     }
-    const long n = v / nvox_per_n, vv = v % nvox_per_n;
+    const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
     for (int k = 0; k < ncls; ++k) {
       float s = 0.f;
 #pragma unroll
@@ -352,7 +356,7 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
     float x[8], o[8];
     load16<T>(a + v * 64 + sub * 8, x);
     if constexpr (sizeof(T) == 4) load16<T>(a + v * 64 + sub * 8 + 4, x + 4);
-    const long n = v / nvox_per_n, vv = v % nvox_per_n;
+    const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = 0.f;
     for (int k = 0; k < ncls && k < 4; ++k) {
@@ -623,6 +627,7 @@ int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scal
 }
 
 int pcms_maxpool_fwd(int dtype, const void* a, void* p, int N, int D, int H, int W, int C, hipStream_t s) {
+  if ((long)N * D * H * W * C >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   const long total = (long)N * (D / 2) * (H / 2) * (W / 2) * (C / VEC);
   const int grid = grid_for(total, TPB);
@@ -633,6 +638,7 @@ int pcms_maxpool_fwd(int dtype, const void* a, void* p, int N, int D, int H, int
 
 int pcms_maxpool_bwd(int dtype, const void* a, const void* dp, void* da, int N, int D, int H, int W, int C,
                      hipStream_t s) {
+  if ((long)N * D * H * W * C >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   const long total = (long)N * (D / 2) * (H / 2) * (W / 2) * (C / VEC);
   const int grid = grid_for(total, TPB);
@@ -643,6 +649,7 @@ int pcms_maxpool_bwd(int dtype, const void* a, const void* dp, void* da, int N, 
 
 int pcms_box_channel_sum(int dtype, const void* x, float* out, int N, int D, int H, int W, int C,
                          int z0, int y0, int x0, int bd, int bh, int bw, hipStream_t s) {
+  if ((long)N * D * H * W >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || TPB % (C / VEC)) return -1;
   const long nv = (long)N * bd * bh * bw;
@@ -655,6 +662,7 @@ int pcms_box_channel_sum(int dtype, const void* x, float* out, int N, int D, int
 
 int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* logits, long nvox_per_n, int N,
                   int ncls, hipStream_t s) {
+  if ((long)N * nvox_per_n >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   const int grid = grid_for((long)N * nvox_per_n * 8, TPB);
   if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, w, b, logits, nvox_per_n, N, ncls);
   else hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, w, b, logits, nvox_per_n, N, ncls);
@@ -663,6 +671,7 @@ int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, floa
 
 int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w, void* da, float* dw, float* db,
                   long nvox_per_n, int N, int ncls, hipStream_t s) {
+  if ((long)N * nvox_per_n >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   if (ncls > 4) return -1;
   const int grid = grid_for((long)N * nvox_per_n * 8, TPB, 2048);
   if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, dw, db, nvox_per_n, N, ncls);
