@@ -439,6 +439,8 @@ struct WgradParams {
   int nco, nci;          // 64-channel output blocks, 32-channel input blocks
   int dma;               // bf16: stage by buffer LDS-DMA (byte sizes below < 2^31)
   uint32_t x0bytes, x1bytes, dybytes;
+  float* dw;             // direct (one split, bf16): dw [Cout][cw][27] += through an LDS transpose
+  int cw, direct;
 };
 
 // dy tile: 128-B (bf16) rows, 64-B halves swizzled by row bit 1 (conflict-free tr reads).
@@ -774,6 +776,33 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // kernel's own time at level 0.)
   float* prow = p.dwt + (long)split * 27 * p.Cout * p.Cin;
   if constexpr (kW2) {
+    if (p.direct) {
+      // one split: no partial rows to reduce.  Per 32-row co half, the workgroup's
+      // [32 co][32 ci][27 taps] tile is transposed through LDS (the staging buffers are free)
+      // and added to the contiguous [ci][27] runs of the torch-layout dw.
+      float* tile = reinterpret_cast<float*>(wlds);
+      const int nci = min(32, p.cw - ci_base);
+      for (int ct = 0; ct < 2; ++ct) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (j >= ntap2) continue;
+          const int tap = wave + 8 * j;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int col = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+            tile[(col * 32 + (lane & 31)) * 27 + tap] = acc[ct * 4 + j][e];
+          }
+        }
+        __syncthreads();
+        for (int i = tid; i < 32 * 32 * 27; i += kWThreads) {
+          const int col = i / 864, r = i % 864;  // r = ci * 27 + tap
+          const int co = co_base + ct * 32 + col;
+          if (co < p.Cout && r < nci * 27) p.dw[((long)co * p.cw + ci_base) * 27 + r] += tile[i];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j >= ntap2) continue;
@@ -2570,6 +2599,9 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   const int splits = q.splits;
   p.nco = Cout / 64;
   p.nci = cdiv(Cin, 32);
+  p.dw = dw;
+  p.cw = cin_w;
+  p.direct = splits == 1 && dtype == PCMS_BF16 && !(PCMS_ABL & 16384);
   dim3 grid(splits * p.nco * p.nci);
   size_t lds;
   if (dtype == PCMS_BF16) {
@@ -2586,6 +2618,7 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
+  if (p.direct) return 0;  // the kernel added into dw itself
   const long E = 27L * Cout * Cin;
   int R = splits, stride = 1;
   if (splits > 16) {
