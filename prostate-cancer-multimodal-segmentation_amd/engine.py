@@ -17,6 +17,7 @@ that forward (checked).  Only device code runs: there is no CPU path.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from typing import Dict, List, Optional, Tuple
 
@@ -110,6 +111,9 @@ class UNetEngine:
         self.act_ckpt = False
         self.wgrad_target = 256  # conv weight-gradient workgroups: one round of 1 WG per CU (fewer partial rows to reduce than 512)
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
+        self.wgrad_side_stream = False  # ablation: weight gradients on a side stream (measured 119.9 vs 121.6 vol/s: off)
+        self._side_stream = None
+        self._side_used = False
         self._flatten()
         for bn in self.bns:
             c = bn.c
@@ -152,9 +156,30 @@ class UNetEngine:
         self.grad_ranges = module_grad_ranges(self.model)
 
     def _grads_done(self, module: str):
-        """Report a finished module gradient range to the data-parallel hook (dp.GradSync)."""
+        """A module's backward is complete: join the weight-gradient stream (its dW kernels and
+        the gradient buffers they read are then safe for the all-reduce and for reuse), and
+        report the module's flat range to the data-parallel hook (dp.GradSync)."""
+        self._join_side()
         if self.grad_ready is not None:
             self.grad_ready(*self.grad_ranges[module])
+
+    # weight gradients run on a side stream beside the data-gradient chain (dgrad -> BN ->
+    # dgrad ...): they only read activations and the dY buffer of their layer, which the main
+    # stream does not overwrite before the next _join_side()
+    def _side(self):
+        if not self.wgrad_side_stream:
+            return contextlib.nullcontext()
+        if self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(device=self.device)
+        main = torch.cuda.current_stream(self.device)
+        self._side_stream.wait_stream(main)
+        self._side_used = True
+        return torch.cuda.stream(self._side_stream)
+
+    def _join_side(self):
+        if self._side_used:
+            torch.cuda.current_stream(self.device).wait_stream(self._side_stream)
+            self._side_used = False
 
     def sync_params(self):
         """Re-flatten if a module op (``.to()``, ``.cuda()``, param reassignment) replaced
@@ -249,6 +274,7 @@ class UNetEngine:
             b[f"gx{l}"] = act(l, C[l])      # grad of encoder output x_l (skip + path)
             b[f"gA{l}"] = act(l, C[l])      # grad of a1 / block outputs (scratch)
             b[f"gY{l}"] = act(l, C[l])      # grad of pre-BN conv outputs (scratch)
+            b[f"gZ{l}"] = act(l, C[l])      # second one (the side stream may still read gY)
             b[f"gU{l}"] = act(l, C[l])      # grad of up output / pooled input (scratch)
         b["gH"] = act(0, C[0])              # grad of the decoder output (head input)
         # workspaces
@@ -373,22 +399,24 @@ class UNetEngine:
         the block input into gx_out0 (channels [0, cy0)) / gx_out1 (rest); None = skip."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
-        gY, gA = b[f"gY{lvl}"], b[f"gA{lvl}"]
-        # BN1/ReLU backward -> dy2
+        gY, gZ, gA = b[f"gY{lvl}"], b[f"gZ{lvl}"], b[f"gA{lvl}"]
+        # BN1/ReLU backward -> dy2; its weight gradient on the side stream
         self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
-        call("pcms_conv3_wgrad", self.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
-             b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target)
+        with self._side():
+            call("pcms_conv3_wgrad", self.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
+                 b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target)
         # dgrad conv1 -> grad of a1
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
-        # BN0/ReLU backward -> dy1 (reuse gY)
-        self._bn_bwd(blk.b0, gA, acts["y1"], gY, nvox)
-        if blk is self.enc[0] and self.stem_fast:
-            call("pcms_stem_wgrad", x0, gY, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S, 256)
-        else:
-            call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gY, blk.c0.mod.weight.grad, b["dwt"], N, *S,
-                 blk.c0.cout, blk.c0.cin, self.wgrad_target)
+        # BN0/ReLU backward -> dy1 (a second buffer: the side stream may still read gY)
+        self._bn_bwd(blk.b0, gA, acts["y1"], gZ, nvox)
+        with self._side():
+            if blk is self.enc[0] and self.stem_fast:
+                call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S, 256)
+            else:
+                call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gZ, blk.c0.mod.weight.grad, b["dwt"], N,
+                     *S, blk.c0.cout, blk.c0.cin, self.wgrad_target)
         if gx_out0 is not None:
-            self._dgrad(blk.c0, gY, gx_out0, gx_out1, cy0, N, S)
+            self._dgrad(blk.c0, gZ, gx_out0, gx_out1, cy0, N, S)
 
     def _bn_bwd(self, bn: BNSpec, ga, y, gy, nvox):
         b = self.bufs
