@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--kernel-reps", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--zero-fill", action="store_true", help="config 4: 1-2 modalities zeroed")
+    ap.add_argument("--ckpt-decoder", action="store_true", help="config 5: decoder activation checkpointing")
     return ap.parse_args()
 
 
@@ -149,7 +150,7 @@ def main():
     spatial = tuple(int(v) for v in a.size.split(","))
     torch.manual_seed(0)
     cfg = {"device": f"cuda:{local}", "learning_rate": 1e-4, "batch_size": a.batch, "num_epochs": 1,
-           "loss": "bce_dice", "precision": a.precision}
+           "loss": "bce_dice", "precision": a.precision, "checkpoint_decoder": a.ckpt_decoder}
     tr = Trainer(cfg)
     batches = []
     for i in range(2):
@@ -190,7 +191,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.precision,
             "data": "synthetic (U[0,1) images, ellipsoid labels; random-init weights, seed 0)",
             "config": {"workload": f"UNet3D 5->1, {a.batch} x 5x{'x'.join(map(str, spatial))} per GPU, "
-                                   f"BCEDiceLoss, Adam(1e-4, wd 1e-5){', zero_fill' if a.zero_fill else ''}",
+                                   f"BCEDiceLoss, Adam(1e-4, wd 1e-5){', zero_fill' if a.zero_fill else ''}"
+                                   f"{', decoder checkpointing' if a.ckpt_decoder else ''}",
                        "global_batch": world * a.batch, "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu,
             "mfma_util_step": round(flops / dt / MFMA_BF16_PEAK, 4), "final_loss": round(loss, 5),

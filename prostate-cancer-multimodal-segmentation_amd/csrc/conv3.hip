@@ -19,6 +19,8 @@
 #include "common.h"
 #include "pcms_hip.h"
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 // PCMS_ABL: ablation switches for the stem kernels, set only by the test-tooling build
@@ -1246,8 +1248,12 @@ constexpr int kSDHaloBytes = kSDHaloRows * 16;
 constexpr int kSDLds = 2 * kSDHaloBytes + 8 * 64 * 3 * 4;     // halo x2 + stats reduction
 constexpr int kSDThr = (PCMS_ABL & 8192) ? 256 : 512;  // product variant (256: same time, 101 vs 102 us)
 
-template <int LBD, int LBH, int THR>
-__global__ void __launch_bounds__(THR, 512 / THR) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
+// PIPE: software-pipelined stores.  Tile mt = 0 of a box is computed first and its 16
+// stores are issued between the MFMAs of tile mt = 1; tile 1's stores go out between the
+// MFMAs of the NEXT box's tile 0 (the last one after the loop).  Stores and BN sums thus run
+// inside the MFMA gaps of the same wave instead of after all its MFMAs.
+template <int LBD, int LBH, int THR, bool PIPE = false>
+__global__ void __launch_bounds__(THR, (PIPE && THR == 256) ? 1 : 512 / THR) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
                                                                          uint32_t xbytes, uint32_t ybytes) {
   constexpr int kSDThreads = THR, NWV = THR / 64;
   static_assert((1 << (LBD + LBH + 4)) == NWV * 64, "box = 64 voxels per wave");
@@ -1335,6 +1341,103 @@ __global__ void __launch_bounds__(THR, 512 / THR) stem_fwd_direct_kernel(Conv3Pa
   int b = blockIdx.x;
   if (b < nbox) stage(b, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (PIPE) {
+    // one pending tile: values, store soffset, validity inputs
+    struct Tile {
+      f32x16_t v[2];
+      uint32_t so;
+      int rd, rh, d0, h0, w0;
+      bool full;
+    };
+    auto tile_meta = [&](Tile& t, int bb, int mt) {
+      int n, d0, h0, w0;
+      origin(bb, n, d0, h0, w0);
+      const int R0 = wave * 4 + mt * 2;
+      t.rd = R0 >> LBH; t.rh = R0 & (bh - 1);
+      t.d0 = d0; t.h0 = h0; t.w0 = w0;
+      t.full = d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
+      const int bv = ((n * D + d0) * H + h0) * W + w0;
+      t.so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (t.rd * H + t.rh) * W) * 128u);
+    };
+    // element e of tile t: one buffer store + BN shifted sums
+    auto store_e = [&](const Tile& t, int e) {
+      const int g = e >> 2, rw = 4 * g + (e & 3);
+      const bool gB = (g == 1 || g == 2);
+      const float v0 = t.v[0][e], v1 = t.v[1][e];
+      uint32_t voff = gB ? vB : vA;
+      float e0 = v0 - K[0], e1 = v1 - K[1];
+      if (!t.full) {
+        const int xh = (gB ? 1 : 0) ^ hsel;
+        const bool valid = (t.d0 + t.rd < D) & (t.h0 + t.rh + xh < H) & (t.w0 + rw < W);
+        voff = valid ? voff : kOOB;
+        e0 = valid ? e0 : 0.f;
+        e1 = valid ? e1 : 0.f;
+        cnt += valid ? 1.f : 0.f;
+      }
+      __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, t.so + rw * 128, 0);
+      s1[0] += e0; s2[0] += e0 * e0;
+      s1[1] += e1; s2[1] += e1 * e1;
+    };
+    auto count_full = [&](const Tile& t) { if (t.full) cnt += 16.f; };
+    Tile pend, cur;
+    bool have_pend = false;
+    int hs16 = hsel * 16;
+    asm volatile("" : "+v"(hs16));
+    for (int it = 0; b < nbox; b += gridDim.x, ++it) {
+      __syncthreads();
+      const int bn = b + gridDim.x;
+      if (bn < nbox) stage(bn, (it + 1) & 1);
+      const char* hl = lds + (it & 1) * kSDHaloBytes;
+      // one 32-row tile: 14 k-steps x 2 MFMAs; `st_` = the tile whose stores fill the gaps
+      auto run_tile = [&](auto with_st, int mt, Tile& out, const Tile& st_) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) out.v[j][e] = bias_l[j];
+        auto load_a = [&](int st) {
+          const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
+          return *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + o0 * 16 + hs16 * (o1 - o0));
+        };
+        s16x8_t abuf[2];
+        abuf[0] = load_a(0);
+#pragma unroll
+        for (int st = 0; st < kStemSteps; ++st) {
+          if (st + 1 < kStemSteps) abuf[(st + 1) & 1] = load_a(st + 1);
+          out.v[0] = mfma(abuf[st & 1], wb[st][0], out.v[0]);
+          out.v[1] = mfma(abuf[st & 1], wb[st][1], out.v[1]);
+          if constexpr (decltype(with_st)::value) {  // 16 stores over 14 steps: two extra on the first two
+            store_e(st_, st);
+            if (st < 2) store_e(st_, 14 + st);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      if (have_pend) {
+        run_tile(std::true_type{}, 0, cur, pend);
+        count_full(pend);
+      } else {
+        run_tile(std::false_type{}, 0, cur, pend);
+      }
+      tile_meta(cur, b, 0);
+      if (first) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(cur.v[nt][0], r_lane, 64);
+        first = false;
+      }
+      run_tile(std::true_type{}, 1, pend, cur);
+      count_full(cur);
+      tile_meta(pend, b, 1);
+      have_pend = true;
+      // the next halo's DMA was issued before this box's stores (16 on the first box, 32 after)
+      if (it == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    }
+    if (have_pend) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) store_e(pend, e);
+      count_full(pend);
+    }
+  } else
   for (int it = 0; b < nbox; b += gridDim.x, ++it) {
     // halo(b) has landed for this wave (vmcnt above / at the loop end); barrier: for all
     // waves, and every wave is done reading the buffer the next DMA overwrites
@@ -2468,16 +2571,28 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
   const bool direct = b.lbw == 4 && b.lbd + b.lbh == 5 && (b.lbd == 2 || b.lbd == 3) && ybytes < (long)kOOB;
   if (direct) {
     const int grid = std::min(nbox, ncu);
-    auto kern = b.lbd == 2 ? stem_fwd_direct_kernel<2, 3, 512> : stem_fwd_direct_kernel<3, 2, 512>;
+    // store-pipelined variant unless PCMS_STEM_FWD_PIPE=0 (A/B switch for the measurements)
+    // 0: plain stores after the MFMAs; 1: store-pipelined, 8 waves; 2: store-pipelined,
+    // one 4-wave workgroup per CU (512 registers per wave)
+    static const int pipe = [] { const char* e = getenv("PCMS_STEM_FWD_PIPE"); return e ? atoi(e) : 0; }();
+    auto kern = b.lbd == 2 ? (pipe == 1 ? stem_fwd_direct_kernel<2, 3, 512, true> : stem_fwd_direct_kernel<2, 3, 512>)
+                           : (pipe == 1 ? stem_fwd_direct_kernel<3, 2, 512, true> : stem_fwd_direct_kernel<3, 2, 512>);
     int g2 = grid;
-    if (kSDThr == 256) {  // 4x4x16 boxes, two workgroups per CU; rows stay <= the caller's
+    int thr = kSDThr;
+    if (pipe == 2) {  // 4x4x16 boxes, one 4-wave workgroup per CU
+      p.lbd = 2; p.lbh = 2;
+      p.nbd = cdiv(D, 4); p.nbh = cdiv(H, 4);
+      g2 = std::min(std::min(p.N * p.nbd * p.nbh * p.nbw, ncu), nbox);
+      kern = stem_fwd_direct_kernel<2, 2, 256, true>;
+      thr = 256;
+    } else if (kSDThr == 256) {  // 4x4x16 boxes, two workgroups per CU; rows stay <= the caller's
       p.lbd = 2; p.lbh = 2;
       p.nbd = cdiv(D, 4); p.nbh = cdiv(H, 4);
       g2 = std::min(std::min(p.N * p.nbd * p.nbh * p.nbw, 2 * ncu), nbox);
       kern = stem_fwd_direct_kernel<2, 2, 256>;
     }
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSDLds);
-    hipLaunchKernelGGL(kern, dim3(g2), dim3(kSDThr), kSDLds, s, p, kSDThr == 256 ? p.N * p.nbd * p.nbh * p.nbw : nbox,
+    hipLaunchKernelGGL(kern, dim3(g2), dim3(thr), kSDLds, s, p, thr == 256 ? p.N * p.nbd * p.nbh * p.nbw : nbox,
                        nbox, (uint32_t)xbytes,
                        (uint32_t)ybytes);
     PCMS_CHECK_LAUNCH();

@@ -108,7 +108,14 @@ class UNetEngine:
         self.buf_key = None
         self.epoch = 0
         self.saved_epoch = -1
+        # decoder activation checkpointing: the decoder blocks'
+        # pre-BN conv outputs and first ReLU output (y1, a1, y2) are not kept per level; the
+        # forward writes them into one shared level-0-sized set and the backward recomputes
+        # them level by level with the forward's BatchNorm coefficients (no statistics pass,
+        # running stats untouched).  Decoder convs then run unsplit (no split-K atomics), so the
+        # recomputed tensors are bit-identical to the forward's.
         self.act_ckpt = False
+        self.unsplit = False  # every conv unsplit (no split-K fp32 atomics): a deterministic step
         self.wgrad_target = 256  # conv weight-gradient workgroups: one round of 1 WG per CU (fewer partial rows to reduce than 512)
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
         self.wgrad_side_stream = False  # ablation: weight gradients on a side stream (measured 119.9 vs 121.6 vol/s: off)
@@ -244,7 +251,7 @@ class UNetEngine:
         return s
 
     def _alloc(self, N, D, H, W):
-        key = (N, D, H, W)
+        key = (N, D, H, W, self.act_ckpt, self.wgrad_side_stream)
         if self.buf_key == key:
             return
         self.bufs = None
@@ -267,14 +274,18 @@ class UNetEngine:
             for k in ("y1", "a1", "y2", "x"):
                 b[f"e{l}_{k}"] = act(l, C[l])
         for l in range(4):
-            for k in ("u", "y1", "a1", "y2", "a2"):
+            for k in (("u", "a2") if self.act_ckpt else ("u", "y1", "a1", "y2", "a2")):
                 b[f"d{l}_{k}"] = act(l, C[l])
+        if self.act_ckpt:  # shared decoder set (level 0 is the largest: bytes per level ~ 4^-l)
+            for k in ("y1", "a1", "y2"):
+                b[f"ck_{k}"] = act(0, C[0])
         # gradient buffers
         for l in range(5):
             b[f"gx{l}"] = act(l, C[l])      # grad of encoder output x_l (skip + path)
             b[f"gA{l}"] = act(l, C[l])      # grad of a1 / block outputs (scratch)
             b[f"gY{l}"] = act(l, C[l])      # grad of pre-BN conv outputs (scratch)
-            b[f"gZ{l}"] = act(l, C[l])      # second one (the side stream may still read gY)
+            # second one while the side stream may still read gY; else an alias
+            b[f"gZ{l}"] = act(l, C[l]) if self.wgrad_side_stream else b[f"gY{l}"]
             b[f"gU{l}"] = act(l, C[l])      # grad of up output / pooled input (scratch)
         b["gH"] = act(0, C[0])              # grad of the decoder output (head input)
         # workspaces
@@ -312,12 +323,17 @@ class UNetEngine:
             return 1
         return max(1, min(nch, -(-384 // wgs)))
 
-    def _conv(self, cs: ConvSpec, x0, c0, x1, c1, y, N, S, stats: bool, training: bool, bn: BNSpec):
-        """y = conv(x) + b; then BN statistics (train) or eval coefficients."""
+    def _conv(self, cs: ConvSpec, x0, c0, x1, c1, y, N, S, stats: bool, training: bool, bn: BNSpec,
+              recompute: bool = False):
+        """y = conv(x) + b; then BN statistics (train) or eval coefficients.  ``recompute``:
+        the conv alone (checkpointed decoder: the forward's BN coefficients are reused)."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
-        splits = self._splits(N, S, c0 + c1, cs.cout)
-        st = b["stats"] if training else None
+        if self.unsplit or self.buf_key[4] and any(cs is blk.c0 or cs is blk.c1 for blk in self.dec):
+            splits = 1  # deterministic: the recompute reproduces the forward bit for bit
+        else:
+            splits = self._splits(N, S, c0 + c1, cs.cout)
+        st = b["stats"] if training and not recompute else None
         if cs is self.convs[0] and self.stem_fast:
             call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2])
             rows = query("pcms_stem_fwd_rows", N, *S)
@@ -332,6 +348,8 @@ class UNetEngine:
                  acc, None, 0, N, S[0], S[1], S[2], cs.cout, splits)
             call("pcms_split_epilogue", self.code, acc, cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox)
             rows = query("pcms_split_epilogue_rows", nvox)
+        if recompute:
+            return
         m = bn.mod
         if training:
             if nvox <= 1:
@@ -344,12 +362,24 @@ class UNetEngine:
             call("pcms_bn_eval_coeffs", m.weight, m.bias, m.running_mean, m.running_var, BN_EPS, bn.c,
                  bn.scale, bn.shift)
 
-    def _block_fwd(self, blk: BlockSpec, x0, c0, x1, c1, out: Dict[str, torch.Tensor], N, S, training):
+    def _block_fwd(self, blk: BlockSpec, x0, c0, x1, c1, out: Dict[str, torch.Tensor], N, S, training,
+                   recompute: bool = False):
+        """conv -> BN -> ReLU -> conv -> BN -> ReLU.  ``recompute`` (checkpointed decoder
+        backward): y1, a1, y2 again from the same inputs with the forward's BN scale/shift; no
+        statistics, no running-stat update, a2 not rewritten."""
         nvox = N * S[0] * S[1] * S[2]
-        self._conv(blk.c0, x0, c0, x1, c1, out["y1"], N, S, True, training, blk.b0)
+        self._conv(blk.c0, x0, c0, x1, c1, out["y1"], N, S, True, training, blk.b0, recompute)
         call("pcms_bn_relu", self.code, out["y1"], out["a1"], blk.b0.scale, blk.b0.shift, blk.c0.cout, nvox)
-        self._conv(blk.c1, out["a1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1)
-        call("pcms_bn_relu", self.code, out["y2"], out["a2"], blk.b1.scale, blk.b1.shift, blk.c1.cout, nvox)
+        self._conv(blk.c1, out["a1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1, recompute)
+        if not recompute:
+            call("pcms_bn_relu", self.code, out["y2"], out["a2"], blk.b1.scale, blk.b1.shift, blk.c1.cout, nvox)
+
+    def _dec_acts(self, l: int) -> Dict[str, torch.Tensor]:
+        b = self.bufs
+        if not self.buf_key[4]:  # the mode the buffers were laid out for
+            return {k: b[f"d{l}_{k}"] for k in ("y1", "a1", "y2", "a2")}
+        n = b["nv"][l] * b["C"][l]
+        return {"y1": b["ck_y1"][:n], "a1": b["ck_a1"][:n], "y2": b["ck_y2"][:n], "a2": b[f"d{l}_a2"]}
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
@@ -382,8 +412,8 @@ class UNetEngine:
             fpack, _ = self.convt_packs[i]
             call("pcms_convt_fwd", self.code, h, fpack, up.bias, b[f"d{l}_u"], N, *S[l + 1], up.in_channels,
                  up.out_channels, *S[l])
-            out = {"y1": b[f"d{l}_y1"], "a1": b[f"d{l}_a1"], "y2": b[f"d{l}_y2"], "a2": b[f"d{l}_a2"]}
-            self._block_fwd(self.dec[i], b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], out, N, S[l], training)
+            self._block_fwd(self.dec[i], b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], self._dec_acts(l), N, S[l],
+                            training)
             h = b[f"d{l}_a2"]
         logits = torch.empty((N, self.ncls, D, H, W), dtype=torch.float32, device=self.device)
         oc = self.model.outc
@@ -457,7 +487,9 @@ class UNetEngine:
         for i in reversed(range(4)):
             l = 3 - i
             blk = self.dec[i]
-            acts = {"y1": b[f"d{l}_y1"], "a1": b[f"d{l}_a1"], "y2": b[f"d{l}_y2"]}
+            acts = self._dec_acts(l)
+            if self.buf_key[4]:
+                self._block_fwd(blk, b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], acts, N, S[l], True, recompute=True)
             gu = b[f"gU{l}"]
             self._block_bwd(blk, g, acts, b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], b[f"gx{l}"], gu, C[l], N,
                             S[l], l)

@@ -88,7 +88,7 @@ class UNet3D(nn.Module):
     """3D U-Net, 4 down / 4 up levels, widths 64 -> 1024 (models/unet3d.py:160-344)."""
 
     def __init__(self, n_modalities: int = 5, n_classes: int = 2, *, in_channels: Optional[int] = None,
-                 out_channels: Optional[int] = None, precision: str = "bf16"):
+                 out_channels: Optional[int] = None, precision: str = "bf16", checkpoint_decoder: bool = False):
         super().__init__()
         if in_channels is not None:
             n_modalities = in_channels
@@ -100,6 +100,8 @@ class UNet3D(nn.Module):
         self.n_classes = n_classes
         self.init_features = 64
         self.precision = precision
+        # decoder activation checkpointing (config 5; no reference equivalent)
+        self.checkpoint_decoder = bool(checkpoint_decoder)
         f = self.init_features
         # construction order == reference order (same RNG consumption)
         self.inc = DoubleConv3D(n_modalities, f)
@@ -134,6 +136,7 @@ class UNet3D(nn.Module):
             self.__dict__["_engine"] = eng
         else:
             eng.sync_params()
+        eng.act_ckpt = self.checkpoint_decoder
         return eng
 
     def __getstate__(self):

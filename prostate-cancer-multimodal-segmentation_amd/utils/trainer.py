@@ -65,7 +65,8 @@ class BaseTrainer:
     # ---- construction (utils/trainer.py:76-158) ----
     def _create_model(self):
         return UNet3D(n_modalities=self.config.get("n_modalities", 5), n_classes=1,
-                      precision=self.config.get("precision", "bf16")).to(self.device)
+                      precision=self.config.get("precision", "bf16"),
+                      checkpoint_decoder=self.config.get("checkpoint_decoder", False)).to(self.device)
 
     def _create_criterion(self):
         return BCEDiceLoss() if self.config.get("loss", "dice") == "bce_dice" else DiceLoss()

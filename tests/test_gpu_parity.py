@@ -22,12 +22,12 @@ PRE_BN_BIAS = ("conv.0.bias", "conv.3.bias")  # exact grad 0, referen
 GRAD_RL2 = {"c16_bcedice": 5e-2, "cfg1_dice": 5e-3, "odd_bcedice": 5e-2, "c16_ncls2_dice": 5e-2}
 
 
-def _build(name, precision):
+def _build(name, precision, ckpt=False):
     import pcms_amd
     from pcms_amd.models.unet3d import UNet3D
     ncls = gu.CASES[name][0]
     torch.manual_seed(0)
-    m = UNet3D(n_modalities=5, n_classes=ncls, precision=precision)
+    m = UNet3D(n_modalities=5, n_classes=ncls, precision=precision, checkpoint_decoder=ckpt)
     return m.cuda()
 
 
@@ -41,10 +41,12 @@ def _opt(m, name):
     return FlatAdam(m, lr=gu.CASES[name][5], weight_decay=1e-5)
 
 
-@pytest.mark.parametrize("name", list(gu.CASES))
-def test_fp32_parity_full_step(name):
+# (case, decoder activation checkpointing): the checkpointed step must meet
+# the same bars against the reference as the plain one
+@pytest.mark.parametrize("name,ckpt", [(n, False) for n in gu.CASES] + [("cfg1_dice", True), ("odd_bcedice", True)])
+def test_fp32_parity_full_step(name, ckpt):
     g = gu.load(name)
-    m = _build(name, "fp32")
+    m = _build(name, "fp32", ckpt)
     assert gu.sd_hash({k: v.cpu() for k, v in m.state_dict().items()}) == str(g["sd_sha256"])
     crit, opt = _crit(name), _opt(m, name)
     x, y = gu.batch(name, 0)
@@ -117,10 +119,11 @@ def test_fp32_parity_full_step(name):
     assert abs(float(l1.detach()) - float(g["loss1_64"])) <= max(4 * e_ref, 1e-3), (float(l1.detach()), float(g["loss1"]))
 
 
-@pytest.mark.parametrize("name", ["c16_bcedice", "cfg1_dice", "odd_bcedice"])
-def test_bf16_parity_step(name):
+@pytest.mark.parametrize("name,ckpt", [("c16_bcedice", False), ("cfg1_dice", False), ("odd_bcedice", False),
+                                       ("cfg1_dice", True)])
+def test_bf16_parity_step(name, ckpt):
     g = gu.load(name)
-    m = _build(name, "bf16")
+    m = _build(name, "bf16", ckpt)
     crit, opt = _crit(name), _opt(m, name)
     x, y = gu.batch(name, 0)
     m.train()
@@ -168,3 +171,51 @@ def test_shape_mismatch_and_cpu_refusal():
     mm = UNet3D(n_modalities=5, n_classes=1).cuda()
     with pytest.raises(ValueError):
         mm(torch.zeros(1, 5, 16, 16, 16, device="cuda"))  # 1 value per channel at the bottleneck
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_decoder_checkpointing_matches_plain_step(precision):
+    """Decoder activation checkpointing against the plain step, both with
+    unsplit convs (``engine.unsplit``; split-K adds fp32 partials in arrival order): the
+    first forward is bit-identical (same loss), the gradients agree to backward-summation
+    noise, the BatchNorm running stats are updated exactly once per step (the recompute
+    leaves them alone), and checkpointing keeps fewer buffers."""
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    from pcms_amd.models.unet3d import UNet3D
+    runs = []
+    for ckpt in (False, True):
+        torch.manual_seed(0)
+        m = UNet3D(n_modalities=5, n_classes=1, precision=precision, checkpoint_decoder=ckpt).cuda()
+        m.engine().unsplit = True
+        opt = FlatAdam(m, lr=1e-4, weight_decay=1e-5)
+        crit = BCEDiceLoss()
+        losses, grads = [], None
+        for step in range(2):
+            gen = torch.Generator().manual_seed(77 + step)
+            x = torch.rand(2, 5, 32, 32, 32, generator=gen).cuda()
+            y = (torch.rand(2, 1, 32, 32, 32, generator=gen) < 0.3).float().cuda()
+            m.train()
+            opt.zero_grad()
+            loss = crit(m(x), y)
+            loss.backward()
+            if step == 0:
+                grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+            opt.step()
+            losses.append(float(loss))
+        eng = m.engine()
+        nbuf = sum(1 for k in eng.bufs if k.startswith("d") or k.startswith("ck_"))
+        runs.append((losses, grads, {k: v.detach().clone() for k, v in m.state_dict().items()}, nbuf))
+    (l0, g0, s0, n0), (l1, g1, s1, n1) = runs
+    bf = precision == "bf16"
+    assert l0[0] == l1[0], (l0, l1)
+    assert abs(l0[1] - l1[1]) <= (1e-3 if bf else 1e-5), (l0, l1)
+    for k in g0:
+        rl2 = float((g1[k] - g0[k]).float().norm() / g0[k].float().norm().clamp_min(1e-30))
+        assert rl2 <= (2e-2 if bf else 1e-5) or k.endswith(PRE_BN_BIAS), (k, rl2)
+    for k in s0:
+        if k.endswith("num_batches_tracked"):
+            assert int(s0[k]) == int(s1[k]) == 2, k
+        elif "running" in k:
+            assert torch.allclose(s0[k], s1[k], rtol=1e-2 if bf else 1e-5, atol=1e-3 if bf else 1e-6), k
+    assert n1 < n0
