@@ -39,6 +39,8 @@ int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1);
 int pcms_conv3_big_min_boxes(int v);               /* set (v > 0) / query; returns old */
 /* master W [Cout][Cin][3][3][3] fp32 -> kernel pack; flip=1 builds the dgrad pack      */
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s);
+// Both packs of one conv (forward and dgrad, as pcms_conv3_pack flip 0 / 1) from one read of w.
+int pcms_conv3_pack2(int dtype, const float* w, void* fwd, void* dgrad, int Cout, int Cin, hipStream_t s);
 /* Y = conv(X) + bias, X = channel-concat(x0[:, :c0], x1[:, :c1]) (Up3D cat, :156),
  * output channels [0, cy0) -> y0, [cy0, Cout) -> y1 (dgrad concat split).
  * stats: BN partials or NULL: [mblocks][Cout][2] fp32 (sum, M2 = sum of squared

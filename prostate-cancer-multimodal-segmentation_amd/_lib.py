@@ -22,6 +22,7 @@ SIGNATURES = {
     "pcms_conv3_fwd_rows": "iiiiiii",
     "pcms_conv3_big_min_boxes": "i",
     "pcms_conv3_pack": "ippiiis",
+    "pcms_conv3_pack2": "ipppiis",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiis",

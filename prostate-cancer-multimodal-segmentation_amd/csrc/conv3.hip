@@ -1008,6 +1008,51 @@ __device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
   return (kd * HH + kh) * HW + kw;
 }
 
+// Both bf16 packs of one conv from ONE read of the fp32 weight (Cin % 32 == Cout % 32 == 0).
+// Block (co j0 .. j0+32, ci c*32 .. +32): the 32 contiguous 864-float runs w[co][c*32..][27]
+// are converted to bf16 once into LDS (same rounding as pack_bf16x2), then both packs are
+// written as whole 64-B rows:
+//   fwd   [ci/32][t][co][ci%32] = w[co][ci][t]
+//   dgrad [co/32][t][ci][co%32] = w[co][ci][26 - t]
+__global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* w, bf16_t* fwd, bf16_t* dgr,
+                                                                   int Cout, int Cin) {
+  __shared__ __attribute__((aligned(16))) uint16_t tb[32 * 864];
+  const int chunk = blockIdx.y;
+  const int j0 = blockIdx.x * 32;
+  // all 27 loads of a thread in flight at once (the tile is 32 x 216 = 27 x 256 f32x4)
+  f32x4_t v[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+    const int e = threadIdx.x + i * 256, run = e / 216, q = e % 216;
+    v[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(w + ((long)(j0 + run) * Cin + chunk * 32) * 27) + q);
+  }
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+    const int e = threadIdx.x + i * 256, run = e / 216, q = e % 216;
+    uint2 o;
+    o.x = pack_bf16x2(v[i][0], v[i][1]);
+    o.y = pack_bf16x2(v[i][2], v[i][3]);
+    *reinterpret_cast<uint2*>(tb + run * 864 + 4 * q) = o;
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < 27 * 128; g += 256) {
+    const int t = g >> 7, co = (g >> 2) & 31, k8 = (g & 3) * 8;
+    u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (uint32_t)tb[co * 864 + (k8 + 2 * i) * 27 + t] | ((uint32_t)tb[co * 864 + (k8 + 2 * i + 1) * 27 + t] << 16);
+    *reinterpret_cast<u32x4_t*>(fwd + (((long)chunk * 27 + t) * Cout + j0 + co) * 32 + k8) = o;
+  }
+  for (int g = threadIdx.x; g < 27 * 128; g += 256) {
+    const int t = g >> 7, ci = (g >> 2) & 31, k8 = (g & 3) * 8, ts = 26 - t;
+    u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (uint32_t)tb[(k8 + 2 * i) * 864 + ci * 27 + ts] | ((uint32_t)tb[(k8 + 2 * i + 1) * 864 + ci * 27 + ts] << 16);
+    *reinterpret_cast<u32x4_t*>(dgr + (((long)(j0 >> 5) * 27 + t) * Cin + chunk * 32 + ci) * 32 + k8) = o;
+  }
+}
+
 // Persistent stem forward: one 8-wave workgroup per CU walks boxes b = blockIdx.x,
 // b += gridDim.x.  LDS: weights (loaded once) | halo x2 (LDS-DMA, next box prefetched while
 // the current one computes) | bf16 C tile (16-B coalesced stores).  Every thread issues
@@ -2449,6 +2494,17 @@ int pcms_conv3_big_min_boxes(int v) {
 }
 
 int pcms_conv3_chunk(int dtype) { return dtype == PCMS_BF16 ? Traits<bf16_t>::CK : Traits<float>::CK; }
+
+// forward and dgrad packs together (one weight read); other shapes / dtypes: the two packs
+int pcms_conv3_pack2(int dtype, const float* w, void* fwd, void* dgrad, int Cout, int Cin, hipStream_t s) {
+  if (dtype == PCMS_BF16 && Cin % 32 == 0 && Cout % 32 == 0) {
+    hipLaunchKernelGGL(pack_conv3_bf16_both_kernel, dim3(Cout / 32, Cin / 32), dim3(256), 0, s, w, (bf16_t*)fwd,
+                       (bf16_t*)dgrad, Cout, Cin);
+    PCMS_CHECK_LAUNCH();
+  }
+  const int rc = pcms_conv3_pack(dtype, w, fwd, Cout, Cin, 0, s);
+  return rc ? rc : pcms_conv3_pack(dtype, w, dgrad, Cout, Cin, 1, s);
+}
 
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s) {
   const int CK = pcms_conv3_chunk(dtype);

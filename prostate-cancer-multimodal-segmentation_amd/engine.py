@@ -224,9 +224,10 @@ class UNetEngine:
                 if i != 0:  # the stem's input needs no gradient -> no dgrad pack
                     nchd = -(-cs.cout // ck)
                     cs.dgrad = torch.empty(nchd * 27 * cs.cin * ck, dtype=self.tdtype, device=self.device)
-            call("pcms_conv3_pack", self.code, w, cs.fwd, cs.cout, cs.cin, 0)
             if cs.dgrad is not None:
-                call("pcms_conv3_pack", self.code, w, cs.dgrad, cs.cout, cs.cin, 1)
+                call("pcms_conv3_pack2", self.code, w, cs.fwd, cs.dgrad, cs.cout, cs.cin)
+            else:
+                call("pcms_conv3_pack", self.code, w, cs.fwd, cs.cout, cs.cin, 0)
         if self.stem_fast:
             if self.stem_pack is None:
                 self.stem_pack = torch.empty(query("pcms_stem_pack_elems"), dtype=self.tdtype, device=self.device)

@@ -500,3 +500,22 @@ def test_stem_fwd_wgrad_bf16(N, S):
     close(var, yr.var(1, unbiased=False), 1e-3, "stem stats var")
     assert dw[-guard:].abs().max().item() == 0.0
     close(dw[:-guard].cpu().view(64, 5, 3, 3, 3), wr.grad, 1e-4, "stem wgrad")
+
+
+@pytest.mark.parametrize("cout,cin", [(64, 64), (128, 256), (64, 128), (512, 1024)])
+def test_conv3_pack2_equals_two_packs(cout, cin):
+    """pcms_conv3_pack2 (forward + dgrad bf16 packs from one weight read) is bit-identical to
+    pcms_conv3_pack with flip 0 and flip 1."""
+    L = _lib()
+    code = 1  # bf16
+    ck = L.query("pcms_conv3_chunk", code)
+    w = torch.randn(cout, cin, 3, 3, 3, device=DEV)
+    f1 = torch.empty(-(-cin // ck) * 27 * cout * ck, dtype=torch.bfloat16, device=DEV)
+    d1 = torch.empty(-(-cout // ck) * 27 * cin * ck, dtype=torch.bfloat16, device=DEV)
+    f2, d2 = torch.full_like(f1, 7), torch.full_like(d1, 7)
+    L.call("pcms_conv3_pack", code, w, f1, cout, cin, 0)
+    L.call("pcms_conv3_pack", code, w, d1, cout, cin, 1)
+    L.call("pcms_conv3_pack2", code, w, f2, d2, cout, cin)
+    torch.cuda.synchronize()
+    assert torch.equal(f1.view(torch.int16), f2.view(torch.int16))
+    assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))

@@ -217,5 +217,5 @@ def test_decoder_checkpointing_matches_plain_step(precision):
         if k.endswith("num_batches_tracked"):
             assert int(s0[k]) == int(s1[k]) == 2, k
         elif "running" in k:
-            assert torch.allclose(s0[k], s1[k], rtol=1e-2 if bf else 1e-5, atol=1e-3 if bf else 1e-6), k
+            assert torch.allclose(s0[k], s1[k], rtol=1e-2 if bf else 1e-5, atol=5e-3 if bf else 1e-6), k
     assert n1 < n0
