@@ -166,3 +166,18 @@ class UNet3D(nn.Module):
         with torch.no_grad():
             probs = torch.sigmoid(self(x))
             return (probs > threshold).float()
+
+
+def load_weights(model: UNet3D, checkpoint) -> UNet3D:
+    """Load either checkpoint form the reference writes (script/validate_model.py:174-180,
+    script/predict.py:139-145): a full ``save_checkpoint`` dict (``model_state_dict`` key) or
+    a bare state dict (``best_model_epoch_*.pth``).  ``checkpoint``: a path or a loaded dict.
+    Files are read with ``weights_only=True`` (nothing in them is executed)."""
+    if isinstance(checkpoint, (str, bytes)) or hasattr(checkpoint, "__fspath__"):
+        dev = next(model.parameters()).device
+        checkpoint = torch.load(checkpoint, map_location=dev, weights_only=True)
+    sd = checkpoint["model_state_dict"] if "model_state_dict" in checkpoint else checkpoint
+    model.load_state_dict(sd)
+    if model._engine is not None:
+        model._engine.mark_dirty()
+    return model

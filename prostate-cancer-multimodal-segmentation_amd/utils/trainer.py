@@ -20,8 +20,9 @@ BatchNorm statistics and the global Dice stay per replica (plain BatchNorm3d, SU
 
 Config keys follow utils/trainer.py:40-49 (``device``, ``learning_rate``, ``batch_size``,
 ``num_epochs``, ``save_dir``, ``validation`` ...) plus ``loss`` ('dice' | 'bce_dice'),
-``precision`` ('bf16' | 'fp32').  The NIfTI data pipeline (script/data_loader.py) is not
-part of this engine: pass ``train_loader`` / ``val_loader`` iterables of batch dicts.
+``precision`` ('bf16' | 'fp32'), ``checkpoint_decoder``.  With ``data_dir`` the loaders come
+from ``pcms_amd.data.get_dataloader`` (script/data_loader.py); otherwise pass
+``train_loader`` / ``val_loader`` iterables of batch dicts.
 """
 from __future__ import annotations
 
@@ -78,10 +79,17 @@ class BaseTrainer:
         return torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, mode="min", patience=10, factor=0.5)
 
     def _create_dataloader(self, mode):
+        """utils/trainer.py:139-158 with the arguments get_dataloader actually takes (the
+        reference passes ``mode=`` / ``handle_missing_modalities=``, which it rejects)."""
         if self.config.get("data_dir") is None:
             return None
-        raise NotImplementedError("the NIfTI loader (script/data_loader.py) is outside this engine; "
-                                  "pass train_loader= / val_loader= iterables of {'image','label'} batches")
+        from ..data import get_dataloader
+        return get_dataloader(self.config["data_dir"], batch_size=self.config["batch_size"], shuffle=mode == "train",
+                              modalities=self.config.get("modalities"),
+                              missing_strategy=self.config.get("handle_missing_modalities",
+                                                               self.config.get("missing_strategy", "zero_fill")),
+                              target_size=tuple(self.config.get("target_size", (128, 128, 128))),
+                              is_training=mode == "train", data_type=self.config.get("data_type", "BPH"))
 
     def _broadcast_params(self):
         eng = self.model.engine()
@@ -178,10 +186,23 @@ class BaseTrainer:
             torch.save(self.model.state_dict(),
                        os.path.join(self.config["save_dir"], f"best_model_epoch_{epoch}.pth"))
 
-    def train(self):
+    def load_checkpoint(self, path: str):
+        """Resume from a ``save_checkpoint`` file (ours or the reference's: same keys, Adam
+        state in torch.optim.Adam's format): model, optimizer and ReduceLROnPlateau state.
+        Returns ``(epoch, loss)``; ``train(start_epoch=epoch)`` continues from there."""
+        ckpt = torch.load(path, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(ckpt["model_state_dict"])
+        self.model.engine().mark_dirty()
+        if "optimizer_state_dict" in ckpt:
+            self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+        if "scheduler_state_dict" in ckpt:
+            self.scheduler.load_state_dict(ckpt["scheduler_state_dict"])
+        return int(ckpt.get("epoch", 0)), ckpt.get("loss")
+
+    def train(self, start_epoch: int = 0):
         """Epoch loop with ReduceLROnPlateau and early stopping at patience 20 (:280-345)."""
         best, patience = float("inf"), 0
-        for epoch in range(self.config["num_epochs"]):
+        for epoch in range(start_epoch, self.config["num_epochs"]):
             train_loss = self.train_epoch()
             val_loss = self.validate_epoch()
             cur = val_loss if val_loss is not None else train_loss
