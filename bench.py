@@ -66,16 +66,18 @@ def stem_roofline(tr, N, spatial, reps):
 
     eng._ensure_packs()
 
+    sup = L.query("pcms_stem_supported", N, D, H, W) if eng.stem_fast else 0
+
     def fwd(s):
-        if eng.stem_fast:
+        if sup & 1:
             L.call("pcms_stem_fwd", s[0], eng.stem_pack, cs.mod.bias, s[1], stats, N, D, H, W)
         else:
             L.call("pcms_conv3_fwd", code, s[0], eng.cp, None, 0, cs.fwd, cs.mod.bias, s[1], None, 64, None,
                    stats, 0, N, D, H, W, 64, 1)
 
     def wgrad(s):
-        if eng.stem_fast:
-            L.call("pcms_stem_wgrad", s[0], s[2], dw, dwt, 5, N, D, H, W, 256)
+        if sup & 2:
+            L.call("pcms_stem_wgrad", s[0], s[2], dw, dwt, 5, N, D, H, W)
         else:
             L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
 

@@ -45,9 +45,12 @@ int pcms_conv3_pack2(int dtype, const float* w, void* fwd, void* dgrad, int Cout
  * output channels [0, cy0) -> y0, [cy0, Cout) -> y1 (dgrad concat split).
  * stats: BN partials or NULL: [mblocks][Cout][2] fp32 (sum, M2 = sum of squared
  * deviations from the row's own mean) followed by [mblocks] fp32 row voxel counts
- * (numerically stable moments; consumed by pcms_bn_finalize).  splits > 1: fp32
- * atomic accumulation into the zeroed yacc [Nvox][Cout]; finish with
- * pcms_split_epilogue.  Also used for dgrad with the flip pack.                      */
+ * (numerically stable moments; consumed by pcms_bn_finalize).  splits > 1 (split-K over
+ * input channels): every split stores its fp32 partial sums into its own slab of
+ * yacc [pcms_conv3_splits(...)][Nvox][Cout] (plain stores, no zeroing, no atomics);
+ * finish with pcms_split_epilogue, which adds the slabs in split order (deterministic).
+ * Also used for dgrad with the flip pack.                                              */
+int pcms_conv3_splits(int dtype, int Cin, int splits);  /* slabs a split-K launch uses   */
 int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
                    float* yacc, float* stats, int accumulate,
@@ -60,7 +63,10 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, hipStream_t s);
 /* Stem (inc.conv.0, bf16 build): input stored with 8 channels (n_modalities <= 8).
- * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32).                  */
+ * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32).
+ * pcms_stem_supported: bit 0 = pcms_stem_fwd runs this shape, bit 1 = pcms_stem_wgrad
+ * does (other shapes: the general pcms_conv3_fwd / pcms_conv3_wgrad).                   */
+int pcms_stem_supported(int N, int D, int H, int W);
 int pcms_stem_pack_elems(void);
 int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
 /* y = stem conv(x) + bias; BatchNorm partial moments into stats, laid out as pcms_conv3_fwd
@@ -68,16 +74,16 @@ int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
 int pcms_stem_fwd_rows(int N, int D, int H, int W);
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
                   int N, int D, int H, int W, hipStream_t s);
-/* dw [64][cin_w][27] += stem weight gradient.  D % 4 == H % 4 == W % 16 == 0: streaming
- * kernel (one partial row per CU in ws, then a fixed-order sum), ws =
- * pcms_stem_wgrad_ws_floats(...) floats; other shapes: tiled kernel (ws unused).          */
+/* dw [64][cin_w][27] += stem weight gradient (streaming kernel: one partial row per
+ * workgroup in ws, then a fixed-order sum), ws = pcms_stem_wgrad_ws_floats(...) floats.   */
 int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w);
 int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H,
-                    int W, int target_wgs, hipStream_t s);
-/* stats layout as pcms_conv3_fwd with rows = pcms_split_epilogue_rows(nvox)              */
+                    int W, hipStream_t s);
+/* y = sum of the `splits` slabs of acc (in split order) + bias -> storage type; stats
+ * layout as pcms_conv3_fwd with rows = pcms_split_epilogue_rows(nvox)                    */
 int pcms_split_epilogue_rows(long nvox);
-int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0,
-                        float* stats, int C, long nvox, hipStream_t s);
+int pcms_split_epilogue(int dtype, const float* acc, int splits, const float* bias, void* y0, void* y1,
+                        int cy0, float* stats, int C, long nvox, hipStream_t s);
 
 /* ---- BatchNorm3d (train / eval) + ReLU(inplace): models/unet3d.py:31-39 ----------- */
 /* part: the [rows][C][2] (sum, M2) partials + [rows] counts written by the conv / stem /
@@ -116,15 +122,20 @@ int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Co
 int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
                      int target_wgs, hipStream_t s);
-/* out[c] += sum over the sub-box of x (ConvTranspose3d bias gradient)                  */
-int pcms_box_channel_sum(int dtype, const void* x, float* out, int N, int D, int H, int W, int C,
+/* out[c] += sum over the sub-box of x (ConvTranspose3d bias gradient); ws:
+ * pcms_box_channel_sum_ws_floats(...) fp32 (per-block partial rows, fixed-order sum)     */
+int pcms_box_channel_sum_ws_floats(int dtype, int N, int C, int bd, int bh, int bw);
+int pcms_box_channel_sum(int dtype, const void* x, float* out, float* ws, int N, int D, int H, int W, int C,
                          int z0, int y0, int x0, int bd, int bh, int bw, hipStream_t s);
 
 /* ---- outc Conv3d(64, ncls, 1): models/unet3d.py:222,295 ---------------------------- */
 int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* logits,
                   long nvox_per_n, int N, int ncls, hipStream_t s);
+/* da = dlogits . w (written); dw / db += (per-block partial rows in ws, fixed-order sum);
+ * ws: pcms_head_bwd_ws_floats(...) fp32                                                  */
+int pcms_head_bwd_ws_floats(long nvox_per_n, int N, int ncls);
 int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w, void* da, float* dw,
-                  float* db, long nvox_per_n, int N, int ncls, hipStream_t s);
+                  float* db, float* ws, long nvox_per_n, int N, int ncls, hipStream_t s);
 
 /* ---- DiceLoss / BCEDiceLoss: utils/losses.py:44-92, 124-152 ------------------------ */
 int pcms_loss_rows(long M);
@@ -134,9 +145,21 @@ int pcms_loss_bwd(const float* x, const float* t, long M, const double* sums, fl
                   float wd, const float* gout, float* dx, hipStream_t s);
 
 /* ---- torch.optim.Adam(lr, weight_decay=1e-5): utils/trainer.py:113-117 ------------- */
-/* g_eff = gscale * g + wd * p (gscale = 1/world for the data-parallel mean)           */
-int pcms_adam(float* p, const float* g, float* m, float* v, long n, float step_size, float b1, float b2,
-              float eps, float wd, float bc2_sqrt, float gscale, hipStream_t s);
+/* g_eff = s * g + wd * p, s = gscale * (*gmul if gmul != NULL): gscale = 1/world (the
+ * data-parallel mean of summed gradients), *gmul = a device-side multiplier (gradient-clip
+ * coefficient x AMP unscale, from pcms_grad_clip).  When s != 1, s * g is written back to g. */
+int pcms_adam(float* p, float* g, float* m, float* v, long n, float step_size, float b1, float b2,
+              float eps, float wd, float bc2_sqrt, float gscale, const float* gmul, hipStream_t s);
+
+/* ---- torch.nn.utils.clip_grad_norm_(params, max_norm): train_bph.py:166,
+ * train_bph_cv.py:311 ------------------------------------------------------------------
+ * norm = gscale * ||g||_2 over the flat gradient (fp64 block partials, fixed-order sum);
+ * mul = gscale * min(1, max_norm / (norm + 1e-6)) (max_norm <= 0: gscale) -> device floats;
+ * apply != 0: g *= mul in place (else pass mul to pcms_adam as gmul).  A non-finite norm
+ * flags inf/NaN gradients (GradScaler's found_inf).  ws: pcms_grad_clip_ws_doubles().      */
+int pcms_grad_clip_ws_doubles(void);
+int pcms_grad_clip(float* g, long n, float gscale, float max_norm, int apply, double* ws, float* norm_out,
+                   float* mul_out, hipStream_t s);
 
 /* ---- misc -------------------------------------------------------------------------- */
 int pcms_add(int dtype, void* dst, const void* src, long n, hipStream_t s);

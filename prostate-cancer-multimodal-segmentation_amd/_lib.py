@@ -23,17 +23,19 @@ SIGNATURES = {
     "pcms_conv3_big_min_boxes": "i",
     "pcms_conv3_pack": "ippiiis",
     "pcms_conv3_pack2": "ipppiis",
+    "pcms_conv3_splits": "iii",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiis",
     "pcms_stem_pack_elems": "",
     "pcms_stem_pack": "ppis",
+    "pcms_stem_supported": "iiii",
     "pcms_stem_fwd_rows": "iiii",
     "pcms_stem_fwd": "pppppiiiis",
     "pcms_stem_wgrad_ws_floats": "iiiii",
-    "pcms_stem_wgrad": "ppppiiiiiis",
+    "pcms_stem_wgrad": "ppppiiiiis",
     "pcms_split_epilogue_rows": "l",
-    "pcms_split_epilogue": "ippppipils",
+    "pcms_split_epilogue": "ipipppipils",
     "pcms_bn_ws_doubles": "i",
     "pcms_bn_finalize": "piidpppppffppppps",
     "pcms_bn_eval_coeffs": "ppppfipps",
@@ -47,13 +49,17 @@ SIGNATURES = {
     "pcms_convt_dgrad": "ipppiiiiiiiiis",
     "pcms_convt_wgrad_ws_floats": "iiiiiii",
     "pcms_convt_wgrad": "ippppiiiiiiiiiis",
-    "pcms_box_channel_sum": "ippiiiiiiiiiiis",
+    "pcms_box_channel_sum_ws_floats": "iiiiii",
+    "pcms_box_channel_sum": "ipppiiiiiiiiiiis",
     "pcms_head_fwd": "ippppliis",
-    "pcms_head_bwd": "ippppppliis",
+    "pcms_head_bwd_ws_floats": "lii",
+    "pcms_head_bwd": "ipppppppliis",
     "pcms_loss_rows": "l",
     "pcms_loss_fwd": "pplfffppps",
     "pcms_loss_bwd": "pplpfffpps",
-    "pcms_adam": "pppplfffffffs",
+    "pcms_adam": "pppplfffffffps",
+    "pcms_grad_clip_ws_doubles": "",
+    "pcms_grad_clip": "plffippps",
     "pcms_add": "ippls",
 }
 

@@ -23,85 +23,9 @@
 #include <type_traits>
 #include <utility>
 
-// PCMS_ABL: ablation switches for the stem kernels, set only by the test-tooling build
-// (tests/kexp/Makefile) to time their parts separately; 0 in the product build.
-#ifndef PCMS_ABL
-#define PCMS_ABL 0
-#endif
+#include "conv_common.h"
 
 namespace {
-
-constexpr int kThreads = 256;
-constexpr int kRowBytes = 64;      // one halo row = one LDS row of the current ci-chunk
-constexpr int kHaloMax = 1152;     // halo voxels per workgroup (72 KiB LDS, 2 WG / CU)
-
-__device__ __attribute__((aligned(16))) uint32_t g_zero16[4];  // zero page for LDS-DMA padding
-constexpr uint32_t kOOB = 0x80000000u;  // buffer voffset past num_records: reads zeros
-
-template <typename T> struct Traits;
-template <> struct Traits<bf16_t> {
-  static constexpr int CK = 32;    // channels per chunk (64 B rows)
-  static constexpr int KS = 2;     // MFMA k-steps per chunk and tap (K = 16 each)
-  static constexpr int VEC = 8;    // elements per 16-byte piece
-  typedef s16x8_t Frag;
-};
-template <> struct Traits<float> {
-  static constexpr int CK = 16;
-  static constexpr int KS = 8;     // K = 2 each
-  static constexpr int VEC = 4;
-  typedef float Frag;
-};
-
-__device__ __forceinline__ f32x16_t mfma(s16x8_t a, s16x8_t b, f32x16_t c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x16_t mfma(float a, float b, f32x16_t c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-// 16-byte slot swizzle inside a 64-byte halo row (spreads ds_read_b128 lane groups).
-__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
-
-// MFMA row -> box voxel permutation inside a 32-row M-tile.  ds_read_b128 serves a wave in
-// the lane groups G0 = {0-3, 12-15, 20-27} and G1 = {4-11, 16-19, 28-31} (and +32).  With
-// 16-voxel w-runs (box width 16) G0 reads 16 consecutive halo rows of one h-row and G1 16 of
-// the next, so with swz() every group covers all 64 banks exactly once, for every tap.
-__device__ __forceinline__ int perm32(int r) {
-  if (r < 4) return r;
-  if (r < 12) return 16 + (r - 4);
-  if (r < 16) return 4 + (r - 12);
-  if (r < 20) return 24 + (r - 16);
-  if (r < 28) return 8 + (r - 20);
-  return 28 + (r - 28);
-}
-
-// A fragment from the halo tile. ks = k-step inside the chunk, h = lane >> 5.
-__device__ __forceinline__ s16x8_t lds_a(const char* lds, int row, int ks, int h, bf16_t*) {
-  int slot = (ks * 2 + h) ^ swz(row);
-  return *reinterpret_cast<const s16x8_t*>(lds + row * kRowBytes + slot * 16);
-}
-__device__ __forceinline__ float lds_a(const char* lds, int row, int ks, int h, float*) {
-  int c = ks * 2 + h;  // channel in chunk (0..15)
-  int slot = (c >> 2) ^ swz(row);
-  return *reinterpret_cast<const float*>(lds + row * kRowBytes + slot * 16 + (c & 3) * 4);
-}
-// B fragment (weights) straight from global: packed [chunk][27][Cout][CK].
-__device__ __forceinline__ s16x8_t gl_b(const bf16_t* wrow, int ks, int h) {
-  return *reinterpret_cast<const s16x8_t*>(wrow + ks * 16 + h * 8);
-}
-__device__ __forceinline__ float gl_b(const float* wrow, int ks, int h) { return wrow[ks * 2 + h]; }
-
-struct Conv3Params {
-  const void* x0; const void* x1; int c0; int c1;
-  const void* w; const float* bias;
-  void* y0; void* y1; int cy0;
-  float* yacc; float* stats;
-  int accumulate;
-  int N, D, H, W, Cin, Cout;
-  int nchunk, chunks_per_split;
-  int lbd, lbh, lbw, nbd, nbh, nbw;
-};
 
 // LBD/LBH/LBW >= 0: compile-time box geometry (the hot (4, 8, 16) box: halo decode and tap
 // offsets become constant arithmetic); -1: runtime geometry from p.
@@ -324,8 +248,8 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
         for (int nt = 0; nt < 2; ++nt) {
           const int co = co_base + nt * 32 + r_lane;
           float v = acc[mt][nt][e];
-          if (p.yacc) {
-            atomicAdd(p.yacc + vox * p.Cout + co, v);
+          if (p.yacc) {  // split-K: this split's own fp32 slab (summed in a fixed order later)
+            p.yacc[((long)blockIdx.z * p.nvox + vox) * p.Cout + co] = v;
             continue;
           }
           v += bias_l[nt];
@@ -445,15 +369,6 @@ struct WgradParams {
   int cw, direct;
 };
 
-// dy tile: 128-B (bf16) rows, 64-B halves swizzled by row bit 1 (conflict-free tr reads).
-__device__ __forceinline__ int dy_off_bf16(int v, int co) {  // co in 0..63 (element)
-  int half = (co >> 5) ^ ((v >> 1) & 1);
-  return v * 128 + half * 64 + (co & 31) * 2;
-}
-
-__device__ __forceinline__ s16x4_t tr_read(const char* lds, int byte_off) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + byte_off));
-}
 
 template <typename T, int LBD, int LBH, int LBW>
 __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p) {
@@ -472,7 +387,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   const int ntap = (tg == 3) ? 6 : 7;
   // bf16 layout: wave w owns taps w, w + 8, w + 16 (, w + 24) for BOTH co tiles, so each B
   // (x) fragment feeds 2 MFMAs: 1.5 LDS reads per MFMA instead of 2.3 (8 accumulators)
-  constexpr bool kW2 = sizeof(T) == 2 && !(PCMS_ABL & 16384);
+  constexpr bool kW2 = sizeof(T) == 2;
   const int ntap2 = wave < 3 ? 4 : 3;
   // 1-D grid, logical id XCD-aware (dispatch is round-robin over 8 XCDs: consecutive logical
   // ids land on one XCD at about the same time), tile (co block, ci block) fastest: the
@@ -639,29 +554,6 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           }
         }
         continue;
-      } else if constexpr (sizeof(T) == 2) {
-        // lane 4q+p of each 16-lane group: row q, cols 4p..4p+3 of a 4x16 block
-        const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-        const int v_a = k0 + 8 * hsel + qq;          // rows for elements 0..3; +4 for 4..7
-        const int co = cot * 32 + g * 16 + pp * 4;
-        s16x4_t lo = tr_read(buf, dy_off_bf16(v_a, co));
-        s16x4_t hi = tr_read(buf, dy_off_bf16(v_a + 4, co));
-        a = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        // with a compile-time box of width >= 16 the lane's rows share (rd, rh) with k0
-        const int hr0 = LBW >= 4 ? halo_row(k0) + 8 * hsel + qq : halo_row(v_a);
-        const int hr1 = LBW >= 4 ? hr0 + 4 : halo_row(v_a + 4);
-        const int ci = g * 16 + pp * 4;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) {
-          if (j < ntap) {
-            const int tap = tg + 4 * j;
-            const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-            const int off = (kd * HH + kh) * HW + kw;
-            s16x4_t l2 = tr_read(xb, (hr0 + off) * Tr::XROW + ci * 2);
-            s16x4_t h2 = tr_read(xb, (hr1 + off) * Tr::XROW + ci * 2);
-            bf[j] = (s16x8_t){l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
-          }
-        }
       } else {
         const int v = k0 + hsel;
         a = *reinterpret_cast<const float*>(buf + v * Tr::DYROW + (cot * 32 + (lane & 31)) * 4);
@@ -742,9 +634,9 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       __syncthreads();
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
-        if (b + 1 < b_end && !(PCMS_ABL & 4096)) stage_load(b + 1);
-        if (!(PCMS_ABL & 8192)) compute(wlds + cur * BUFBYTES);
-        if (b + 1 < b_end && !(PCMS_ABL & 4096)) stage_store(wlds + (cur ^ 1) * BUFBYTES);
+        if (b + 1 < b_end) stage_load(b + 1);
+        compute(wlds + cur * BUFBYTES);
+        if (b + 1 < b_end) stage_store(wlds + (cur ^ 1) * BUFBYTES);
         __syncthreads();
       }
     } else {
@@ -937,77 +829,6 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_kernel(const float* w, bf
   }
 }
 
-struct Box { int lbd, lbh, lbw; };
-
-int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
-
-// Pick a power-of-two box (<= maxvol voxels, halo <= maxhalo rows) minimising padded
-// volume (then maximising box size) for a D x H x W grid.
-Box choose_box(int D, int H, int W, int maxvol, int maxhalo, int minw, int minvol) {
-  Box best{3, 3, 3};  // (8,8,8): always valid (vol 512, halo 1000) -- overwritten below
-  double best_cost = 1e30;
-  for (int a = 0; a <= 4; ++a)
-    for (int b = 0; b <= 5; ++b)
-      for (int c = 0; c <= 6; ++c) {
-        const int bd = 1 << a, bh = 1 << b, bw = 1 << c;
-        if (bd * bh * bw > maxvol || bd * bh * bw < minvol) continue;
-        if ((bd + 2) * (bh + 2) * (bw + 2) > maxhalo) continue;
-        if (bw < minw && bw < W) continue;
-        const double padded = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh * cdiv(W, bw) * bw;
-        const double halo = (double)cdiv(D, bd) * cdiv(H, bh) * cdiv(W, bw) * (bd + 2) * (bh + 2) * (bw + 2);
-        const double cost = padded + 0.15 * halo;
-        if (cost < best_cost - 1e-9) { best_cost = cost; best = Box{a, b, c}; }
-      }
-  return best;
-}
-
-// Forward/dgrad box: 512 voxels; width 16 whenever the grid is that wide (perm32 layout).
-Box fwd_box(int D, int H, int W) {
-  if (W >= 16) {
-    Box best{0, 0, 4};
-    double bc = 1e30;
-    for (int a = 0; a <= 5; ++a) {
-      const int b = 5 - a;  // bd * bh = 32
-      const int bd = 1 << a, bh = 1 << b;
-      if ((bd + 2) * (bh + 2) * 18 > kHaloMax) continue;
-      const double cost = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh +
-                          0.15 * cdiv(D, bd) * cdiv(H, bh) * (bd + 2) * (bh + 2) * 18 / 16.0;
-      if (cost < bc - 1e-9 || (cost < bc + 1e-9 && a == 2)) { bc = cost; best = Box{a, b, 4}; }
-    }
-    return best;
-  }
-  return choose_box(D, H, W, 512, kHaloMax, 4, 32);
-}
-
-// ------------------------------------------------------------------------------------
-// Stem conv (inc.conv.0: n_modalities -> 64, input stored with 8 channels), bf16.
-// The generic kernel would spend 4x its MFMA work on zero channels (K = 27 x 32); here the
-// K dimension packs two taps per MFMA k-step: k = (tap 2s + h, channel c), h = lane >> 5,
-// so K = 14 x 16 = 224 (135 real).  HBM-bound: 16 B in + 128 B out per voxel.
-// ------------------------------------------------------------------------------------
-constexpr int kStemSteps = 14;                    // 28 taps (27 + 1 zero) / 2
-constexpr int kStemWBytes = kStemSteps * 64 * 16 * 2;  // packed weights [14][64][16] bf16
-
-// master W[64][cin_w][27] fp32 -> [14][64][16] bf16, k = h * 8 + c <-> (tap 2s + h, c);
-// the 64 output columns are ordered (nt, j) -> channel 2 j + nt so that a lane's two MFMA
-// tiles hold an adjacent channel pair (one packed bf16x2 LDS write per row)
-__global__ void stem_pack_kernel(const float* w, bf16_t* out, int cin_w) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= kStemSteps * 64 * 16) return;
-  const int k = i & 15, col = (i >> 4) & 63, s = i >> 10;
-  const int co = 2 * (col & 31) + (col >> 5);  // MFMA column (nt, j) <-> channel 2 j + nt
-  const int tap = 2 * s + (k >> 3), c = k & 7;
-  float v = 0.f;
-  if (tap < 27 && c < cin_w) v = w[((long)co * cin_w + c) * 27 + tap];
-  out[i] = f2bf(v);
-}
-
-__device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
-  if (tap >= 27) return 0;  // zero-weight pad tap: any in-halo row
-  const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-  return (kd * HH + kh) * HW + kw;
-}
-
 // Both bf16 packs of one conv from ONE read of the fp32 weight (Cin % 32 == Cout % 32 == 0).
 // Block (co j0 .. j0+32, ci c*32 .. +32): the 32 contiguous 864-float runs w[co][c*32..][27]
 // are converted to bf16 once into LDS (same rounding as pack_bf16x2), then both packs are
@@ -1053,1128 +874,6 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* 
   }
 }
 
-// Persistent stem forward: one 8-wave workgroup per CU walks boxes b = blockIdx.x,
-// b += gridDim.x.  LDS: weights (loaded once) | halo x2 (LDS-DMA, next box prefetched while
-// the current one computes) | bf16 C tile (16-B coalesced stores).  Every thread issues
-// exactly kStemStores stores per box (invalid ones go to a sink), so the next halo's DMA,
-// issued before them, is retired by s_waitcnt vmcnt(kStemStores).
-constexpr int kStemThreads = 512;
-constexpr int kStemHaloBytes = kHaloMax * 16;                 // 18 KiB
-constexpr int kStemCtOff = 2 * kStemHaloBytes;                 // C tile offset
-constexpr int kStemLds = kStemCtOff + 512 * 64 * 2 + 6144;     // + stats reduction [8][64][3]
-constexpr int kStemStores = 512 * 8 / kStemThreads;            // 16-B stores per thread per box
-__device__ __attribute__((aligned(16))) uint32_t g_sink[4 * 512];
-
-template <int LBD, int LBH, int LBW>
-__global__ void __launch_bounds__(kStemThreads, 1) stem_fwd_kernel(Conv3Params p, int nbox) {
-  const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  bf16_t* ct = reinterpret_cast<bf16_t*>(lds + kStemCtOff);
-  float* red = reinterpret_cast<float*>(lds + kStemCtOff + 512 * 64 * 2);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r_lane = lane & 31, hsel = lane >> 5;
-  const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
-  const int boxvol = bd * bh * bw;
-  const int HH = bh + 2, HW = bw + 2;
-  const int HV = (bd + 2) * HH * HW;
-  const long plane = (long)p.H * p.W;
-  const bf16_t* x0 = (const bf16_t*)p.x0;
-  const bool w16 = lbw_ == 4;
-  const int prow = w16 ? perm32(r_lane) : r_lane;
-  int hb[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    int r = wave * 64 + mt * 32 + prow;
-    if (r >= boxvol) r = 0;
-    const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
-    hb[mt] = (rd * HH + rh) * HW + rw;
-  }
-  const bool wave_active = wave * 64 < boxvol;
-  float bias_l[2] = {0.f, 0.f};
-  if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
-
-  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
-    int bwi = b % p.nbw; b /= p.nbw;
-    int bhi = b % p.nbh; b /= p.nbh;
-    int bdi = b % p.nbd;
-    n = b / p.nbd;
-    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
-  };
-  auto stage_halo = [&](int b, char* hl) {
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-    for (int base = wave * 64; base < HV; base += kStemThreads) {
-      const int hv = base + lane;
-      const void* src = g_zero16;
-      if (hv < HV) {
-        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
-        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W)
-          src = x0 + (((long)n * p.D + gd) * plane + (long)gh * p.W + gw) * 8;
-      }
-      __builtin_amdgcn_global_load_lds(src, (LDS_AS void*)(hl + base * 16), 16, 0, 0);
-    }
-  };
-  // prologue: the B fragments of all 14 k-steps stay in registers for the whole kernel
-  // (28 x 16 B per lane, loaded once); first halo
-  s16x8_t wb[kStemSteps][2];
-  {
-    const bf16_t* wg = (const bf16_t*)p.w;
-#pragma unroll
-    for (int st = 0; st < kStemSteps; ++st) {
-      wb[st][0] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + r_lane) * 16 + hsel * 8);
-      wb[st][1] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
-    }
-  }
-  int b = blockIdx.x;
-  if (b < nbox) stage_halo(b, lds);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
-    char* hl = lds + (it & 1) * kStemHaloBytes;
-    const int bn = b + gridDim.x;
-    if (bn < nbox) stage_halo(bn, lds + ((it + 1) & 1) * kStemHaloBytes);
-    f32x16_t acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];  // bias folded into the accumulator
-    if (wave_active) {
-      // lane half hsel reads tap 2 st + hsel: constant base offset + hsel * constant delta.
-      // A fragments are prefetched one k-step ahead; sched_barrier keeps the compiler from
-      // hoisting every step's LDS reads (register pressure: the weights live in VGPRs).
-      // (hs16 is opaque so the 28 per-step lane addresses are formed in the loop, not
-      // hoisted out of it into spilled registers)
-      int hs16 = hsel * 16;
-      asm volatile("" : "+v"(hs16));
-      auto load_a = [&](int st, s16x8_t (&a)[2]) {
-        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
-        const int off16 = o0 * 16 + hs16 * (o1 - o0);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb[mt] * 16 + off16);
-      };
-      s16x8_t abuf[2][2];
-      load_a(0, abuf[0]);
-#pragma unroll
-      for (int st = 0; st < kStemSteps; ++st) {
-        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
-          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-    const bool interior = d0 + bd <= p.D && h0 + bh <= p.H && w0 + bw <= p.W;
-    // Epilogue: C tile -> LDS as packed bf16 channel pairs; BatchNorm partials single-pass,
-    // shifted by the wave's row-0 value K of each channel: per wave S1 = sum d + n K,
-    // M2 = sum d^2 - (sum d)^2 / n (d = v - K), waves merged with Chan's formula below.
-    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(acc[0][nt][0], r_lane, 64);
-    float nw = 0.f;
-    __syncthreads();  // previous box's C-tile reads (stores) are done in every wave
-    if (wave_active) {
-      // row of (mt, e) = perm32((e & 3) + 8 (e >> 2) + 4 hsel) as constant + (+-16 hsel); the
-      // opaque hp keeps the per-row indices from being hoisted out of the box loop (they
-      // would pin ~100 VGPRs)
-      int hp = hsel * 16;
-      asm volatile("" : "+v"(hp));
-      auto row_of = [&](int mt, int e) {
-        const int g = e >> 2;
-        const int base = wave * 64 + mt * 32 + (e & 3);
-        if (w16) return base + (g == 0 ? hp : g == 1 ? 20 - hp : g == 2 ? 24 - hp : 12 + hp);
-        return base + 8 * g + (hp >> 2);
-      };
-      if (interior && boxvol == 512) {  // every row valid: no per-row tests
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int r = row_of(mt, e);
-            const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-            *reinterpret_cast<uint32_t*>(ct + r * 64 + 2 * r_lane) = pack_bf16x2(v0, v1);
-            const float e0 = v0 - K[0], e1 = v1 - K[1];
-            s1[0] += e0; s2[0] += e0 * e0;
-            s1[1] += e1; s2[1] += e1 * e1;
-          }
-        nw = 64.f;
-      } else {
-        int cnt = 0;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int r = row_of(mt, e);
-            const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-            *reinterpret_cast<uint32_t*>(ct + r * 64 + 2 * r_lane) = pack_bf16x2(v0, v1);
-            const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
-            const bool valid = r < boxvol && d0 + rd < p.D && h0 + rh < p.H && w0 + rw < p.W;
-            const float e0 = valid ? v0 - K[0] : 0.f, e1 = valid ? v1 - K[1] : 0.f;
-            s1[0] += e0; s2[0] += e0 * e0;
-            s1[1] += e1; s2[1] += e1 * e1;
-            cnt += valid ? 1 : 0;
-          }
-        nw = (float)(cnt + __shfl_xor(cnt, 32, 64));
-      }
-    }
-    if (p.stats) {
-      const float inv = nw > 0.f ? 1.f / nw : 0.f;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        s1[nt] += __shfl_xor(s1[nt], 32, 64);
-        s2[nt] += __shfl_xor(s2[nt], 32, 64);
-        if (hsel == 0) {
-          float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
-          rp[0] = s1[nt] + nw * K[nt];
-          rp[1] = s2[nt] - s1[nt] * s1[nt] * inv;
-          rp[2] = nw;
-        }
-      }
-    }
-    __syncthreads();
-    if (p.stats && tid < 64) {
-      float S = 0.f, Nn = 0.f;
-#pragma unroll
-      for (int w = 0; w < kStemThreads / 64; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
-      const float m = Nn > 0.f ? S / Nn : 0.f;
-      float M2 = 0.f, sdd = 0.f;
-#pragma unroll
-      for (int w = 0; w < kStemThreads / 64; ++w) {
-        const float c = red[(w * 64 + tid) * 3 + 2];
-        if (c > 0.f) {
-          const float d = red[(w * 64 + tid) * 3] / c - m;
-          M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
-          sdd += c * d;
-        }
-      }
-      if (Nn > 0.f) M2 -= sdd * sdd / Nn;
-      float* stp = p.stats + ((long)b * 64 + tid) * 2;
-      stp[0] = S;
-      stp[1] = M2;
-      if (tid == 0) p.stats[(long)nbox * 64 * 2 + b] = Nn;
-    }
-#pragma unroll 2
-    for (int i = 0; i < kStemStores; ++i) {
-      const int pc = tid + i * kStemThreads;
-      const int r = pc >> 3, q = pc & 7;
-      const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
-      const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
-      u32x4_t* dst = reinterpret_cast<u32x4_t*>(g_sink) + (tid & 511);
-      if (r < boxvol && (interior || (gd < p.D && gh < p.H && gw < p.W)))
-        dst = reinterpret_cast<u32x4_t*>((bf16_t*)p.y0 + (((long)n * p.D + gd) * plane + (long)gh * p.W + gw) * 64 + q * 8);
-      *dst = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
-    }
-    // the next halo's LDS-DMA (issued before the stores) has landed; make it visible
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStemStores) : "memory");
-    __syncthreads();
-  }
-}
-
-// Persistent stem forward, direct-store variant for 16-wide 512-voxel boxes (bd x bh = 32).
-// No C tile: the weight columns are ordered so that lane r_lane of a wave holds channels
-// (2 r_lane, 2 r_lane + 1) of each of its rows, so the 32 lanes of a half-wave write one
-// voxel's 64 channels (128 contiguous bytes) with ONE buffer_store_dword, addressed by a
-// per-lane voffset (2 variants), a wave-uniform soffset and an immediate offset: no VALU
-// address math, no LDS round trip, one barrier per box.  The halo arrives by buffer LDS-DMA
-// (out-of-range voffset = zero padding); weights stay in VGPRs; BatchNorm partials are
-// accumulated over all boxes of the workgroup (shifted sums) and written as ONE stats row
-// per workgroup (rows >= gridDim.x are zeroed: count 0).
-// THR = 512: one 8-wave workgroup per CU, 512-voxel boxes; THR = 256: two independent
-// 4-wave workgroups per CU with 256-voxel boxes (each workgroup's barrier-synchronised
-// compute and store phases drift against the other's).
-constexpr int kSDHaloRows = kHaloMax;                         // 1152 rows (18 x 64)
-constexpr int kSDHaloBytes = kSDHaloRows * 16;
-constexpr int kSDLds = 2 * kSDHaloBytes + 8 * 64 * 3 * 4;     // halo x2 + stats reduction
-constexpr int kSDThr = (PCMS_ABL & 8192) ? 256 : 512;  // product variant (256: same time, 101 vs 102 us)
-
-// PIPE: software-pipelined stores.  Tile mt = 0 of a box is computed first and its 16
-// stores are issued between the MFMAs of tile mt = 1; tile 1's stores go out between the
-// MFMAs of the NEXT box's tile 0 (the last one after the loop).  Stores and BN sums thus run
-// inside the MFMA gaps of the same wave instead of after all its MFMAs.
-template <int LBD, int LBH, int THR, bool PIPE = false>
-__global__ void __launch_bounds__(THR, (PIPE && THR == 256) ? 1 : 512 / THR) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
-                                                                         uint32_t xbytes, uint32_t ybytes) {
-  constexpr int kSDThreads = THR, NWV = THR / 64;
-  static_assert((1 << (LBD + LBH + 4)) == NWV * 64, "box = 64 voxels per wave");
-  constexpr int bd = 1 << LBD, bh = 1 << LBH, bw = 16;
-  constexpr int HH = bh + 2, HW = bw + 2, HV = (bd + 2) * HH * HW;
-  constexpr int NP = (HV + kSDThreads - 1) / kSDThreads;  // halo pieces per thread
-  static_assert(HV <= kSDHaloRows, "halo fits");
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* red = reinterpret_cast<float*>(lds + 2 * kSDHaloBytes);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR math)
-  const int r_lane = lane & 31, hsel = lane >> 5;
-  const int D = p.D, H = p.H, W = p.W;
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x0, 0, xbytes, 0x00020000);
-  const auto yr = __builtin_amdgcn_make_buffer_rsrc(p.y0, 0, ybytes, 0x00020000);
-
-  // weights: B fragments of all 14 k-steps in registers
-  s16x8_t wb[kStemSteps][2];
-  {
-    const bf16_t* wg = (const bf16_t*)p.w;
-#pragma unroll
-    for (int st = 0; st < kStemSteps; ++st) {
-      wb[st][0] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + r_lane) * 16 + hsel * 8);
-      wb[st][1] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
-    }
-  }
-  float bias_l[2] = {0.f, 0.f};
-  if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
-  // halo rows of the two 32-row MFMA tiles (perm32 layout)
-  int hb16[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int r = wave * 64 + mt * 32 + perm32(r_lane);
-    const int rd = r >> (LBH + 4), rh = (r >> 4) & (bh - 1), rw = r & 15;
-    hb16[mt] = ((rd * HH + rh) * HW + rw) * 16;
-  }
-  // halo pieces of this thread: relative source offset (bytes) and packed coordinates
-  int prel[NP], pco[NP];
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int hv = tid + i * kSDThreads;
-    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-    prel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
-    pco[i] = hv < HV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
-  }
-  // store voffsets: rows x = perm32((e & 3) + 8 g + 4 hsel) have x & 15 = 4 g + (e & 3) and
-  // x >> 4 = (g in {1, 2}) ^ hsel
-  const uint32_t vb0 = r_lane * 4, vb1 = r_lane * 4 + (uint32_t)W * 128;
-  const uint32_t vA = hsel ? vb1 : vb0;  // g = 0, 3
-  const uint32_t vB = hsel ? vb0 : vb1;  // g = 1, 2
-
-  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
-    const int nbw = p.nbw, nbh = p.nbh, nbd = p.nbd;
-    int q = b;
-    const int bwi = q % nbw; q /= nbw;
-    const int bhi = q % nbh; q /= nbh;
-    const int bdi = q % nbd;
-    n = q / nbd;
-    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
-  };
-  auto stage = [&](int b, int buf) {
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-    const int base16 = ((((n * D + d0) * H + h0) * W) + w0) * 16;
-    const bool inner = d0 >= 1 && d0 + bd < D && h0 >= 1 && h0 + bh < H && w0 >= 1 && w0 + bw < W;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      if (wave * 64 + i * kSDThreads >= HV) break;  // whole wave past the halo (uniform)
-      uint32_t voff = (uint32_t)(base16 + prel[i]);
-      const int c = pco[i];
-      if (c < 0) {
-        voff = kOOB;
-      } else if (!inner) {
-        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
-        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (LDS_AS void*)(lds + buf * kSDHaloBytes + (wave * 64 + i * kSDThreads) * 16),
-                                           16, voff, 0, 0, 0);
-    }
-  };
-
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2] = {0.f, 0.f};
-  float cnt = 0.f;
-  bool first = true;
-  int b = blockIdx.x;
-  if (b < nbox) stage(b, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (PIPE) {
-    // one pending tile: values, store soffset, validity inputs
-    struct Tile {
-      f32x16_t v[2];
-      uint32_t so;
-      int rd, rh, d0, h0, w0;
-      bool full;
-    };
-    auto tile_meta = [&](Tile& t, int bb, int mt) {
-      int n, d0, h0, w0;
-      origin(bb, n, d0, h0, w0);
-      const int R0 = wave * 4 + mt * 2;
-      t.rd = R0 >> LBH; t.rh = R0 & (bh - 1);
-      t.d0 = d0; t.h0 = h0; t.w0 = w0;
-      t.full = d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
-      const int bv = ((n * D + d0) * H + h0) * W + w0;
-      t.so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (t.rd * H + t.rh) * W) * 128u);
-    };
-    // element e of tile t: one buffer store + BN shifted sums
-    auto store_e = [&](const Tile& t, int e) {
-      const int g = e >> 2, rw = 4 * g + (e & 3);
-      const bool gB = (g == 1 || g == 2);
-      const float v0 = t.v[0][e], v1 = t.v[1][e];
-      uint32_t voff = gB ? vB : vA;
-      float e0 = v0 - K[0], e1 = v1 - K[1];
-      if (!t.full) {
-        const int xh = (gB ? 1 : 0) ^ hsel;
-        const bool valid = (t.d0 + t.rd < D) & (t.h0 + t.rh + xh < H) & (t.w0 + rw < W);
-        voff = valid ? voff : kOOB;
-        e0 = valid ? e0 : 0.f;
-        e1 = valid ? e1 : 0.f;
-        cnt += valid ? 1.f : 0.f;
-      }
-      __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, t.so + rw * 128, 0);
-      s1[0] += e0; s2[0] += e0 * e0;
-      s1[1] += e1; s2[1] += e1 * e1;
-    };
-    auto count_full = [&](const Tile& t) { if (t.full) cnt += 16.f; };
-    Tile pend, cur;
-    bool have_pend = false;
-    int hs16 = hsel * 16;
-    asm volatile("" : "+v"(hs16));
-    for (int it = 0; b < nbox; b += gridDim.x, ++it) {
-      __syncthreads();
-      const int bn = b + gridDim.x;
-      if (bn < nbox) stage(bn, (it + 1) & 1);
-      const char* hl = lds + (it & 1) * kSDHaloBytes;
-      // one 32-row tile: 14 k-steps x 2 MFMAs; `st_` = the tile whose stores fill the gaps
-      auto run_tile = [&](auto with_st, int mt, Tile& out, const Tile& st_) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) out.v[j][e] = bias_l[j];
-        auto load_a = [&](int st) {
-          const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
-          return *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + o0 * 16 + hs16 * (o1 - o0));
-        };
-        s16x8_t abuf[2];
-        abuf[0] = load_a(0);
-#pragma unroll
-        for (int st = 0; st < kStemSteps; ++st) {
-          if (st + 1 < kStemSteps) abuf[(st + 1) & 1] = load_a(st + 1);
-          out.v[0] = mfma(abuf[st & 1], wb[st][0], out.v[0]);
-          out.v[1] = mfma(abuf[st & 1], wb[st][1], out.v[1]);
-          if constexpr (decltype(with_st)::value) {  // 16 stores over 14 steps: two extra on the first two
-            store_e(st_, st);
-            if (st < 2) store_e(st_, 14 + st);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-      if (have_pend) {
-        run_tile(std::true_type{}, 0, cur, pend);
-        count_full(pend);
-      } else {
-        run_tile(std::false_type{}, 0, cur, pend);
-      }
-      tile_meta(cur, b, 0);
-      if (first) {
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(cur.v[nt][0], r_lane, 64);
-        first = false;
-      }
-      run_tile(std::true_type{}, 1, pend, cur);
-      count_full(cur);
-      tile_meta(pend, b, 1);
-      have_pend = true;
-      // the next halo's DMA was issued before this box's stores (16 on the first box, 32 after)
-      if (it == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    }
-    if (have_pend) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) store_e(pend, e);
-      count_full(pend);
-    }
-  } else
-  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
-    // halo(b) has landed for this wave (vmcnt above / at the loop end); barrier: for all
-    // waves, and every wave is done reading the buffer the next DMA overwrites
-    __syncthreads();
-    const int bn = b + gridDim.x;
-    if (bn < nbox && !(PCMS_ABL & 4)) stage(bn, (it + 1) & 1);
-    const char* hl = lds + (it & 1) * kSDHaloBytes;
-    f32x16_t acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];
-    if (!(PCMS_ABL & 1)) {
-      int hs16 = hsel * 16;
-      asm volatile("" : "+v"(hs16));
-      auto load_a = [&](int st, s16x8_t (&a)[2]) {
-        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
-        const int off16 = o0 * 16 + hs16 * (o1 - o0);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + off16);
-      };
-      s16x8_t abuf[2][2];
-      load_a(0, abuf[0]);
-#pragma unroll
-      for (int st = 0; st < kStemSteps; ++st) {
-        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
-          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // ---- epilogue: direct stores + shifted BN sums ----
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-    const bool full = d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
-    if (first) {
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(acc[0][nt][0], r_lane, 64);
-      first = false;
-    }
-    const int bv = ((n * D + d0) * H + h0) * W + w0;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const int R0 = wave * 4 + mt * 2;          // even (rd, rh) linear index of the tile
-      const int rd0 = R0 >> LBH, rh0 = R0 & (bh - 1);
-      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (rd0 * H + rh0) * W) * 128u);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int g = e >> 2, rw = 4 * g + (e & 3);
-        const bool gB = (g == 1 || g == 2);
-        const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-        uint32_t voff = gB ? vB : vA;
-        float e0 = v0 - K[0], e1 = v1 - K[1];
-        if (!full) {  // uniform branch: boundary boxes only
-          const int xh = (gB ? 1 : 0) ^ hsel;
-          const bool valid = (d0 + rd0 < D) & (h0 + rh0 + xh < H) & (w0 + rw < W);
-          voff = valid ? voff : kOOB;
-          e0 = valid ? e0 : 0.f;
-          e1 = valid ? e1 : 0.f;
-          cnt += valid ? 1.f : 0.f;
-        }
-        if (!(PCMS_ABL & 2)) __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so + rw * 128, 0);
-        s1[0] += e0; s2[0] += e0 * e0;
-        s1[1] += e1; s2[1] += e1 * e1;
-      }
-    }
-    if (full) cnt += 32.f;
-    // the next halo's DMA was issued before this box's 32 stores
-    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-  }
-  if (!p.stats) return;
-  // per wave (lanes r_lane and r_lane + 32 share channels and K): S = sum d + n K,
-  // M2 = sum d^2 - (sum d)^2 / n; then Chan across the 8 waves
-  const float nw = cnt + __shfl_xor(cnt, 32, 64);
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    s1[nt] += __shfl_xor(s1[nt], 32, 64);
-    s2[nt] += __shfl_xor(s2[nt], 32, 64);
-    if (hsel == 0) {
-      float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
-      rp[0] = s1[nt] + nw * K[nt];
-      rp[1] = nw > 0.f ? s2[nt] - s1[nt] * s1[nt] / nw : 0.f;
-      rp[2] = nw;
-    }
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float S = 0.f, Nn = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
-    const float m = Nn > 0.f ? S / Nn : 0.f;
-    float M2 = 0.f, sdd = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) {
-      const float c = red[(w * 64 + tid) * 3 + 2];
-      if (c > 0.f) {
-        const float d = red[(w * 64 + tid) * 3] / c - m;
-        M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
-        sdd += c * d;
-      }
-    }
-    if (Nn > 0.f) M2 -= sdd * sdd / Nn;
-    float* st = p.stats + ((long)blockIdx.x * 64 + tid) * 2;
-    st[0] = S;
-    st[1] = M2;
-    float* cnts = p.stats + (long)mrows * 128;  // row counts after the [mrows][64][2] block
-    if (tid == 0) cnts[blockIdx.x] = Nn;
-    // zero this workgroup's share of the rows past gridDim.x
-    for (int r = blockIdx.x + gridDim.x; r < mrows; r += gridDim.x) {
-      p.stats[((long)r * 64 + tid) * 2] = 0.f;
-      p.stats[((long)r * 64 + tid) * 2 + 1] = 0.f;
-      if (tid == 0) cnts[r] = 0.f;
-    }
-  }
-}
-
-// Wave-independent persistent stem forward: the hot case D % 2 == H % 2 == 0, W % 16 == 0.
-// Every wave owns a private stream of 2x2x16-voxel boxes (64 voxels = two 32-row MFMA
-// tiles) with its own 3-slot LDS ring of halos (4x4x18 rows, buffer LDS-DMA, prefetch
-// distance 2): no barrier inside the box loop, so the two waves sharing a SIMD drift apart
-// and one's MFMAs cover the other's epilogue.  MFMA row r of tile mt is voxel
-// (rd, rh, rw) = (mt, r >> 4, 2 (r & 3) + ((r >> 2) & 1) + 8 ((r >> 3) & 1)), so an
-// accumulator register of the 32x32 layout holds two ADJACENT voxels (lane halves) and each
-// buffer_store_dword writes 256 contiguous bytes with a per-lane constant voffset, a
-// per-(mt, row pair) soffset and an immediate offset.  Weights stay in VGPRs; BatchNorm
-// partials (shifted sums) are merged over the workgroup once at the end: ONE stats row per
-// workgroup (pcms_stem_fwd_rows).  Box order is XCD-aware (8 consecutive logical
-// workgroups' neighbouring boxes share one L2).
-constexpr int kSWvThreads = 512;
-constexpr int kSWvHalo = 4 * 4 * 18;                           // 288 halo rows
-constexpr int kSWvPieces = 5;                                  // DMA instructions per box (320 rows)
-constexpr int kSWvSlot = kSWvPieces * 64 * 16;                 // 5 KiB per ring slot
-constexpr int kSWvLds = 8 * 3 * kSWvSlot + 8 * 64 * 3 * 4;     // 120 KiB rings + stats merge
-
-__global__ void __launch_bounds__(kSWvThreads, 1) stem_fwd_wave_kernel(const bf16_t* x, const bf16_t* wpack,
-                                                                      const float* bias, bf16_t* y, float* stats,
-                                                                      int N, int D, int H, int W,
-                                                                      uint32_t xbytes, uint32_t ybytes) {
-  constexpr int HH = 4, HW = 18;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* red = reinterpret_cast<float*>(lds + 8 * 3 * kSWvSlot);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r_lane = lane & 31, hsel = lane >> 5;
-  const i32x4_t xr = buffer_desc(x, xbytes);
-  const auto yr = __builtin_amdgcn_make_buffer_rsrc(y, 0, ybytes, 0x00020000);
-  const int nbw = W >> 4, nbh = H >> 1, nbd = D >> 1;
-  const int nwb = N * nbd * nbh * nbw;
-  // logical workgroup: consecutive logical ids on one XCD (dispatch is round-robin over 8)
-  const int G = gridDim.x;
-  const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-  const int stride = G * 8;
-
-  s16x8_t wb[kStemSteps][2];
-#pragma unroll
-  for (int st = 0; st < kStemSteps; ++st) {
-    wb[st][0] = *reinterpret_cast<const s16x8_t*>(wpack + (st * 64 + r_lane) * 16 + hsel * 8);
-    wb[st][1] = *reinterpret_cast<const s16x8_t*>(wpack + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
-  }
-  const float bias0 = bias ? bias[2 * r_lane] : 0.f, bias1 = bias ? bias[2 * r_lane + 1] : 0.f;
-  // A rows: halo row of this lane's voxel in tile mt
-  int hb16[2];
-  {
-    const int q = r_lane & 15;
-    const int rw = 2 * (q & 3) + ((q >> 2) & 1) + 8 * ((q >> 3) & 1);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) hb16[mt] = ((mt * HH + (r_lane >> 4)) * HW + rw) * 16;
-  }
-  // halo pieces: row hv = 64 j + lane of the 4x4x18 halo; source offset relative to the box
-  // origin voxel, packed halo coordinates (-1: past the halo)
-  int prel[kSWvPieces], pco[kSWvPieces];
-#pragma unroll
-  for (int j = 0; j < kSWvPieces; ++j) {
-    const int hv = j * 64 + lane;
-    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-    prel[j] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
-    pco[j] = hv < kSWvHalo ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
-  }
-  const uint32_t ring = lds_addr(lds) + wave * 3 * kSWvSlot;
-  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
-    int q = b;
-    const int bwi = q % nbw; q /= nbw;
-    const int bhi = q % nbh; q /= nbh;
-    const int bdi = q % nbd;
-    n = q / nbd;
-    d0 = bdi * 2; h0 = bhi * 2; w0 = bwi * 16;
-  };
-  // exactly kSWvPieces DMA instructions per call (b >= nwb: all out of range -> zeros), so
-  // the vmcnt arithmetic below is the same for every iteration
-  auto stage = [&](int b, int slot) {
-    const uint32_t lb = __builtin_amdgcn_readfirstlane(ring + slot * kSWvSlot);
-    if (b >= nwb) {
-#pragma unroll
-      for (int j = 0; j < kSWvPieces; ++j) dma16(xr, lb + j * 1024, kOOB, 0);
-      return;
-    }
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-    const int base16 = (((n * D + d0) * H + h0) * W + w0) * 16;
-    const bool inner = d0 >= 1 && d0 + 2 < D && h0 >= 1 && h0 + 2 < H && w0 >= 1 && w0 + 16 < W;
-#pragma unroll
-    for (int j = 0; j < kSWvPieces; ++j) {
-      uint32_t voff = (uint32_t)(base16 + prel[j]);
-      const int c = pco[j];
-      if (c < 0) {
-        voff = kOOB;
-      } else if (!inner) {
-        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
-        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
-      }
-      dma16(xr, lb + j * 1024, voff, 0);
-    }
-  };
-
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2] = {0.f, 0.f};
-  float cnt = 0.f;
-  const uint32_t vlane = r_lane * 4 + hsel * 128;  // store voffset: channel pair + odd voxel
-  int b = lg * 8 + wave;
-  stage(b, 0);
-  stage(b + stride, 1);
-  for (int it = 0; b < nwb; b += stride, ++it) {
-    // this box's halo has landed (issued after it: DMA of the next box + the stores of the
-    // previous two; capped at the 6-bit counter)
-    if (it == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else if (it == 1) asm volatile("s_waitcnt vmcnt(37)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-    stage(b + 2 * stride, (it + 2) % 3);
-    const char* hl = lds + wave * 3 * kSWvSlot + (it % 3) * kSWvSlot;
-    f32x16_t acc[2][2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) { acc[mt][0][e] = bias0; acc[mt][1][e] = bias1; }
-    if (!(PCMS_ABL & 1)) {
-      int hs16 = hsel * 16;
-      asm volatile("" : "+v"(hs16));
-      auto load_a = [&](int st, s16x8_t (&a)[2]) {
-        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
-        const int off16 = o0 * 16 + hs16 * (o1 - o0);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + off16);
-      };
-      s16x8_t abuf[2][2];
-      load_a(0, abuf[0]);
-#pragma unroll
-      for (int st = 0; st < kStemSteps; ++st) {
-        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
-          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (it == 0) {
-      K[0] = __shfl(acc[0][0][0], r_lane, 64);
-      K[1] = __shfl(acc[0][1][0], r_lane, 64);
-    }
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-    const int bv = ((n * D + d0) * H + h0) * W + w0;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int gh = 0; gh < 2; ++gh) {
-        const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (mt * H + gh) * W) * 128u);
-#pragma unroll
-        for (int gl = 0; gl < 2; ++gl)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int e = (2 * gh + gl) * 4 + i;  // g = e >> 2: gh = g >> 1, gl = g & 1
-            const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-            if (!(PCMS_ABL & 2))
-              __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, vlane + (2 * i + 8 * gl) * 128, so, 0);
-            const float e0 = v0 - K[0], e1 = v1 - K[1];
-            s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
-            s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
-          }
-      }
-    cnt += 32.f;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (!stats) return;
-  // per wave: S = sum d + n K, M2 = sum d^2 - (sum d)^2 / n; Chan merge over the 8 waves
-  const float nw = 2.f * cnt;
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    s1[nt] += __shfl_xor(s1[nt], 32, 64);
-    s2[nt] += __shfl_xor(s2[nt], 32, 64);
-    if (hsel == 0) {
-      float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
-      rp[0] = s1[nt] + nw * K[nt];
-      rp[1] = nw > 0.f ? s2[nt] - s1[nt] * s1[nt] / nw : 0.f;
-      rp[2] = nw;
-    }
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float S = 0.f, Nn = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
-    const float m = Nn > 0.f ? S / Nn : 0.f;
-    float M2 = 0.f, sdd = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      const float c = red[(w * 64 + tid) * 3 + 2];
-      if (c > 0.f) {
-        const float d = red[(w * 64 + tid) * 3] / c - m;
-        M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
-        sdd += c * d;
-      }
-    }
-    if (Nn > 0.f) M2 -= sdd * sdd / Nn;
-    float* st = stats + ((long)blockIdx.x * 64 + tid) * 2;
-    st[0] = S;
-    st[1] = M2;
-    if (tid == 0) stats[(long)gridDim.x * 128 + blockIdx.x] = Nn;
-  }
-}
-
-// Stem weight gradient.  dW[co][c][t] = sum_v dy[v][co] * x[v + t][c], c < cin_w <= 8.
-// Output columns j = (t, c) = 8 t + c, 224 of them in 7 tiles of 32 (= 4 taps x 8 channels).
-// Wave w: both co tiles (64 co), column tiles {w, w + 4} (w < 3) or {3}.  Voxel boxes of
-// 256 are double-buffered through LDS (register-staged prefetch); one atomic flush per WG.
-constexpr int kSBV = 256;
-constexpr int kSHalo = 648;                         // (4+2)(4+2)(16+2) for the 4x4x16 box
-constexpr int kSBuf = kSBV * 128 + kSHalo * 16;     // dy tile (128 B rows) + halo (16 B rows)
-
-template <int LBD, int LBH, int LBW>
-__global__ void __launch_bounds__(256, 1) stem_wgrad_kernel(const bf16_t* x, const bf16_t* dy, float* dw,
-                                                            int N, int D, int H, int W, int cin_w,
-                                                            int lbd_r, int lbh_r, int lbw_r, int nbd, int nbh, int nbw,
-                                                            int nbox, int boxes_per_split) {
-  const int lbd = LBW >= 0 ? LBD : lbd_r, lbh = LBW >= 0 ? LBH : lbh_r, lbw = LBW >= 0 ? LBW : lbw_r;
-  extern __shared__ __attribute__((aligned(16))) char slds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hsel = lane >> 5;
-  const int bd = 1 << lbd, bh = 1 << lbh, bw = 1 << lbw;
-  const int HH = bh + 2, HW = bw + 2;
-  const int HV = (bd + 2) * HH * HW;
-  const int boxvol = bd * bh * bw;
-  const long plane = (long)H * W;
-  const int nj = (wave < 3) ? 2 : 1;
-  const int jt0 = wave, jt1 = wave + 4;
-  const int b_beg = blockIdx.x * boxes_per_split;
-  const int b_end = min(nbox, b_beg + boxes_per_split);
-  f32x16_t acc[2][2];  // [co tile][column tile slot]
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  constexpr int DYP = kSBV * 8;                      // 16-B pieces of the dy tile
-  constexpr int MAXP = (DYP + kSHalo + 255) / 256;  // per thread
-  u32x4_t stg[MAXP];
-  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
-    int bwi = b % nbw; b /= nbw;
-    int bhi = b % nbh; b /= nbh;
-    int bdi = b % nbd;
-    n = b / nbd;
-    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
-  };
-  auto stage_load = [&](int b) {
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-#pragma unroll
-    for (int i = 0; i < MAXP; ++i) {
-      const int pc = tid + i * 256;
-      u32x4_t v = {0u, 0u, 0u, 0u};
-      if (pc < DYP) {
-        const int r = pc >> 3, q = pc & 7;
-        if (r < boxvol) {
-          const int rd = r >> (lbh + lbw), rh = (r >> lbw) & (bh - 1), rw = r & (bw - 1);
-          const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
-          if (gd < D && gh < H && gw < W)
-            v = *reinterpret_cast<const u32x4_t*>(dy + (((long)n * D + gd) * plane + (long)gh * W + gw) * 64 + q * 8);
-        }
-      } else if (pc < DYP + HV) {
-        const int hv = pc - DYP;
-        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
-        if (gd >= 0 && gd < D && gh >= 0 && gh < H && gw >= 0 && gw < W)
-          v = *reinterpret_cast<const u32x4_t*>(x + (((long)n * D + gd) * plane + (long)gh * W + gw) * 8);
-      }
-      stg[i] = v;
-    }
-  };
-  auto stage_store = [&](char* buf) {
-#pragma unroll
-    for (int i = 0; i < MAXP; ++i) {
-      const int pc = tid + i * 256;
-      if (pc < DYP) {
-        const int r = pc >> 3, q = pc & 7;
-        *reinterpret_cast<u32x4_t*>(buf + dy_off_bf16(r, q * 8)) = stg[i];
-      } else if (pc < DYP + HV) {
-        *reinterpret_cast<u32x4_t*>(buf + kSBV * 128 + (pc - DYP) * 16) = stg[i];
-      }
-    }
-  };
-  auto halo_row = [&](int r) {
-    const int rd = r >> (lbh + lbw), rh = (r >> lbw) & (bh - 1), rw = r & (bw - 1);
-    return (rd * HH + rh) * HW + rw;
-  };
-  // per-lane column -> (tap, channel half) for the transposed B reads: in a 16-lane group
-  // lane 4q+p supplies row q and columns 4p..4p+3 of its 16-column block
-  const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-  auto compute = [&](const char* buf) {
-    const char* xb = buf + kSBV * 128;
-#pragma unroll 4
-    for (int k0 = 0; k0 < boxvol; k0 += 16) {
-      const int v_a = k0 + 8 * hsel + qq;
-      s16x8_t a[2];
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        const int co = ct * 32 + g * 16 + pp * 4;
-        s16x4_t lo = tr_read(buf, dy_off_bf16(v_a, co)), hi = tr_read(buf, dy_off_bf16(v_a + 4, co));
-        a[ct] = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      // with a compile-time box of width >= 16 the lane's rows share (rd, rh) with k0
-        const int hr0 = LBW >= 4 ? halo_row(k0) + 8 * hsel + qq : halo_row(v_a);
-        const int hr1 = LBW >= 4 ? hr0 + 4 : halo_row(v_a + 4);
-#pragma unroll
-      for (int js = 0; js < 2; ++js) {
-        if (js >= nj) break;
-        const int jt = js ? jt1 : jt0;
-        // column block of this lane group: 16 columns = taps 4 jt + 2 g, +1; lane: tap + (pp >> 1), ch 4 (pp & 1)
-        const int tap = 4 * jt + 2 * g + (pp >> 1);
-        const int off = tap_off(tap, HH, HW);
-        const int cb = (pp & 1) * 8;  // byte offset of channels 4..7
-        s16x4_t lo = tr_read(xb, (hr0 + off) * 16 + cb), hi = tr_read(xb, (hr1 + off) * 16 + cb);
-        s16x8_t bfr = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[ct][js] = mfma(a[ct], bfr, acc[ct][js]);
-      }
-    }
-  };
-  if (b_beg < b_end) {
-    stage_load(b_beg);
-    stage_store(slds);
-    __syncthreads();
-    for (int b = b_beg; b < b_end; ++b) {
-      const int cur = (b - b_beg) & 1;
-      if (b + 1 < b_end) stage_load(b + 1);
-      compute(slds + cur * kSBuf);
-      if (b + 1 < b_end) stage_store(slds + (cur ^ 1) * kSBuf);
-      __syncthreads();
-    }
-  }
-  // flush: C tile -> LDS [co][t][c] (fp32), then coalesced atomics into dw[co][c][t]
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(slds);  // 64 x 28 x 8 floats = 56 KiB
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-    for (int js = 0; js < 2; ++js) {
-      if (js >= nj) continue;
-      const int jt = js ? jt1 : jt0;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int co = ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
-        const int j = jt * 32 + (lane & 31);  // column = 8 t + c
-        red[co * 224 + j] = acc[ct][js][e];
-      }
-    }
-  __syncthreads();
-  const int total = 64 * cin_w * 27;
-  for (int i = tid; i < total; i += 256) {
-    const int t = i % 27, c = (i / 27) % cin_w, co = i / (27 * cin_w);
-    atomicAdd(dw + i, red[co * 224 + t * 8 + c]);
-  }
-}
-
-// Streaming stem weight gradient (the HBM-bound hot case: D % 4 == H % 4 == W % 16 == 0).
-// dW[co][c][t] = sum_v dy[v][co] x[v + t][c]: GEMM with M = 64 co, N = 224 (tap, channel)
-// columns, K = voxels.  Persistent: one 4-wave workgroup per CU walks 4x4x16 voxel boxes
-// b = blockIdx.x + k gridDim.x.  Each box's dy tile (256 voxels x 128 B) and x halo
-// (6x6x18 rows x 16 B) arrive by buffer LDS-DMA (inline asm, see dma16) into a 3-slot ring:
-// two boxes in flight while one computes, counted vmcnt + raw s_barrier, every source
-// offset a per-thread constant + the box base.  Wave w owns k-steps w, w + 4, w + 8, w + 12
-// of every box and ALL 14 output tiles (2 co x 7 column tiles, accumulators in AGPRs), so
-// each A / B fragment is read from LDS exactly once per box (ds_read_b64_tr_b16 transposes
-// both operands) and the next k-step's fragments are read during this one's 14 MFMAs.
-// Flush: one fp32 partial row [64][cin_w][27] per workgroup (plain stores), summed into dw
-// by stem_wgrad_reduce_kernel (deterministic, no atomics).
-constexpr int kSWT = 256;                                  // 4 waves, one per SIMD
-// BD = box depth (boxes BD x 4 x 16), NS = ring slots (NS - 1 boxes in flight).  The load
-// pipeline is latency-bound (bytes in flight per CU), so the product ring uses 2-deep boxes
-// in 6 slots (115 KB in flight) rather than 4-deep boxes in 3 slots (86 KB).
-template <int BD> struct SWGeom {
-  static constexpr int BV = BD * 64;                            // voxels per box
-  static constexpr int HV = (BD + 2) * 6 * 18;                  // halo rows (16 B)
-  static constexpr int HRows = (HV + 63) / 64 * 64;             // rows written
-  static constexpr int Buf = BV * 128 + HRows * 16;             // bytes per ring slot
-  static constexpr int DYP = BV * 8 / kSWT;                     // dy DMA pieces per thread
-  static constexpr int XI = (HRows / 64 + 3) / 4;               // halo DMA rounds per wave
-};
-constexpr int kSWBD = (PCMS_ABL & 4096) ? 2 : 4;  // 2-deep x 6 slots measured slower
-constexpr int kSWNS = kSWBD == 4 ? 3 : 6;
-constexpr int kSWLds = kSWNS * SWGeom<kSWBD>::Buf;
-static_assert(kSWLds >= 64 * 224 * 4, "flush tile fits in the ring");
-static_assert(kSWLds <= 160 * 1024, "ring fits in LDS");
-
-template <int BD, int NS>
-__global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t* x, const bf16_t* dy, float* part,
-                                                                    int N, int D, int H, int W, int cin_w,
-                                                                    uint32_t xbytes, uint32_t dybytes) {
-  typedef SWGeom<BD> Gm;
-  constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
-  constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
-  extern __shared__ __attribute__((aligned(16))) char swl[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hsel = lane >> 5;
-  const int nbw = W / BW, nbh = H / BH, nbd = D / BD;
-  const int nbox = N * nbd * nbh * nbw;
-  const i32x4_t xr = buffer_desc(x, xbytes);
-  const i32x4_t dr = buffer_desc(dy, dybytes);
-
-  // per-thread DMA source offsets relative to the box origin (constant over boxes)
-  uint32_t dyrel[Gm::DYP];
-#pragma unroll
-  for (int i = 0; i < Gm::DYP; ++i) {
-    const int pc = tid + i * kSWT;
-    const int r = pc >> 3, q = pc & 7;
-    const int ql = q ^ (((r >> 1) & 1) << 2);  // dy_off_bf16: 64-B halves swapped on odd row pairs
-    const int rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
-    dyrel[i] = (uint32_t)(((rd * H + rh) * W + rw) * 128 + ql * 16);
-  }
-  // halo pieces of this wave: rows wave*64 + lane + 256 i < HRows (XI or XI - 1 of them)
-  const int nxp = (Gm::HRows / 64 - wave + 3) / 4;
-  int xrel[Gm::XI], xco[Gm::XI];
-#pragma unroll
-  for (int i = 0; i < Gm::XI; ++i) {
-    const int hv = wave * 64 + lane + i * kSWT;
-    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-    xrel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
-    xco[i] = hv < kSWHV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
-  }
-  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
-    int q = b;
-    const int bwi = q % nbw; q /= nbw;
-    const int bhi = q % nbh; q /= nbh;
-    const int bdi = q % nbd;
-    n = q / nbd;
-    d0 = bdi * BD; h0 = bhi * BH; w0 = bwi * BW;
-  };
-  auto stage = [&](int b, int slot) {
-    int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
-    const int vb = ((n * D + d0) * H + h0) * W + w0;
-    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(swl) + slot * kSWBuf + wave * 64 * 16);
-    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)vb * 128u);
-#pragma unroll
-    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
-    const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
-#pragma unroll
-    for (int i = 0; i < Gm::XI; ++i) {
-      if (i >= nxp) break;
-      uint32_t voff = (uint32_t)(vb * 16 + xrel[i]);
-      const int c = xco[i];
-      if (c < 0) {
-        voff = kOOB;
-      } else if (!inner) {
-        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
-        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
-      }
-      dma16(xr, lb + kSWBV * 128 + i * kSWT * 16, voff, 0);
-    }
-  };
-
-  const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-  f32x16_t acc[2][7];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 7; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  // lane offsets of the tr reads, with the wave's k-step offset folded in (k-step s = wave +
-  // 4 i is box row (rd = i, rh = wave): dy rows at s * 2048, halo rows at (i HH + wave) HW)
-  const int aoff0 = dy_off_bf16(8 * hsel + qq, g * 16 + pp * 4) + wave * 2048;
-  const int aoff1 = dy_off_bf16(8 * hsel + qq, 32 + g * 16 + pp * 4) + wave * 2048;
-  int boff[7];  // column tile j: taps 4 j + 2 g + (pp >> 1), channels 4 (pp & 1) .. + 3
-#pragma unroll
-  for (int j = 0; j < 7; ++j)
-    boff[j] = kSWBV * 128 + (8 * hsel + qq + tap_off(4 * j + 2 * g + (pp >> 1), HH, HW) + wave * HW) * 16 + (pp & 1) * 8;
-  auto compute = [&](const char* buf) {
-    uint32_t pa0 = lds_addr(buf) + aoff0, pa1 = lds_addr(buf) + aoff1, pb[7];
-#pragma unroll
-    for (int j = 0; j < 7; ++j) pb[j] = lds_addr(buf) + boff[j];
-    asm volatile("" : "+v"(pa0), "+v"(pa1), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]),
-                 "+v"(pb[5]), "+v"(pb[6]));
-    auto tr = [](uint32_t p, int off) {
-      return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(uintptr_t)(p + off));
-    };
-    auto cat = [](s16x4_t lo, s16x4_t hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); };
-    auto load = [&](int i, s16x8_t (&a)[2], s16x8_t (&bq)[7]) {
-      const int dyb = i * 4 * 2048;
-      const int hrb = i * HH * HW * 16;
-      a[0] = cat(tr(pa0, dyb), tr(pa0, dyb + 512));
-      a[1] = cat(tr(pa1, dyb), tr(pa1, dyb + 512));
-#pragma unroll
-      for (int j = 0; j < 7; ++j) bq[j] = cat(tr(pb[j], hrb), tr(pb[j], hrb + 64));
-    };
-    s16x8_t a[2][2], bq[2][7];
-    load(0, a[0], bq[0]);
-#pragma unroll
-    for (int i = 0; i < BD; ++i) {
-      if (i + 1 < BD) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
-#pragma unroll
-      for (int j = 0; j < 7; ++j)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[ct][j] = mfma(a[i & 1][ct], bq[i & 1][j], acc[ct][j]);
-    }
-  };
-
-  const int G = gridDim.x;
-  int b = blockIdx.x;
-#pragma unroll
-  for (int k = 0; k < NS - 1; ++k)
-    if (b + k * G < nbox) stage(b + k * G, k);
-  for (int it = 0; b < nbox; b += G, ++it) {
-    // retire box b's DMA (the NS - 2 boxes after it may stay in flight), then barrier:
-    // every wave's share of box b has landed and every wave is done reading the slot
-    // refilled below
-    if (b + (NS - 2) * G < nbox) {
-      if (nxp == Gm::XI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI)) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI - 1)) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int b2 = b + (NS - 1) * G;
-    if (b2 < nbox) stage(b2, (it + NS - 1) % NS);
-    compute(swl + (it % NS) * kSWBuf);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // flush: the 4 waves' partial tiles summed in LDS [co][224 cols] (fixed order)
-  float* red = reinterpret_cast<float*>(swl);
-  for (int pass = 0; pass < 4; ++pass) {
-    if (wave == pass) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int j = 0; j < 7; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int co = ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
-            float* dst = red + co * 224 + j * 32 + (lane & 31);
-            if (pass == 0) *dst = acc[ct][j][e];
-            else *dst += acc[ct][j][e];
-          }
-    }
-    __syncthreads();
-  }
-  const int total = 64 * cin_w * 27;
-  float* prow = part + (long)blockIdx.x * total;
-  for (int i = tid; i < total; i += kSWT) {
-    const int t = i % 27, c = (i / 27) % cin_w, co = i / (27 * cin_w);
-    prow[i] = red[co * 224 + t * 8 + c];
-  }
-}
-
-// dw[o] += sum over the workgroup partial rows (fixed order).  Block = 32 outputs x 8 row
-// groups: 32 independent 128-B row segments in flight per thread group, LDS combine.
-__global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* part, int rows, int total, float* dw) {
-  __shared__ float red[8][32];
-  const int ol = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int o = blockIdx.x * 32 + ol;
-  float s = 0.f;
-  if (o < total) {
-#pragma unroll 8
-    for (int r = rg; r < rows; r += 8) s += part[(long)r * total + o];
-  }
-  red[rg][ol] = s;
-  __syncthreads();
-  if (rg == 0 && o < total) {
-    float t = 0.f;
-#pragma unroll
-    for (int g2 = 0; g2 < 8; ++g2) t += red[g2][ol];
-    dw[o] += t;
-  }
-}
-
 // ------------------------------------------------------------------------------------
 // Big-box forward / dgrad (bf16; the level-0/1 hot case: D % 8 == H % 8 == 0, W % 16 == 0,
 // input channels in 16-channel chunks).  One 4-wave workgroup per CU computes an
@@ -2204,7 +903,7 @@ template <int BD> struct BgGeom {
   static constexpr int Dist = BD == 8 ? 8 : 2;  // B prefetch distance (taps); (Dist + 1) | 27
   static_assert(27 % (Dist + 1) == 0, "B ring index must continue across chunks");
 };
-constexpr int kBgBD = (PCMS_ABL & 1024) ? 4 : 8;  // product box depth (depth 4 measured slower)
+constexpr int kBgBD = 8;  // box depth (depth 4 with 2 workgroups per CU measured slower)
 
 // hidden 16-B global load (the compiler's waitcnt pass does not count it): retired by
 // vm_wait2<N>, which also orders the register's readers after the wait
@@ -2347,18 +1046,13 @@ __global__ void __launch_bounds__(kBgThreads, BgGeom<BD>::PerCU) conv3_fwd_big_k
     static_for<27>([&](auto tc) {
       constexpr int tap = decltype(tc)::value;
       constexpr int tn = tap + Gm::Dist;
-      if constexpr (!(PCMS_ABL & 64)) {
-        if constexpr (tn < 27) load_b(bset[tn % (Gm::Dist + 1)], chunk, tn);
-        else load_b(bset[tn % (Gm::Dist + 1)], chunk + 1, tn - 27);
-      }
-      if constexpr (tap < Gm::Pieces && !(PCMS_ABL & 32)) stage_piece(chunk + 1, buf ^ 1, tap, more);
+      if constexpr (tn < 27) load_b(bset[tn % (Gm::Dist + 1)], chunk, tn);
+      else load_b(bset[tn % (Gm::Dist + 1)], chunk + 1, tn - 27);
+      if constexpr (tap < Gm::Pieces) stage_piece(chunk + 1, buf ^ 1, tap, more);
       constexpr int cur = tap & 1;
-      if constexpr (tap + 1 < 27) {
-        if constexpr (!(PCMS_ABL & 256)) read_a(a[cur ^ 1], tap + 1);
-        else if constexpr (tap == 0) read_a(a[1], 1);
-      }
+      if constexpr (tap + 1 < 27) read_a(a[cur ^ 1], tap + 1);
       s16x8_t(&b)[2] = bset[tap % (Gm::Dist + 1)];
-      if constexpr (!(PCMS_ABL & 128)) vm_wait2<bg_wait<Gm::Pieces, Gm::Dist>(tap)>(b[0], b[1]);
+      vm_wait2<bg_wait<Gm::Pieces, Gm::Dist>(tap)>(b[0], b[1]);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -2394,7 +1088,7 @@ __global__ void __launch_bounds__(kBgThreads, BgGeom<BD>::PerCU) conv3_fwd_big_k
       const int rd = (BD / 4) * wave + (mt >> 2), rh = 2 * (mt & 3);
       const long vox = vrow + (long)rd * plane + (long)rh * p.W;
       const float v0 = acc[mt][0][e] + bias0, v1 = acc[mt][1][e] + bias1;
-      if (!(PCMS_ABL & 512)) *reinterpret_cast<uint32_t*>(yb + vox * ys + yc) = pack_bf16x2(v0, v1);
+      *reinterpret_cast<uint32_t*>(yb + vox * ys + yc) = pack_bf16x2(v0, v1);
       s1[0] += v0;
       s1[1] += v1;
     }
@@ -2520,8 +1214,18 @@ int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int
   PCMS_CHECK_LAUNCH();
 }
 
-// Forward (or dgrad) 3x3x3 conv. See Conv3Params.  splits > 1: fp32 atomic accumulate
-// into yacc (caller zeroes it; bias/stats/conversion then done by pcms_conv3_split_epilogue).
+// Input-channel splits a split-K launch with `splits` requested actually uses (whole
+// chunks per split): the slab count of yacc and of pcms_split_epilogue.
+int pcms_conv3_splits(int dtype, int Cin, int splits) {
+  const int nchunk = cdiv(Cin, pcms_conv3_chunk(dtype));
+  splits = std::max(1, std::min(splits, nchunk));
+  return cdiv(nchunk, cdiv(nchunk, splits));
+}
+
+// Forward (or dgrad) 3x3x3 conv. See Conv3Params.  splits > 1: every split writes its fp32
+// partial sums into its own slab of yacc [splits][N*D*H*W][Cout] (plain stores, no zeroing
+// needed); pcms_split_epilogue then sums the slabs in split order (deterministic), adds the
+// bias, converts, and forms the BN statistics.
 int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
                    float* yacc, float* stats, int accumulate,
@@ -2540,6 +1244,7 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   p.yacc = splits > 1 ? yacc : nullptr;
   p.stats = stats; p.accumulate = accumulate;
   p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
+  p.nvox = (long)N * D * H * W;
   p.nchunk = cdiv(Cin, CK);
   if (splits < 1) splits = 1;
   if (splits > p.nchunk) splits = p.nchunk;
@@ -2571,154 +1276,6 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
 }
 
 
-// ---- stem (inc.conv.0), bf16: dedicated HBM-bound kernels ----
-int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s) {
-  if (cin_w > 8) return -1;
-  hipLaunchKernelGGL(stem_pack_kernel, dim3(cdiv(kStemSteps * 64 * 16, 256)), dim3(256), 0, s, w, (bf16_t*)out, cin_w);
-  PCMS_CHECK_LAUNCH();
-}
-int pcms_stem_pack_elems(void) { return kStemSteps * 64 * 16; }
-
-static int device_cus();
-// the wave-independent stem forward measured slower than the direct kernel (110 vs 97 us at
-// config 2): kept for tuning behind an ablation switch
-static bool stem_fwd_wave_shape(int N, int D, int H, int W) {
-  return (PCMS_ABL & 2048) && D % 2 == 0 && H % 2 == 0 && W % 16 == 0 && (long)N * D * H * W * 128 < (long)kOOB;
-}
-static int stem_fwd_wave_grid(int N, int D, int H, int W) {
-  const long nwb = (long)N * (D / 2) * (H / 2) * (W / 16);
-  return (int)std::max(1L, std::min((long)device_cus(), (nwb + 7) / 8));
-}
-
-// BatchNorm statistics rows pcms_stem_fwd writes
-int pcms_stem_fwd_rows(int N, int D, int H, int W) {
-  if (stem_fwd_wave_shape(N, D, H, W)) return stem_fwd_wave_grid(N, D, H, W);
-  return pcms_conv3_mblocks(N, D, H, W);
-}
-
-// x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_stem_fwd_rows
-int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
-                  int N, int D, int H, int W, hipStream_t s) {
-  Box b = fwd_box(D, H, W);
-  Conv3Params p;
-  p.x0 = x; p.x1 = nullptr; p.c0 = 8; p.c1 = 0;
-  p.w = wpack; p.bias = bias; p.y0 = y; p.y1 = nullptr; p.cy0 = 64;
-  p.yacc = nullptr; p.stats = stats; p.accumulate = 0;
-  p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = 8; p.Cout = 64;
-  p.nchunk = 1; p.chunks_per_split = 1;
-  p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
-  p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
-  const int nbox = N * p.nbd * p.nbh * p.nbw;
-  if ((1 << (b.lbd + b.lbh + b.lbw)) > 512) return -5;
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
-  const long xbytes = (long)N * D * H * W * 16, ybytes = (long)N * D * H * W * 128;
-  if (stem_fwd_wave_shape(N, D, H, W)) {
-    const int grid = stem_fwd_wave_grid(N, D, H, W);
-    (void)hipFuncSetAttribute((const void*)stem_fwd_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kSWvLds);
-    hipLaunchKernelGGL(stem_fwd_wave_kernel, dim3(grid), dim3(kSWvThreads), kSWvLds, s, (const bf16_t*)x,
-                       (const bf16_t*)wpack, bias, (bf16_t*)y, stats, N, D, H, W, (uint32_t)xbytes, (uint32_t)ybytes);
-    PCMS_CHECK_LAUNCH();
-  }
-  const bool direct = b.lbw == 4 && b.lbd + b.lbh == 5 && (b.lbd == 2 || b.lbd == 3) && ybytes < (long)kOOB;
-  if (direct) {
-    const int grid = std::min(nbox, ncu);
-    // store-pipelined variant unless PCMS_STEM_FWD_PIPE=0 (A/B switch for the measurements)
-    // 0: plain stores after the MFMAs; 1: store-pipelined, 8 waves; 2: store-pipelined,
-    // one 4-wave workgroup per CU (512 registers per wave)
-    static const int pipe = [] { const char* e = getenv("PCMS_STEM_FWD_PIPE"); return e ? atoi(e) : 0; }();
-    auto kern = b.lbd == 2 ? (pipe == 1 ? stem_fwd_direct_kernel<2, 3, 512, true> : stem_fwd_direct_kernel<2, 3, 512>)
-                           : (pipe == 1 ? stem_fwd_direct_kernel<3, 2, 512, true> : stem_fwd_direct_kernel<3, 2, 512>);
-    int g2 = grid;
-    int thr = kSDThr;
-    if (pipe == 2) {  // 4x4x16 boxes, one 4-wave workgroup per CU
-      p.lbd = 2; p.lbh = 2;
-      p.nbd = cdiv(D, 4); p.nbh = cdiv(H, 4);
-      g2 = std::min(std::min(p.N * p.nbd * p.nbh * p.nbw, ncu), nbox);
-      kern = stem_fwd_direct_kernel<2, 2, 256, true>;
-      thr = 256;
-    } else if (kSDThr == 256) {  // 4x4x16 boxes, two workgroups per CU; rows stay <= the caller's
-      p.lbd = 2; p.lbh = 2;
-      p.nbd = cdiv(D, 4); p.nbh = cdiv(H, 4);
-      g2 = std::min(std::min(p.N * p.nbd * p.nbh * p.nbw, 2 * ncu), nbox);
-      kern = stem_fwd_direct_kernel<2, 2, 256>;
-    }
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSDLds);
-    hipLaunchKernelGGL(kern, dim3(g2), dim3(thr), kSDLds, s, p, thr == 256 ? p.N * p.nbd * p.nbh * p.nbw : nbox,
-                       nbox, (uint32_t)xbytes,
-                       (uint32_t)ybytes);
-    PCMS_CHECK_LAUNCH();
-  }
-  if (b.lbd == 2 && b.lbh == 3 && b.lbw == 4) {
-    (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<2, 3, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kStemLds);
-    hipLaunchKernelGGL((stem_fwd_kernel<2, 3, 4>), dim3(std::min(nbox, ncu)), dim3(kStemThreads), kStemLds, s, p, nbox);
-  } else {
-    (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<-1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, kStemLds);
-    hipLaunchKernelGGL((stem_fwd_kernel<-1, -1, -1>), dim3(std::min(nbox, ncu)), dim3(kStemThreads), kStemLds, s, p, nbox);
-  }
-  PCMS_CHECK_LAUNCH();
-}
-
-static int device_cus() {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
-  return ncu;
-}
-
-static bool stem_wgrad_streams(int N, int D, int H, int W) {
-  return D % kSWBD == 0 && H % 4 == 0 && W % 16 == 0 && (long)N * D * H * W * 128 < (1L << 31);
-}
-
-// fp32 workspace floats pcms_stem_wgrad needs (0: none)
-int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w) {
-  if (!stem_wgrad_streams(N, D, H, W)) return 0;
-  const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
-  return std::min(nbox, device_cus()) * 64 * cin_w * 27;
-}
-
-// dw [64][cin_w][27] fp32 += stem weight gradient (x: 8-channel bf16 input, dy: 64 ch);
-// ws: pcms_stem_wgrad_ws_floats(...) floats
-int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H, int W,
-                    int target_wgs, hipStream_t s) {
-  if (cin_w > 8 || cin_w < 1) return -1;
-  if (stem_wgrad_streams(N, D, H, W)) {
-    if (ws == nullptr) return -2;
-    const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
-    const int grid = std::min(nbox, device_cus());
-    const long xbytes = (long)N * D * H * W * 16, dybytes = (long)N * D * H * W * 128;
-    auto kern = stem_wgrad_stream_kernel<kSWBD, kSWNS>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSWLds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT), kSWLds, s, (const bf16_t*)x,
-                       (const bf16_t*)dy, ws, N, D, H, W, cin_w, (uint32_t)xbytes, (uint32_t)dybytes);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
-    const int total = 64 * cin_w * 27;
-    hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, (const float*)ws, grid,
-                       total, dw);
-    PCMS_CHECK_LAUNCH();
-  }
-  Box b = choose_box(D, H, W, kSBV, kSHalo, 4, 16);
-  const int nbd = cdiv(D, 1 << b.lbd), nbh = cdiv(H, 1 << b.lbh), nbw = cdiv(W, 1 << b.lbw);
-  const int nbox = N * nbd * nbh * nbw;
-  if (target_wgs <= 0) target_wgs = 256;
-  int splits = std::max(1, std::min(nbox, target_wgs));
-  const int bps = cdiv(nbox, splits);
-  splits = cdiv(nbox, bps);
-  const size_t lds = 2 * (size_t)kSBuf;
-  auto kern = (b.lbd == 2 && b.lbh == 2 && b.lbw == 4) ? stem_wgrad_kernel<2, 2, 4> : stem_wgrad_kernel<-1, -1, -1>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(splits), dim3(256), lds, s, (const bf16_t*)x, (const bf16_t*)dy, dw,
-                     N, D, H, W, cin_w, b.lbd, b.lbh, b.lbw, nbd, nbh, nbw, nbox, bps);
-  PCMS_CHECK_LAUNCH();
-}
 
 // Weight-gradient launch plan: box geometry, boxes per split, split count (shared by the
 // launch and its workspace query)
@@ -2772,7 +1329,7 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   p.nci = cdiv(Cin, 32);
   p.dw = dw;
   p.cw = cin_w;
-  p.direct = splits == 1 && dtype == PCMS_BF16 && !(PCMS_ABL & 16384);
+  p.direct = splits == 1 && dtype == PCMS_BF16;
   dim3 grid(splits * p.nco * p.nci);
   size_t lds;
   if (dtype == PCMS_BF16) {

@@ -1,0 +1,144 @@
+// Device helpers shared by the 3x3x3 convolution kernels (conv3.hip, stem.hip), gfx950.
+#pragma once
+#include "common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kRowBytes = 64;      // one halo row = one LDS row of the current ci-chunk
+constexpr int kHaloMax = 1152;     // halo voxels per workgroup (72 KiB LDS, 2 WG / CU)
+
+__device__ __attribute__((aligned(16))) uint32_t g_zero16[4];  // zero page for LDS-DMA padding
+constexpr uint32_t kOOB = 0x80000000u;  // buffer voffset past num_records: reads zeros
+
+template <typename T> struct Traits;
+template <> struct Traits<bf16_t> {
+  static constexpr int CK = 32;    // channels per chunk (64 B rows)
+  static constexpr int KS = 2;     // MFMA k-steps per chunk and tap (K = 16 each)
+  static constexpr int VEC = 8;    // elements per 16-byte piece
+  typedef s16x8_t Frag;
+};
+template <> struct Traits<float> {
+  static constexpr int CK = 16;
+  static constexpr int KS = 8;     // K = 2 each
+  static constexpr int VEC = 4;
+  typedef float Frag;
+};
+
+__device__ __forceinline__ f32x16_t mfma(s16x8_t a, s16x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16_t mfma(float a, float b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// 16-byte slot swizzle inside a 64-byte halo row (spreads ds_read_b128 lane groups).
+__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+
+// MFMA row -> box voxel permutation inside a 32-row M-tile.  ds_read_b128 serves a wave in
+// the lane groups G0 = {0-3, 12-15, 20-27} and G1 = {4-11, 16-19, 28-31} (and +32).  With
+// 16-voxel w-runs (box width 16) G0 reads 16 consecutive halo rows of one h-row and G1 16 of
+// the next, so with swz() every group covers all 64 banks exactly once, for every tap.
+__device__ __forceinline__ int perm32(int r) {
+  if (r < 4) return r;
+  if (r < 12) return 16 + (r - 4);
+  if (r < 16) return 4 + (r - 12);
+  if (r < 20) return 24 + (r - 16);
+  if (r < 28) return 8 + (r - 20);
+  return 28 + (r - 28);
+}
+
+// A fragment from the halo tile. ks = k-step inside the chunk, h = lane >> 5.
+__device__ __forceinline__ s16x8_t lds_a(const char* lds, int row, int ks, int h, bf16_t*) {
+  int slot = (ks * 2 + h) ^ swz(row);
+  return *reinterpret_cast<const s16x8_t*>(lds + row * kRowBytes + slot * 16);
+}
+__device__ __forceinline__ float lds_a(const char* lds, int row, int ks, int h, float*) {
+  int c = ks * 2 + h;  // channel in chunk (0..15)
+  int slot = (c >> 2) ^ swz(row);
+  return *reinterpret_cast<const float*>(lds + row * kRowBytes + slot * 16 + (c & 3) * 4);
+}
+// B fragment (weights) straight from global: packed [chunk][27][Cout][CK].
+__device__ __forceinline__ s16x8_t gl_b(const bf16_t* wrow, int ks, int h) {
+  return *reinterpret_cast<const s16x8_t*>(wrow + ks * 16 + h * 8);
+}
+__device__ __forceinline__ float gl_b(const float* wrow, int ks, int h) { return wrow[ks * 2 + h]; }
+
+struct Conv3Params {
+  const void* x0; const void* x1; int c0; int c1;
+  const void* w; const float* bias;
+  void* y0; void* y1; int cy0;
+  float* yacc; float* stats;
+  int accumulate;
+  int N, D, H, W, Cin, Cout;
+  int nchunk, chunks_per_split;
+  long nvox;             // N * D * H * W (split-K slab stride, in voxels)
+  int lbd, lbh, lbw, nbd, nbh, nbw;
+};
+
+// dy tile: 128-B (bf16) rows, 64-B halves swizzled by row bit 1 (conflict-free tr reads).
+__device__ __forceinline__ int dy_off_bf16(int v, int co) {  // co in 0..63 (element)
+  int half = (co >> 5) ^ ((v >> 1) & 1);
+  return v * 128 + half * 64 + (co & 31) * 2;
+}
+
+__device__ __forceinline__ s16x4_t tr_read(const char* lds, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + byte_off));
+}
+
+struct Box { int lbd, lbh, lbw; };
+
+int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
+
+// Pick a power-of-two box (<= maxvol voxels, halo <= maxhalo rows) minimising padded
+// volume (then maximising box size) for a D x H x W grid.
+Box choose_box(int D, int H, int W, int maxvol, int maxhalo, int minw, int minvol) {
+  Box best{3, 3, 3};  // (8,8,8): always valid (vol 512, halo 1000) -- overwritten below
+  double best_cost = 1e30;
+  for (int a = 0; a <= 4; ++a)
+    for (int b = 0; b <= 5; ++b)
+      for (int c = 0; c <= 6; ++c) {
+        const int bd = 1 << a, bh = 1 << b, bw = 1 << c;
+        if (bd * bh * bw > maxvol || bd * bh * bw < minvol) continue;
+        if ((bd + 2) * (bh + 2) * (bw + 2) > maxhalo) continue;
+        if (bw < minw && bw < W) continue;
+        const double padded = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh * cdiv(W, bw) * bw;
+        const double halo = (double)cdiv(D, bd) * cdiv(H, bh) * cdiv(W, bw) * (bd + 2) * (bh + 2) * (bw + 2);
+        const double cost = padded + 0.15 * halo;
+        if (cost < best_cost - 1e-9) { best_cost = cost; best = Box{a, b, c}; }
+      }
+  return best;
+}
+
+// Forward/dgrad box: 512 voxels; width 16 whenever the grid is that wide (perm32 layout).
+Box fwd_box(int D, int H, int W) {
+  if (W >= 16) {
+    Box best{0, 0, 4};
+    double bc = 1e30;
+    for (int a = 0; a <= 5; ++a) {
+      const int b = 5 - a;  // bd * bh = 32
+      const int bd = 1 << a, bh = 1 << b;
+      if ((bd + 2) * (bh + 2) * 18 > kHaloMax) continue;
+      const double cost = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh +
+                          0.15 * cdiv(D, bd) * cdiv(H, bh) * (bd + 2) * (bh + 2) * 18 / 16.0;
+      if (cost < bc - 1e-9 || (cost < bc + 1e-9 && a == 2)) { bc = cost; best = Box{a, b, 4}; }
+    }
+    return best;
+  }
+  return choose_box(D, H, W, 512, kHaloMax, 4, 32);
+}
+
+// compute units of the current device (persistent-grid sizing)
+inline int device_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
+
+}  // namespace

@@ -280,9 +280,10 @@ __global__ void maxpool_bwd_kernel(const T* a, const T* dp, T* da, int N, int D,
 
 // ---------------- sum over a sub-box of an NDHWC tensor (ConvT bias grad) ----------
 // Block: 256 threads = (256 / CG) voxel lanes x CG groups of VEC channels; 16-byte loads,
-// LDS reduce over voxel lanes, one atomic per channel per block.
+// LDS reduce over voxel lanes, one partial row [C] per block (summed in block order by
+// rows_sum_kernel: no atomics, run-to-run reproducible).
 template <typename T>
-__global__ void __launch_bounds__(TPB) box_channel_sum_kernel(const T* x, float* out, int N, int D, int H, int W,
+__global__ void __launch_bounds__(TPB) box_channel_sum_kernel(const T* x, float* part, int N, int D, int H, int W,
                                                               int C, int z0, int y0, int x0, int bd, int bh, int bw) {
   constexpr int VEC = Elem<T>::kVec;
   __shared__ float red[TPB * VEC];
@@ -308,8 +309,33 @@ __global__ void __launch_bounds__(TPB) box_channel_sum_kernel(const T* x, float*
   for (int c = threadIdx.x; c < C; c += TPB) {
     float s = 0.f;
     for (int l = 0; l < VL; ++l) s += red[l * C + c];
-    atomicAdd(out + c, s);
+    part[(long)blockIdx.x * C + c] = s;
   }
+}
+
+// out[c] += sum_r part[r][c] in a fixed order (deterministic).  Block = 8 columns x 32 row
+// lanes: lane l sums rows l, l + 32, ... (4 independent chains); the 32 lane sums are
+// added by a fixed LDS tree.
+__global__ void __launch_bounds__(256) rows_sum_kernel(const float* part, int rows, int C, float* out) {
+  __shared__ float red[32][9];
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int r = rl;
+    for (; r + 96 < rows; r += 128) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += part[(long)(r + 32 * j) * C + c];
+    }
+    for (int j = 0; r < rows; r += 32, ++j) s[j & 3] += part[(long)r * C + c];
+  }
+  red[rl][cl] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  for (int w = 16; w > 0; w >>= 1) {
+    if (rl < w) red[rl][cl] += red[rl + w][cl];
+    __syncthreads();
+  }
+  if (rl == 0 && c < C) out[c] += red[0][cl];
 }
 
 // ---------------- output head: logits (NCDHW fp32) = b + a . w ----------------
@@ -341,11 +367,11 @@ __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, floa
   }
 }
 
-// da[v, c] = sum_k dl[k, v] w[k, c]  (written);  dw[k, c] += sum_v dl a;  db[k] += sum_v dl
+// da[v, c] = sum_k dl[k, v] w[k, c]  (written);  per-block partials of dw[k, c] = sum_v dl a,
+// db[k] = sum_v dl
 template <typename T>
 __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* dlogits, const float* w,
-                                                       T* da, float* dw, float* db, long nvox_per_n,
-                                                       int N, int ncls) {
+                                                       T* da, float* part, long nvox_per_n, int N, int ncls) {
   __shared__ float red[TPB / 64][4][65];
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -385,13 +411,23 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
     if (lane == 0) red[wave][k][64] = sb;
   }
   __syncthreads();
+  // this block's partial row [ncls][65] (dw row k, then db[k]); rows_sum_kernel adds the
+  // rows in block order
   for (int idx = threadIdx.x; idx < ncls * 65 && idx < 4 * 65; idx += TPB) {
     const int k = idx / 65, c = idx % 65;
     float s = 0.f;
     for (int wv = 0; wv < TPB / 64; ++wv) s += red[wv][k][c];
-    if (c < 64) atomicAdd(dw + k * 64 + c, s);
-    else atomicAdd(db + k, s);
+    part[(long)blockIdx.x * ncls * 65 + idx] = s;
   }
+}
+
+// dw[k][c] += col (k, c), db[k] += col (k, 64) of the summed head partial rows
+__global__ void head_bwd_finish_kernel(const float* sums, int ncls, float* dw, float* db) {
+  const int idx = threadIdx.x;
+  if (idx >= ncls * 65) return;
+  const int k = idx / 65, c = idx % 65;
+  if (c < 64) dw[k * 64 + c] += sums[idx];
+  else db[k] += sums[idx];
 }
 
 // ---------------- losses ----------------
@@ -457,11 +493,18 @@ __global__ void loss_bwd_kernel(const float* x, const float* t, long M, const do
 }
 
 // ---------------- Adam (torch.optim.Adam, foreach, coupled weight decay) ----------
-__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n, float step_size, float b1,
-                            float b2, float eps, float wd, float bc2_sqrt, float gscale) {
+// g_eff = g * s, s = gscale * (*gmul if gmul) (the data-parallel 1/world mean, the gradient-
+// clip coefficient, the AMP unscale); when s != 1 the scaled gradient is also written back,
+// so param.grad afterwards holds what torch's clip_grad_norm_ / DDP mean would leave there.
+__global__ void adam_kernel(float* p, float* g, float* m, float* v, long n, float step_size, float b1,
+                            float b2, float eps, float wd, float bc2_sqrt, float gscale, const float* gmul) {
+  const float s = gmul ? gscale * gmul[0] : gscale;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float gi = g[i];
-    if (gscale != 1.f) gi *= gscale;   // data-parallel mean of summed gradients
+    if (s != 1.f) {
+      gi *= s;
+      g[i] = gi;
+    }
     const float pi = p[i];
     if (wd != 0.f) gi = gi + wd * pi;
     float mi = m[i];
@@ -474,10 +517,61 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n
   }
 }
 
-// fp32 split-K accumulator -> + bias, store T, BN partial sums; 64 voxels per block row
+// ---------------- global gradient norm / clip (torch.nn.utils.clip_grad_norm_) ----------
+// pass 1: per-block fp64 partial sums of g^2 (fp32 squares), one row per block
+constexpr int kNormBlocks = 1024;
+__global__ void __launch_bounds__(TPB) sumsq_kernel(const float* g, long n, double* part) {
+  __shared__ double red[TPB / 64];
+  double s = 0.0;
+  const long n4 = n / 4;
+  const f32x4_t* g4 = reinterpret_cast<const f32x4_t*>(g);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const f32x4_t v = g4[i];
+    s += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+  }
+  if (blockIdx.x == 0)
+    for (long i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += (double)(g[i] * g[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < TPB / 64; ++w) t += red[w];
+    part[blockIdx.x] = t;
+  }
+}
+// pass 2 (one block): norm = gscale * sqrt(sum of rows, in row order); mul = gscale *
+// min(1, max_norm / (norm + 1e-6)) (clip_grad_norm_'s clamped coefficient; max_norm <= 0:
+// no clipping, mul = gscale)
+__global__ void clip_finalize_kernel(const double* part, int rows, float gscale, float max_norm, float* norm_out,
+                                     float* mul_out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int r = threadIdx.x; r < rows; r += 256) s += part[r];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 256; ++i) t += red[i];
+    const float norm = (float)sqrt(t) * gscale;
+    float coef = 1.f;
+    if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+    if (norm_out) norm_out[0] = norm;
+    if (mul_out) mul_out[0] = gscale * coef;
+  }
+}
+// g *= *mul (in place)
+__global__ void scale_kernel(float* g, long n, const float* mul) {
+  const float s = mul[0];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) g[i] *= s;
+}
+
+// fp32 split-K slabs [splits][nvox][C] -> sum in split order + bias, store T, BN partial
+// sums; 64 voxels per block row
 template <typename T>
-__global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, const float* bias, T* y0, T* y1,
-                                                             int cy0, float* stats, int C, long nvox) {
+__global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, int splits, const float* bias, T* y0,
+                                                             T* y1, int cy0, float* stats, int C, long nvox) {
   // stats row = (sum, M2 about the row mean), count row after the [rows][C][2] block
   constexpr int NV = TPB / 64, KPT = 64 / NV;
   __shared__ float red[NV][64][3];
@@ -493,7 +587,9 @@ __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, c
     const long v = v0 + vl + i * NV;
     xs[i] = 0.f;
     if (v >= nvox) continue;
-    const float x = acc[v * C + c] + bc;
+    float x = acc[v * C + c];  // the split slabs in split order: a fixed summation order
+    for (int sp = 1; sp < splits; ++sp) x += acc[((long)sp * nvox + v) * C + c];
+    x += bc;
     T* dst = c < cy0 ? y0 + v * cy0 + c : y1 + v * (C - cy0) + (c - cy0);
     Elem<T>::st(dst, x);
     xs[i] = x;
@@ -647,16 +743,27 @@ int pcms_maxpool_bwd(int dtype, const void* a, const void* dp, void* da, int N, 
   PCMS_CHECK_LAUNCH();
 }
 
-int pcms_box_channel_sum(int dtype, const void* x, float* out, int N, int D, int H, int W, int C,
+static int box_sum_rows(int dtype, int N, int C, int bd, int bh, int bw) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  const int VL = TPB / (C / VEC);
+  return grid_for((long)N * bd * bh * bw, VL * 8, 1024);
+}
+int pcms_box_channel_sum_ws_floats(int dtype, int N, int C, int bd, int bh, int bw) {
+  return box_sum_rows(dtype, N, C, bd, bh, bw) * C;
+}
+
+int pcms_box_channel_sum(int dtype, const void* x, float* out, float* ws, int N, int D, int H, int W, int C,
                          int z0, int y0, int x0, int bd, int bh, int bw, hipStream_t s) {
   if ((long)N * D * H * W >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || TPB % (C / VEC)) return -1;
-  const long nv = (long)N * bd * bh * bw;
-  const int VL = TPB / (C / VEC);
-  const int grid = grid_for(nv, VL * 8, 1024);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(box_channel_sum_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)x, out, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
-  else hipLaunchKernelGGL(box_channel_sum_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)x, out, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
+  if (ws == nullptr) return -2;
+  const int grid = box_sum_rows(dtype, N, C, bd, bh, bw);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(box_channel_sum_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)x, ws, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
+  else hipLaunchKernelGGL(box_channel_sum_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)x, ws, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rows_sum_kernel, dim3(cdiv(C, 8)), dim3(256), 0, s, (const float*)ws, grid, C, out);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -669,13 +776,28 @@ int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, floa
   PCMS_CHECK_LAUNCH();
 }
 
+static int head_bwd_rows(long nvox) { return grid_for(nvox * 8, TPB, 2048); }
+// workspace: the per-block partial rows + one summed row
+int pcms_head_bwd_ws_floats(long nvox_per_n, int N, int ncls) {
+  return (head_bwd_rows((long)N * nvox_per_n) + 1) * ncls * 65;
+}
+
 int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w, void* da, float* dw, float* db,
-                  long nvox_per_n, int N, int ncls, hipStream_t s) {
+                  float* ws, long nvox_per_n, int N, int ncls, hipStream_t s) {
   if ((long)N * nvox_per_n >= (1L << 31)) return -7;  // 32-bit index math in the kernel
-  if (ncls > 4) return -1;
-  const int grid = grid_for((long)N * nvox_per_n * 8, TPB, 2048);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, dw, db, nvox_per_n, N, ncls);
-  else hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, dlogits, w, (float*)da, dw, db, nvox_per_n, N, ncls);
+  if (ncls > 4 || ncls < 1) return -1;
+  if (ws == nullptr) return -2;
+  const int grid = head_bwd_rows((long)N * nvox_per_n);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, ws, nvox_per_n, N, ncls);
+  else hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, dlogits, w, (float*)da, ws, nvox_per_n, N, ncls);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  float* sums = ws + (long)grid * ncls * 65;
+  (void)hipMemsetAsync(sums, 0, sizeof(float) * ncls * 65, s);
+  hipLaunchKernelGGL(rows_sum_kernel, dim3(cdiv(ncls * 65, 8)), dim3(256), 0, s, (const float*)ws, grid, ncls * 65, sums);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(head_bwd_finish_kernel, dim3(1), dim3(320), 0, s, (const float*)sums, ncls, dw, db);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -699,21 +821,38 @@ int pcms_loss_bwd(const float* x, const float* t, long M, const double* sums, fl
 }
 
 // step_size = lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)  (host fp64 -> fp32)
-int pcms_adam(float* p, const float* g, float* m, float* v, long n, float step_size, float b1, float b2, float eps,
-              float wd, float bc2_sqrt, float gscale, hipStream_t s) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, TPB, 16384)), dim3(TPB), 0, s, p, g, m, v, n, step_size, b1, b2, eps, wd, bc2_sqrt, gscale);
+int pcms_adam(float* p, float* g, float* m, float* v, long n, float step_size, float b1, float b2, float eps,
+              float wd, float bc2_sqrt, float gscale, const float* gmul, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, TPB, 16384)), dim3(TPB), 0, s, p, g, m, v, n, step_size, b1, b2, eps, wd, bc2_sqrt, gscale, gmul);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_grad_clip_ws_doubles(void) { return kNormBlocks; }
+
+int pcms_grad_clip(float* g, long n, float gscale, float max_norm, int apply, double* ws, float* norm_out,
+                   float* mul_out, hipStream_t s) {
+  if (ws == nullptr || mul_out == nullptr || ((uintptr_t)g & 15)) return -1;
+  const int rows = grid_for(n / 4 + 1, TPB, kNormBlocks);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(rows), dim3(TPB), 0, s, (const float*)g, n, ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(clip_finalize_kernel, dim3(1), dim3(256), 0, s, (const double*)ws, rows, gscale, max_norm,
+                     norm_out, mul_out);
+  e = hipGetLastError();
+  if (e != hipSuccess || !apply) return (int)e;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n, TPB, 16384)), dim3(TPB), 0, s, g, n, (const float*)mul_out);
   PCMS_CHECK_LAUNCH();
 }
 
 int pcms_split_epilogue_rows(long nvox) { return cdiv(nvox, 64); }
 
-int pcms_split_epilogue(int dtype, const float* acc, const float* bias, void* y0, void* y1, int cy0, float* stats,
-                        int C, long nvox, hipStream_t s) {
-  if (C % 64) return -1;
+int pcms_split_epilogue(int dtype, const float* acc, int splits, const float* bias, void* y0, void* y1, int cy0,
+                        float* stats, int C, long nvox, hipStream_t s) {
+  if (C % 64 || splits < 1) return -1;
   if (y1 == nullptr) cy0 = C;
   dim3 grid(cdiv(nvox, 64), C / 64);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(TPB), 0, s, acc, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox);
-  else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(TPB), 0, s, acc, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(TPB), 0, s, acc, splits, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox);
+  else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(TPB), 0, s, acc, splits, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -1,0 +1,556 @@
+// Stem convolution (inc.conv.0: n_modalities -> 64, k3 p1), bf16, gfx950: the HBM-bound
+// layer of the U-Net (models/unet3d.py:29 inside inc = DoubleConv3D(n_modalities, 64)).
+#include "conv_common.h"
+#include "pcms_hip.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------
+// Stem conv (inc.conv.0: n_modalities -> 64, input stored with 8 channels), bf16.
+// The generic kernel would spend 4x its MFMA work on zero channels (K = 27 x 32); here the
+// K dimension packs two taps per MFMA k-step: k = (tap 2s + h, channel c), h = lane >> 5,
+// so K = 14 x 16 = 224 (135 real).  HBM-bound: 16 B in + 128 B out per voxel.
+// ------------------------------------------------------------------------------------
+constexpr int kStemSteps = 14;                    // 28 taps (27 + 1 zero) / 2
+
+// master W[64][cin_w][27] fp32 -> [14][64][16] bf16, k = h * 8 + c <-> (tap 2s + h, c);
+// the 64 output columns are ordered (nt, j) -> channel 2 j + nt so that a lane's two MFMA
+// tiles hold an adjacent channel pair (one packed bf16x2 LDS write per row)
+__global__ void stem_pack_kernel(const float* w, bf16_t* out, int cin_w) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kStemSteps * 64 * 16) return;
+  const int k = i & 15, col = (i >> 4) & 63, s = i >> 10;
+  const int co = 2 * (col & 31) + (col >> 5);  // MFMA column (nt, j) <-> channel 2 j + nt
+  const int tap = 2 * s + (k >> 3), c = k & 7;
+  float v = 0.f;
+  if (tap < 27 && c < cin_w) v = w[((long)co * cin_w + c) * 27 + tap];
+  out[i] = f2bf(v);
+}
+
+__device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
+  if (tap >= 27) return 0;  // zero-weight pad tap: any in-halo row
+  const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+  return (kd * HH + kh) * HW + kw;
+}
+
+// Persistent stem forward, direct-store variant for 16-wide 512-voxel boxes (bd x bh = 32).
+// No C tile: the weight columns are ordered so that lane r_lane of a wave holds channels
+// (2 r_lane, 2 r_lane + 1) of each of its rows, so the 32 lanes of a half-wave write one
+// voxel's 64 channels (128 contiguous bytes) with ONE buffer_store_dword, addressed by a
+// per-lane voffset (2 variants), a wave-uniform soffset and an immediate offset: no VALU
+// address math, no LDS round trip, one barrier per box.  The halo arrives by buffer LDS-DMA
+// (out-of-range voffset = zero padding); weights stay in VGPRs; BatchNorm partials are
+// accumulated over all boxes of the workgroup (shifted sums) and written as ONE stats row
+// per workgroup (rows >= gridDim.x are zeroed: count 0).
+constexpr int kSDHaloRows = kHaloMax;                         // 1152 rows (18 x 64)
+constexpr int kSDHaloBytes = kSDHaloRows * 16;
+constexpr int kSDLds = 2 * kSDHaloBytes + 8 * 64 * 3 * 4;     // halo x2 + stats reduction
+constexpr int kSDThr = 512;                                   // one 8-wave workgroup per CU
+
+template <int LBD, int LBH>
+__global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
+                                                                    uint32_t xbytes, uint32_t ybytes) {
+  constexpr int THR = kSDThr;
+  constexpr int kSDThreads = THR, NWV = THR / 64;
+  static_assert((1 << (LBD + LBH + 4)) == NWV * 64, "box = 64 voxels per wave");
+  constexpr int bd = 1 << LBD, bh = 1 << LBH, bw = 16;
+  constexpr int HH = bh + 2, HW = bw + 2, HV = (bd + 2) * HH * HW;
+  constexpr int NP = (HV + kSDThreads - 1) / kSDThreads;  // halo pieces per thread
+  static_assert(HV <= kSDHaloRows, "halo fits");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* red = reinterpret_cast<float*>(lds + 2 * kSDHaloBytes);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR math)
+  const int r_lane = lane & 31, hsel = lane >> 5;
+  const int D = p.D, H = p.H, W = p.W;
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x0, 0, xbytes, 0x00020000);
+  const auto yr = __builtin_amdgcn_make_buffer_rsrc(p.y0, 0, ybytes, 0x00020000);
+
+  // weights: B fragments of all 14 k-steps in registers
+  s16x8_t wb[kStemSteps][2];
+  {
+    const bf16_t* wg = (const bf16_t*)p.w;
+#pragma unroll
+    for (int st = 0; st < kStemSteps; ++st) {
+      wb[st][0] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + r_lane) * 16 + hsel * 8);
+      wb[st][1] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
+    }
+  }
+  float bias_l[2] = {0.f, 0.f};
+  if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
+  // halo rows of the two 32-row MFMA tiles (perm32 layout)
+  int hb16[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int r = wave * 64 + mt * 32 + perm32(r_lane);
+    const int rd = r >> (LBH + 4), rh = (r >> 4) & (bh - 1), rw = r & 15;
+    hb16[mt] = ((rd * HH + rh) * HW + rw) * 16;
+  }
+  // halo pieces of this thread: relative source offset (bytes) and packed coordinates
+  int prel[NP], pco[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int hv = tid + i * kSDThreads;
+    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+    prel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
+    pco[i] = hv < HV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
+  }
+  // store voffsets: rows x = perm32((e & 3) + 8 g + 4 hsel) have x & 15 = 4 g + (e & 3) and
+  // x >> 4 = (g in {1, 2}) ^ hsel
+  const uint32_t vb0 = r_lane * 4, vb1 = r_lane * 4 + (uint32_t)W * 128;
+  const uint32_t vA = hsel ? vb1 : vb0;  // g = 0, 3
+  const uint32_t vB = hsel ? vb0 : vb1;  // g = 1, 2
+
+  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    const int nbw = p.nbw, nbh = p.nbh, nbd = p.nbd;
+    int q = b;
+    const int bwi = q % nbw; q /= nbw;
+    const int bhi = q % nbh; q /= nbh;
+    const int bdi = q % nbd;
+    n = q / nbd;
+    d0 = bdi * bd; h0 = bhi * bh; w0 = bwi * bw;
+  };
+  auto stage = [&](int b, int buf) {
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const int base16 = ((((n * D + d0) * H + h0) * W) + w0) * 16;
+    const bool inner = d0 >= 1 && d0 + bd < D && h0 >= 1 && h0 + bh < H && w0 >= 1 && w0 + bw < W;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      if (wave * 64 + i * kSDThreads >= HV) break;  // whole wave past the halo (uniform)
+      uint32_t voff = (uint32_t)(base16 + prel[i]);
+      const int c = pco[i];
+      if (c < 0) {
+        voff = kOOB;
+      } else if (!inner) {
+        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
+        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (LDS_AS void*)(lds + buf * kSDHaloBytes + (wave * 64 + i * kSDThreads) * 16),
+                                           16, voff, 0, 0, 0);
+    }
+  };
+
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2] = {0.f, 0.f};
+  float cnt = 0.f;
+  bool first = true;
+  int b = blockIdx.x;
+  if (b < nbox) stage(b, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
+    // halo(b) has landed for this wave (vmcnt above / at the loop end); barrier: for all
+    // waves, and every wave is done reading the buffer the next DMA overwrites
+    __syncthreads();
+    const int bn = b + gridDim.x;
+    if (bn < nbox) stage(bn, (it + 1) & 1);
+    const char* hl = lds + (it & 1) * kSDHaloBytes;
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];
+    {
+      int hs16 = hsel * 16;
+      asm volatile("" : "+v"(hs16));
+      auto load_a = [&](int st, s16x8_t (&a)[2]) {
+        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
+        const int off16 = o0 * 16 + hs16 * (o1 - o0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + off16);
+      };
+      s16x8_t abuf[2][2];
+      load_a(0, abuf[0]);
+#pragma unroll
+      for (int st = 0; st < kStemSteps; ++st) {
+        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
+          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // ---- epilogue: direct stores + shifted BN sums ----
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const bool full = d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
+    if (first) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(acc[0][nt][0], r_lane, 64);
+      first = false;
+    }
+    const int bv = ((n * D + d0) * H + h0) * W + w0;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int R0 = wave * 4 + mt * 2;          // even (rd, rh) linear index of the tile
+      const int rd0 = R0 >> LBH, rh0 = R0 & (bh - 1);
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (rd0 * H + rh0) * W) * 128u);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int g = e >> 2, rw = 4 * g + (e & 3);
+        const bool gB = (g == 1 || g == 2);
+        const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
+        uint32_t voff = gB ? vB : vA;
+        float e0 = v0 - K[0], e1 = v1 - K[1];
+        if (!full) {  // uniform branch: boundary boxes only
+          const int xh = (gB ? 1 : 0) ^ hsel;
+          const bool valid = (d0 + rd0 < D) & (h0 + rh0 + xh < H) & (w0 + rw < W);
+          voff = valid ? voff : kOOB;
+          e0 = valid ? e0 : 0.f;
+          e1 = valid ? e1 : 0.f;
+          cnt += valid ? 1.f : 0.f;
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so + rw * 128, 0);
+        s1[0] += e0; s2[0] += e0 * e0;
+        s1[1] += e1; s2[1] += e1 * e1;
+      }
+    }
+    if (full) cnt += 32.f;
+    // the next halo's DMA was issued before this box's 32 stores
+    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  }
+  if (!p.stats) return;
+  // per wave (lanes r_lane and r_lane + 32 share channels and K): S = sum d + n K,
+  // M2 = sum d^2 - (sum d)^2 / n; then Chan across the 8 waves
+  const float nw = cnt + __shfl_xor(cnt, 32, 64);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    s1[nt] += __shfl_xor(s1[nt], 32, 64);
+    s2[nt] += __shfl_xor(s2[nt], 32, 64);
+    if (hsel == 0) {
+      float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
+      rp[0] = s1[nt] + nw * K[nt];
+      rp[1] = nw > 0.f ? s2[nt] - s1[nt] * s1[nt] / nw : 0.f;
+      rp[2] = nw;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float S = 0.f, Nn = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) { S += red[(w * 64 + tid) * 3]; Nn += red[(w * 64 + tid) * 3 + 2]; }
+    const float m = Nn > 0.f ? S / Nn : 0.f;
+    float M2 = 0.f, sdd = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float c = red[(w * 64 + tid) * 3 + 2];
+      if (c > 0.f) {
+        const float d = red[(w * 64 + tid) * 3] / c - m;
+        M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+        sdd += c * d;
+      }
+    }
+    if (Nn > 0.f) M2 -= sdd * sdd / Nn;
+    float* st = p.stats + ((long)blockIdx.x * 64 + tid) * 2;
+    st[0] = S;
+    st[1] = M2;
+    float* cnts = p.stats + (long)mrows * 128;  // row counts after the [mrows][64][2] block
+    if (tid == 0) cnts[blockIdx.x] = Nn;
+    // zero this workgroup's share of the rows past gridDim.x
+    for (int r = blockIdx.x + gridDim.x; r < mrows; r += gridDim.x) {
+      p.stats[((long)r * 64 + tid) * 2] = 0.f;
+      p.stats[((long)r * 64 + tid) * 2 + 1] = 0.f;
+      if (tid == 0) cnts[r] = 0.f;
+    }
+  }
+}
+
+
+// Streaming stem weight gradient (the HBM-bound hot case: D % 4 == H % 4 == W % 16 == 0).
+// dW[co][c][t] = sum_v dy[v][co] x[v + t][c]: GEMM with M = 64 co, N = 224 (tap, channel)
+// columns, K = voxels.  Persistent: one 4-wave workgroup per CU walks 4x4x16 voxel boxes
+// b = blockIdx.x + k gridDim.x.  Each box's dy tile (256 voxels x 128 B) and x halo
+// (6x6x18 rows x 16 B) arrive by buffer LDS-DMA (inline asm, see dma16) into a 3-slot ring:
+// two boxes in flight while one computes, counted vmcnt + raw s_barrier, every source
+// offset a per-thread constant + the box base.  Wave w owns k-steps w, w + 4, w + 8, w + 12
+// of every box and ALL 14 output tiles (2 co x 7 column tiles, accumulators in AGPRs), so
+// each A / B fragment is read from LDS exactly once per box (ds_read_b64_tr_b16 transposes
+// both operands) and the next k-step's fragments are read during this one's 14 MFMAs.
+// Flush: one fp32 partial row [64][cin_w][27] per workgroup (plain stores), summed into dw
+// by stem_wgrad_reduce_kernel (deterministic, no atomics).
+constexpr int kSWT = 256;                                  // 4 waves, one per SIMD
+// BD = box depth (boxes BD x 4 x 16), NS = ring slots (NS - 1 boxes in flight).  The load
+// pipeline is latency-bound (bytes in flight per CU), so the product ring uses 2-deep boxes
+// in 6 slots (115 KB in flight) rather than 4-deep boxes in 3 slots (86 KB).
+template <int BD> struct SWGeom {
+  static constexpr int BV = BD * 64;                            // voxels per box
+  static constexpr int HV = (BD + 2) * 6 * 18;                  // halo rows (16 B)
+  static constexpr int HRows = (HV + 63) / 64 * 64;             // rows written
+  static constexpr int Buf = BV * 128 + HRows * 16;             // bytes per ring slot
+  static constexpr int DYP = BV * 8 / kSWT;                     // dy DMA pieces per thread
+  static constexpr int XI = (HRows / 64 + 3) / 4;               // halo DMA rounds per wave
+};
+constexpr int kSWBD = 4;  // box depth (2-deep boxes in 6 slots measured slower)
+constexpr int kSWNS = kSWBD == 4 ? 3 : 6;
+constexpr int kSWLds = kSWNS * SWGeom<kSWBD>::Buf;
+static_assert(kSWLds >= 64 * 224 * 4, "flush tile fits in the ring");
+static_assert(kSWLds <= 160 * 1024, "ring fits in LDS");
+
+template <int BD, int NS>
+__global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t* x, const bf16_t* dy, float* part,
+                                                                    int N, int D, int H, int W, int cin_w,
+                                                                    uint32_t xbytes, uint32_t dybytes) {
+  typedef SWGeom<BD> Gm;
+  constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
+  constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
+  extern __shared__ __attribute__((aligned(16))) char swl[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hsel = lane >> 5;
+  const int nbw = W / BW, nbh = H / BH, nbd = D / BD;
+  const int nbox = N * nbd * nbh * nbw;
+  const i32x4_t xr = buffer_desc(x, xbytes);
+  const i32x4_t dr = buffer_desc(dy, dybytes);
+
+  // per-thread DMA source offsets relative to the box origin (constant over boxes)
+  uint32_t dyrel[Gm::DYP];
+#pragma unroll
+  for (int i = 0; i < Gm::DYP; ++i) {
+    const int pc = tid + i * kSWT;
+    const int r = pc >> 3, q = pc & 7;
+    const int ql = q ^ (((r >> 1) & 1) << 2);  // dy_off_bf16: 64-B halves swapped on odd row pairs
+    const int rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
+    dyrel[i] = (uint32_t)(((rd * H + rh) * W + rw) * 128 + ql * 16);
+  }
+  // halo pieces of this wave: rows wave*64 + lane + 256 i < HRows (XI or XI - 1 of them)
+  const int nxp = (Gm::HRows / 64 - wave + 3) / 4;
+  int xrel[Gm::XI], xco[Gm::XI];
+#pragma unroll
+  for (int i = 0; i < Gm::XI; ++i) {
+    const int hv = wave * 64 + lane + i * kSWT;
+    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+    xrel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
+    xco[i] = hv < kSWHV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
+  }
+  auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
+    int q = b;
+    const int bwi = q % nbw; q /= nbw;
+    const int bhi = q % nbh; q /= nbh;
+    const int bdi = q % nbd;
+    n = q / nbd;
+    d0 = bdi * BD; h0 = bhi * BH; w0 = bwi * BW;
+  };
+  auto stage = [&](int b, int slot) {
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const int vb = ((n * D + d0) * H + h0) * W + w0;
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(swl) + slot * kSWBuf + wave * 64 * 16);
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)vb * 128u);
+#pragma unroll
+    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
+    const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
+#pragma unroll
+    for (int i = 0; i < Gm::XI; ++i) {
+      if (i >= nxp) break;
+      uint32_t voff = (uint32_t)(vb * 16 + xrel[i]);
+      const int c = xco[i];
+      if (c < 0) {
+        voff = kOOB;
+      } else if (!inner) {
+        const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
+        if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
+      }
+      dma16(xr, lb + kSWBV * 128 + i * kSWT * 16, voff, 0);
+    }
+  };
+
+  const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+  f32x16_t acc[2][7];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // lane offsets of the tr reads, with the wave's k-step offset folded in (k-step s = wave +
+  // 4 i is box row (rd = i, rh = wave): dy rows at s * 2048, halo rows at (i HH + wave) HW)
+  const int aoff0 = dy_off_bf16(8 * hsel + qq, g * 16 + pp * 4) + wave * 2048;
+  const int aoff1 = dy_off_bf16(8 * hsel + qq, 32 + g * 16 + pp * 4) + wave * 2048;
+  int boff[7];  // column tile j: taps 4 j + 2 g + (pp >> 1), channels 4 (pp & 1) .. + 3
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+    boff[j] = kSWBV * 128 + (8 * hsel + qq + tap_off(4 * j + 2 * g + (pp >> 1), HH, HW) + wave * HW) * 16 + (pp & 1) * 8;
+  auto compute = [&](const char* buf) {
+    uint32_t pa0 = lds_addr(buf) + aoff0, pa1 = lds_addr(buf) + aoff1, pb[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) pb[j] = lds_addr(buf) + boff[j];
+    asm volatile("" : "+v"(pa0), "+v"(pa1), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]),
+                 "+v"(pb[5]), "+v"(pb[6]));
+    auto tr = [](uint32_t p, int off) {
+      return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(uintptr_t)(p + off));
+    };
+    auto cat = [](s16x4_t lo, s16x4_t hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); };
+    auto load = [&](int i, s16x8_t (&a)[2], s16x8_t (&bq)[7]) {
+      const int dyb = i * 4 * 2048;
+      const int hrb = i * HH * HW * 16;
+      a[0] = cat(tr(pa0, dyb), tr(pa0, dyb + 512));
+      a[1] = cat(tr(pa1, dyb), tr(pa1, dyb + 512));
+#pragma unroll
+      for (int j = 0; j < 7; ++j) bq[j] = cat(tr(pb[j], hrb), tr(pb[j], hrb + 64));
+    };
+    s16x8_t a[2][2], bq[2][7];
+    load(0, a[0], bq[0]);
+#pragma unroll
+    for (int i = 0; i < BD; ++i) {
+      if (i + 1 < BD) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct][j] = mfma(a[i & 1][ct], bq[i & 1][j], acc[ct][j]);
+    }
+  };
+
+  const int G = gridDim.x;
+  int b = blockIdx.x;
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (b + k * G < nbox) stage(b + k * G, k);
+  for (int it = 0; b < nbox; b += G, ++it) {
+    // retire box b's DMA (the NS - 2 boxes after it may stay in flight), then barrier:
+    // every wave's share of box b has landed and every wave is done reading the slot
+    // refilled below
+    if (b + (NS - 2) * G < nbox) {
+      if (nxp == Gm::XI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI - 1)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int b2 = b + (NS - 1) * G;
+    if (b2 < nbox) stage(b2, (it + NS - 1) % NS);
+    compute(swl + (it % NS) * kSWBuf);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // flush: the 4 waves' partial tiles summed in LDS [co][224 cols] (fixed order)
+  float* red = reinterpret_cast<float*>(swl);
+  for (int pass = 0; pass < 4; ++pass) {
+    if (wave == pass) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int co = ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+            float* dst = red + co * 224 + j * 32 + (lane & 31);
+            if (pass == 0) *dst = acc[ct][j][e];
+            else *dst += acc[ct][j][e];
+          }
+    }
+    __syncthreads();
+  }
+  const int total = 64 * cin_w * 27;
+  float* prow = part + (long)blockIdx.x * total;
+  for (int i = tid; i < total; i += kSWT) {
+    const int t = i % 27, c = (i / 27) % cin_w, co = i / (27 * cin_w);
+    prow[i] = red[co * 224 + t * 8 + c];
+  }
+}
+
+// dw[o] += sum over the workgroup partial rows (fixed order).  Block = 32 outputs x 8 row
+// groups: 32 independent 128-B row segments in flight per thread group, LDS combine.
+__global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* part, int rows, int total, float* dw) {
+  __shared__ float red[8][32];
+  const int ol = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int o = blockIdx.x * 32 + ol;
+  float s = 0.f;
+  if (o < total) {
+#pragma unroll 8
+    for (int r = rg; r < rows; r += 8) s += part[(long)r * total + o];
+  }
+  red[rg][ol] = s;
+  __syncthreads();
+  if (rg == 0 && o < total) {
+    float t = 0.f;
+#pragma unroll
+    for (int g2 = 0; g2 < 8; ++g2) t += red[g2][ol];
+    dw[o] += t;
+  }
+}
+
+}  // namespace
+
+// the dedicated stem kernels' shape conditions (other shapes take the general conv kernels)
+static bool stem_fwd_direct_shape(int N, int D, int H, int W) {
+  const Box b = fwd_box(D, H, W);
+  return b.lbw == 4 && b.lbd + b.lbh == 5 && (b.lbd == 2 || b.lbd == 3) && (long)N * D * H * W * 128 < (long)kOOB;
+}
+static bool stem_wgrad_streams(int N, int D, int H, int W) {
+  return D % kSWBD == 0 && H % 4 == 0 && W % 16 == 0 && (long)N * D * H * W * 128 < (1L << 31);
+}
+
+extern "C" {
+
+int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s) {
+  if (cin_w > 8) return -1;
+  hipLaunchKernelGGL(stem_pack_kernel, dim3(cdiv(kStemSteps * 64 * 16, 256)), dim3(256), 0, s, w, (bf16_t*)out, cin_w);
+  PCMS_CHECK_LAUNCH();
+}
+int pcms_stem_pack_elems(void) { return kStemSteps * 64 * 16; }
+
+// bit 0: pcms_stem_fwd runs this shape; bit 1: pcms_stem_wgrad runs it
+int pcms_stem_supported(int N, int D, int H, int W) {
+  return (stem_fwd_direct_shape(N, D, H, W) ? 1 : 0) | (stem_wgrad_streams(N, D, H, W) ? 2 : 0);
+}
+
+// BatchNorm statistics rows pcms_stem_fwd writes
+int pcms_stem_fwd_rows(int N, int D, int H, int W) { return pcms_conv3_mblocks(N, D, H, W); }
+
+// x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_stem_fwd_rows
+int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
+                  int N, int D, int H, int W, hipStream_t s) {
+  if (!stem_fwd_direct_shape(N, D, H, W)) return -5;
+  const Box b = fwd_box(D, H, W);
+  Conv3Params p;
+  p.x0 = x; p.x1 = nullptr; p.c0 = 8; p.c1 = 0;
+  p.w = wpack; p.bias = bias; p.y0 = y; p.y1 = nullptr; p.cy0 = 64;
+  p.yacc = nullptr; p.stats = stats; p.accumulate = 0;
+  p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = 8; p.Cout = 64;
+  p.nvox = (long)N * D * H * W;
+  p.nchunk = 1; p.chunks_per_split = 1;
+  p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
+  p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
+  const int nbox = N * p.nbd * p.nbh * p.nbw;
+  const long xbytes = p.nvox * 16, ybytes = p.nvox * 128;
+  const int grid = std::min(nbox, device_cus());
+  auto kern = b.lbd == 2 ? stem_fwd_direct_kernel<2, 3> : stem_fwd_direct_kernel<3, 2>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSDLds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThr), kSDLds, s, p, nbox, nbox, (uint32_t)xbytes, (uint32_t)ybytes);
+  PCMS_CHECK_LAUNCH();
+}
+
+// fp32 workspace floats pcms_stem_wgrad needs (0: shape not supported)
+int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w) {
+  if (!stem_wgrad_streams(N, D, H, W)) return 0;
+  const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
+  return std::min(nbox, device_cus()) * 64 * cin_w * 27;
+}
+
+// dw [64][cin_w][27] fp32 += stem weight gradient (x: 8-channel bf16 input, dy: 64 ch);
+// ws: pcms_stem_wgrad_ws_floats(...) floats (one partial row per workgroup, fixed-order sum)
+int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H, int W,
+                    hipStream_t s) {
+  if (cin_w > 8 || cin_w < 1) return -1;
+  if (!stem_wgrad_streams(N, D, H, W)) return -5;
+  if (ws == nullptr) return -2;
+  const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
+  const int grid = std::min(nbox, device_cus());
+  const long xbytes = (long)N * D * H * W * 16, dybytes = (long)N * D * H * W * 128;
+  auto kern = stem_wgrad_stream_kernel<kSWBD, kSWNS>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSWLds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT), kSWLds, s, (const bf16_t*)x, (const bf16_t*)dy, ws, N, D, H, W,
+                     cin_w, (uint32_t)xbytes, (uint32_t)dybytes);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int total = 64 * cin_w * 27;
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, (const float*)ws, grid, total,
+                     dw);
+  PCMS_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -256,12 +256,48 @@ class ProstateDataset(Dataset):
 
 def get_dataloader(data_dir: str, batch_size: int = 2, shuffle: bool = True, modalities=None,
                    missing_strategy: str = "zero_fill", target_size=(128, 128, 128), num_workers: int = 0,
-                   is_training: bool = True, data_type: str = "BPH", indices=None) -> DataLoader:
+                   is_training: bool = True, data_type: str = "BPH", indices=None, rank: int = 0,
+                   world_size: int = 1) -> DataLoader:
     """script/data_loader.py:421-466 (pinned host batches; Trainer stages them to the GPU on
-    a copy stream one batch ahead)."""
+    a copy stream one batch ahead).  ``world_size > 1``: each rank iterates its own
+    DistributedSampler shard (call ``loader.sampler.set_epoch(epoch)`` every epoch)."""
     ds = ProstateDataset(data_dir, modalities=modalities, missing_strategy=missing_strategy,
                          target_size=target_size, is_training=is_training, data_type=data_type)
     if indices is not None:
         ds = torch.utils.data.Subset(ds, indices)
-    return DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
-                      pin_memory=torch.cuda.is_available())
+    sampler = None
+    if world_size > 1:
+        sampler = torch.utils.data.distributed.DistributedSampler(ds, num_replicas=world_size, rank=rank,
+                                                                  shuffle=shuffle)
+    return DataLoader(ds, batch_size=batch_size, shuffle=shuffle and sampler is None, sampler=sampler,
+                      num_workers=num_workers, pin_memory=torch.cuda.is_available())
+
+
+def kfold_indices(n_cases: int, n_splits: int = 5, seed: int = 42):
+    """sklearn ``KFold(n_splits, shuffle=True, random_state=seed).split(range(n_cases))``
+    restated (the reference's get_kfold_splits, script/data_loader.py:468-497): a legacy
+    numpy RandomState(seed) shuffle of arange(n), folds of n // k (+1 for the first n % k),
+    each fold's test and train indices in ascending order."""
+    if n_splits < 2 or n_splits > n_cases:
+        raise ValueError(f"cannot split {n_cases} cases into {n_splits} folds")
+    order = np.arange(n_cases)
+    np.random.RandomState(seed).shuffle(order)
+    sizes = np.full(n_splits, n_cases // n_splits, dtype=int)
+    sizes[: n_cases % n_splits] += 1
+    splits, cur = [], 0
+    for sz in sizes:
+        mask = np.zeros(n_cases, dtype=bool)
+        mask[order[cur:cur + sz]] = True
+        cur += sz
+        idx = np.arange(n_cases)
+        splits.append((idx[~mask], idx[mask]))
+    return splits
+
+
+def get_kfold_splits(data_dir: str, n_splits: int = 5, modalities=None, missing_strategy: str = "zero_fill",
+                     target_size=(128, 128, 128), data_type: str = "BPH"):
+    """script/data_loader.py:468-497: K (train_indices, val_indices) pairs over the case list
+    scanned from <data_dir>/BPH-PCA/<data_type>/ADC (KFold, shuffle, random_state 42)."""
+    ds = ProstateDataset.__new__(ProstateDataset)
+    ds.data_dir, ds.data_type = data_dir, data_type
+    return kfold_indices(len(ds._get_case_list()), n_splits)

@@ -16,7 +16,9 @@ The gradient all-reduce is bucketed and overlapped with the backward: the engine
 each module's gradient range as soon as its backward has written it (decoder first, the
 stem last) and a bucket is launched asynchronously (``async_op=True``: the RCCL kernel is
 ordered after the producing kernels of the compute stream, then runs beside the rest of
-the backward).  ``finish()`` makes the compute stream wait for every bucket before Adam.
+the backward).  ``finish()`` makes the compute stream wait for every bucket before Adam,
+which applies the 1/world mean in its single pass over the gradient and writes the mean
+back, so ``param.grad`` holds the DDP mean after ``optimizer.step()``.
 Buckets are contiguous slices of the flat gradient, so every collective is one large
 message: xGMI rings are per-link bound, so few large transfers beat many small ones.
 """
@@ -69,6 +71,17 @@ class GradSync:
         self._hi: Optional[int] = None
         self._next_hi = flat_g.numel()   # the next ready range must end here
         self.launched: List[Tuple[int, int]] = []   # buckets of the current step (tests / logs)
+
+    def reset(self):
+        """Drop the state of a step whose backward stopped part-way (an exception between
+        the first ``ready`` and ``finish``): wait for the buckets already launched (their
+        sums land in a gradient the next step zeroes anyway), forget the pending range."""
+        for w in self._works:
+            w.wait()
+        self._works = []
+        self._lo = self._hi = None
+        self._next_hi = self.flat_g.numel()
+        self.launched = []
 
     def broadcast_buffers(self, flat_bn: torch.Tensor):
         """DDP broadcast_buffers: every rank takes rank 0's BatchNorm running statistics."""

@@ -100,6 +100,7 @@ class UNetEngine:
         self.convt_packs: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
         # bf16 build: the stem runs on dedicated tap-packed kernels (HBM-bound)
         self.stem_fast = self.code == BF16 and self.cp == 8
+        self.stem_sup = 0  # pcms_stem_supported bits for the allocated shape (set by _alloc)
         self.stem_pack = None
         self._flat_ptrs = None
         self._packed_version = -1
@@ -112,10 +113,10 @@ class UNetEngine:
         # pre-BN conv outputs and first ReLU output (y1, a1, y2) are not kept per level; the
         # forward writes them into one shared level-0-sized set and the backward recomputes
         # them level by level with the forward's BatchNorm coefficients (no statistics pass,
-        # running stats untouched).  Decoder convs then run unsplit (no split-K atomics), so the
-        # recomputed tensors are bit-identical to the forward's.
+        # running stats untouched).  Every reduction in the library sums in a fixed order (split-K
+        # slabs, BN partial rows, weight-gradient partial rows), so the recomputed tensors are
+        # bit-identical to the forward's and two identical steps give identical results.
         self.act_ckpt = False
-        self.unsplit = False  # every conv unsplit (no split-K fp32 atomics): a deterministic step
         self.wgrad_target = 256  # conv weight-gradient workgroups: one round of 1 WG per CU (fewer partial rows to reduce than 512)
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
         self.wgrad_side_stream = False  # ablation: weight gradients on a side stream (measured 119.9 vs 121.6 vol/s: off)
@@ -299,16 +300,31 @@ class UNetEngine:
         b["coef"] = torch.empty(3 * 1024, dtype=torch.float32, device=dev)
         b["bnws"] = torch.empty(query("pcms_bn_ws_doubles", 1024), dtype=torch.float64, device=dev)
         # weight-gradient workspace: per-split partial rows of the largest conv (and the stem)
-        ws = [query("pcms_stem_wgrad_ws_floats", N, *S[0], self.nmod)] if self.stem_fast else []
+        ws = [query("pcms_stem_wgrad_ws_floats", N, *S[0], self.nmod)] if self.stem_fast else [1]
         for blk, l in [(bk, i) for i, bk in enumerate(self.enc)] + [(bk, 3 - i) for i, bk in enumerate(self.dec)]:
             for cs, c1 in ((blk.c0, C[l] if blk in self.dec else 0), (blk.c1, 0)):
                 c0 = cs.cin_store - c1
                 ws.append(query("pcms_conv3_wgrad_ws_floats", self.code, N, *S[l], c0, c1, cs.cout,
                                 self.wgrad_target))
         b["dwt"] = torch.empty(max(ws), dtype=torch.float32, device=dev)
-        # split-K accumulators only where a level can be split (few workgroups along M)
-        split_lv = [l for l in range(5) if query("pcms_conv3_mblocks", N, *S[l]) * (C[l] // 64) < 192]
-        b["yacc"] = torch.empty(max([nv[l] * 2 * C[l] for l in split_lv] + [1]), dtype=torch.float32, device=dev)
+        # split-K slabs [splits][nvox][Cout] for every conv (fwd and dgrad) that splits
+        yacc = 1
+        for blk, l in [(bk, i) for i, bk in enumerate(self.enc)] + [(bk, 3 - i) for i, bk in enumerate(self.dec)]:
+            for cs in (blk.c0, blk.c1):
+                dirs = [(cs.cin_store, cs.cout)] + ([(cs.cout, cs.cin)] if cs is not self.convs[0] else [])
+                for cin, cout in dirs:  # forward, dgrad (the stem has none)
+                    sp = self._splits(N, S[l], cin, cout)
+                    if sp > 1:
+                        yacc = max(yacc, query("pcms_conv3_splits", self.code, cin, sp) * nv[l] * cout)
+        b["yacc"] = torch.empty(yacc, dtype=torch.float32, device=dev)
+        # partial rows of the head / ConvT-bias gradient reductions (summed in a fixed order)
+        red = [query("pcms_head_bwd_ws_floats", D * H * W, N, self.ncls)]
+        for i, up in enumerate(self.ups):
+            l = 3 - i
+            red.append(query("pcms_box_channel_sum_ws_floats", self.code, N, C[l], *[2 * v for v in S[l + 1]]))
+        b["redws"] = torch.empty(max(red), dtype=torch.float32, device=dev)
+        # dedicated stem kernels where they support the shape (else the general conv kernels)
+        self.stem_sup = query("pcms_stem_supported", N, D, H, W) if self.stem_fast else 0
         ctws = [query("pcms_convt_wgrad_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels, 512)
                 for i, up in enumerate(self.ups)]
         b["ctws"] = torch.empty(max(ctws), dtype=torch.float32, device=dev)
@@ -320,7 +336,7 @@ class UNetEngine:
         mb = query("pcms_conv3_mblocks", N, *S)
         wgs = mb * (cout // 64)
         nch = -(-cin // query("pcms_conv3_chunk", self.code))
-        if wgs >= 192 or nch == 1:
+        if wgs >= 192 or nch == 1 or wgs == 0:
             return 1
         return max(1, min(nch, -(-384 // wgs)))
 
@@ -330,12 +346,9 @@ class UNetEngine:
         the conv alone (checkpointed decoder: the forward's BN coefficients are reused)."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
-        if self.unsplit or self.buf_key[4] and any(cs is blk.c0 or cs is blk.c1 for blk in self.dec):
-            splits = 1  # deterministic: the recompute reproduces the forward bit for bit
-        else:
-            splits = self._splits(N, S, c0 + c1, cs.cout)
+        splits = self._splits(N, S, c0 + c1, cs.cout)
         st = b["stats"] if training and not recompute else None
-        if cs is self.convs[0] and self.stem_fast:
+        if cs is self.convs[0] and self.stem_sup & 1:
             call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2])
             rows = query("pcms_stem_fwd_rows", N, *S)
         elif splits == 1:
@@ -343,11 +356,11 @@ class UNetEngine:
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
             rows = query("pcms_conv3_fwd_rows", self.code, N, *S, c0, c1)
         else:
-            acc = b["yacc"][: nvox * cs.cout]
-            acc.zero_()
+            acc = b["yacc"]
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  acc, None, 0, N, S[0], S[1], S[2], cs.cout, splits)
-            call("pcms_split_epilogue", self.code, acc, cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox)
+            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, c0 + c1, splits),
+                 cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox)
             rows = query("pcms_split_epilogue_rows", nvox)
         if recompute:
             return
@@ -441,8 +454,8 @@ class UNetEngine:
         # BN0/ReLU backward -> dy1 (a second buffer: the side stream may still read gY)
         self._bn_bwd(blk.b0, gA, acts["y1"], gZ, nvox)
         with self._side():
-            if blk is self.enc[0] and self.stem_fast:
-                call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S, 256)
+            if blk is self.enc[0] and self.stem_sup & 2:
+                call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
             else:
                 call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gZ, blk.c0.mod.weight.grad, b["dwt"], N,
                      *S, blk.c0.cout, blk.c0.cin, self.wgrad_target)
@@ -463,11 +476,11 @@ class UNetEngine:
             call("pcms_conv3_fwd", self.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  None, None, 0, N, *S, cs.cin, 1)
         else:
-            acc = b["yacc"][: nvox * cs.cin]
-            acc.zero_()
+            acc = b["yacc"]
             call("pcms_conv3_fwd", self.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  acc, None, 0, N, *S, cs.cin, splits)
-            call("pcms_split_epilogue", self.code, acc, None, out0, out1, cy0, None, cs.cin, nvox)
+            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, cs.cout, splits),
+                 None, out0, out1, cy0, None, cs.cin, nvox)
 
     def backward(self, dlogits: torch.Tensor):
         if self.saved_epoch != self.epoch:
@@ -481,7 +494,7 @@ class UNetEngine:
         oc = self.model.outc
         D, H, W = S[0]
         call("pcms_head_bwd", self.code, b["d0_a2"], dlogits, oc.weight, b["gH"], oc.weight.grad, oc.bias.grad,
-             D * H * W, N, self.ncls)
+             b["redws"], D * H * W, N, self.ncls)
         self._grads_done("outc")
         g = b["gH"]
         # decoder, last block first
@@ -502,7 +515,7 @@ class UNetEngine:
             dz = (S[l][0] - 2 * S[l + 1][0]) // 2
             dy_ = (S[l][1] - 2 * S[l + 1][1]) // 2
             dx_ = (S[l][2] - 2 * S[l + 1][2]) // 2
-            call("pcms_box_channel_sum", self.code, gu, up.bias.grad, N, *S[l], C[l], dz, dy_, dx_,
+            call("pcms_box_channel_sum", self.code, gu, up.bias.grad, b["redws"], N, *S[l], C[l], dz, dy_, dx_,
                  2 * S[l + 1][0], 2 * S[l + 1][1], 2 * S[l + 1][2])
             self._grads_done(f"up{i + 1}")
             gnext = b["gx4"] if i == 0 else b[f"gA{l + 1}"]

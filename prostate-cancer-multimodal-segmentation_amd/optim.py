@@ -25,7 +25,11 @@ class FlatAdam(torch.optim.Optimizer):
         super().__init__(list(model.parameters()), defaults)
         self.model = model
         self.step_count = 0
+        # gradient multipliers applied by the Adam kernel (one step): grad_scale (host float:
+        # the data-parallel 1/world) and grad_mul (device fp32 scalar from pcms_grad_clip: the
+        # clip coefficient / AMP unscale), both folded into the single Adam pass
         self.grad_scale = 1.0
+        self.grad_mul = None
         self._m = None
         self._v = None
 
@@ -52,7 +56,11 @@ class FlatAdam(torch.optim.Optimizer):
         bc1 = 1.0 - b1 ** self.step_count
         bc2 = 1.0 - b2 ** self.step_count
         call("pcms_adam", eng.flat_p, eng.flat_g, m, v, eng.flat_p.numel(), g["lr"] / bc1, b1, b2, g["eps"],
-             g["weight_decay"], math.sqrt(bc2), float(self.grad_scale))
+             g["weight_decay"], math.sqrt(bc2), float(self.grad_scale), self.grad_mul)
+        # one-shot multipliers of this step's gradient (the kernel wrote the scaled gradient
+        # back into param.grad)
+        self.grad_scale = 1.0
+        self.grad_mul = None
         eng.mark_dirty()
         return loss
 

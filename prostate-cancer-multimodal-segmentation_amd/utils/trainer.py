@@ -20,18 +20,28 @@ BatchNorm statistics and the global Dice stay per replica (plain BatchNorm3d, SU
 
 Config keys follow utils/trainer.py:40-49 (``device``, ``learning_rate``, ``batch_size``,
 ``num_epochs``, ``save_dir``, ``validation`` ...) plus ``loss`` ('dice' | 'bce_dice'),
-``precision`` ('bf16' | 'fp32'), ``checkpoint_decoder``.  With ``data_dir`` the loaders come
-from ``pcms_amd.data.get_dataloader`` (script/data_loader.py); otherwise pass
-``train_loader`` / ``val_loader`` iterables of batch dicts.
+``precision`` ('bf16' | 'fp32'), ``checkpoint_decoder``, and the step variants of the other
+reference trainers:
+  ``max_grad_norm``  clip_grad_norm_(max_norm) before Adam (train_bph.py:166,
+                     train_bph_cv.py:311 use 1.0): one fused norm pass, the clip coefficient
+                     folded into the Adam kernel;
+  ``use_amp``        GradScaler loss scaling around the step (train_bph_optimized.py:248-298;
+                     see pcms_amd.amp: the reduced-precision engine path is bf16).
+With ``data_dir`` the loaders come from ``pcms_amd.data.get_dataloader`` (script/data_loader.py;
+a DistributedSampler shard per rank under data parallelism); otherwise pass ``train_loader``
+/ ``val_loader`` iterables of batch dicts.
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import Iterable, Optional
 
 import torch
 import torch.distributed as dist
 
+from .._lib import call, query
+from ..amp import GradScaler
 from ..dp import GradSync
 from ..models.unet3d import UNet3D
 from ..optim import FlatAdam
@@ -58,6 +68,11 @@ class BaseTrainer:
             self.val_loader = self._create_dataloader("test")
         self._copy_stream = None
         self._sync = None
+        self.max_grad_norm = config.get("max_grad_norm", config.get("grad_clip"))
+        self.scaler = GradScaler(init_scale=config.get("amp_init_scale", 2.0 ** 16)) if config.get("use_amp") else None
+        self._clip_bufs = None
+        self.last_grad_norm = None   # device tensor: the total gradient norm of the last clipped step
+        self._resume = (float("inf"), 0)   # (best loss, patience) carried by a loaded checkpoint
         if self.distributed:
             self._broadcast_params()
         if config.get("save_dir"):
@@ -80,7 +95,8 @@ class BaseTrainer:
 
     def _create_dataloader(self, mode):
         """utils/trainer.py:139-158 with the arguments get_dataloader actually takes (the
-        reference passes ``mode=`` / ``handle_missing_modalities=``, which it rejects)."""
+        reference passes ``mode=`` / ``handle_missing_modalities=``, which it rejects); under
+        data parallelism each rank reads its own DistributedSampler shard."""
         if self.config.get("data_dir") is None:
             return None
         from ..data import get_dataloader
@@ -89,7 +105,8 @@ class BaseTrainer:
                               missing_strategy=self.config.get("handle_missing_modalities",
                                                                self.config.get("missing_strategy", "zero_fill")),
                               target_size=tuple(self.config.get("target_size", (128, 128, 128))),
-                              is_training=mode == "train", data_type=self.config.get("data_type", "BPH"))
+                              is_training=mode == "train", data_type=self.config.get("data_type", "BPH"),
+                              rank=self.rank, world_size=self.world_size)
 
     def _broadcast_params(self):
         eng = self.model.engine()
@@ -109,26 +126,52 @@ class BaseTrainer:
                                   overlap=self.config.get("dp_overlap", True))
         return eng, self._sync
 
+    def _clip_buffers(self):
+        if self._clip_bufs is None:
+            dev = self.model.engine().flat_g.device
+            self._clip_bufs = (torch.empty(query("pcms_grad_clip_ws_doubles"), dtype=torch.float64, device=dev),
+                               torch.empty(1, device=dev), torch.empty(1, device=dev))
+        return self._clip_bufs
+
     def step_async(self, batch) -> torch.Tensor:
-        """One training step; returns the loss as a device tensor (no host sync)."""
+        """One training step; returns the loss as a device tensor (no host sync unless the
+        AMP variant has to decide whether to skip the update)."""
         images = batch["image"].to(self.device, non_blocking=True)
         labels = batch["label"].to(self.device, non_blocking=True)
         self.model.train()
         self.optimizer.zero_grad()
         if self.distributed:
             eng, sync = self._grad_sync()
+            sync.reset()
             sync.broadcast_buffers(eng.flat_bn)
             eng.grad_ready = sync.ready   # buckets launch as the backward finishes each module
         try:
             outputs = self.model(images)
             loss = self.criterion(outputs, labels)
-            loss.backward()
+            (self.scaler.scale(loss) if self.scaler is not None else loss).backward()
+        except BaseException:
+            if self.distributed:
+                sync.reset()
+            raise
         finally:
             if self.distributed:
                 eng.grad_ready = None
-        if self.distributed:
-            self.optimizer.grad_scale = sync.finish()
-        self.optimizer.step()
+        # sum over ranks -> mean: folded into the Adam pass (which writes the mean back)
+        self.optimizer.grad_scale = sync.finish() if self.distributed else 1.0
+        if self.scaler is not None:
+            self.scaler.unscale_(self.optimizer, max_norm=self.max_grad_norm or 0.0)
+            self.last_grad_norm = self.scaler._norm
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
+        else:
+            if self.max_grad_norm is not None:
+                eng = self.model.engine()
+                ws, norm, mul = self._clip_buffers()
+                call("pcms_grad_clip", eng.flat_g, eng.flat_g.numel(), float(self.optimizer.grad_scale),
+                     float(self.max_grad_norm), 0, ws, norm, mul)
+                self.optimizer.grad_scale, self.optimizer.grad_mul = 1.0, mul
+                self.last_grad_norm = norm
+            self.optimizer.step()
         return loss.detach()
 
     def _prefetched(self, loader):
@@ -149,7 +192,13 @@ class BaseTrainer:
                 ev.record(cs)
             if nxt is not None:
                 yield nxt
-            torch.cuda.current_stream().wait_event(ev)
+            main = torch.cuda.current_stream()
+            main.wait_event(ev)
+            for v in staged.values():
+                if torch.is_tensor(v) and v.device.type == "cuda":
+                    # allocated on the copy stream, used on the compute stream: keep the
+                    # caching allocator from reusing the block before compute is done
+                    v.record_stream(main)
             nxt = staged
         if nxt is not None:
             yield nxt
@@ -174,13 +223,18 @@ class BaseTrainer:
                 n += 1
         return total / max(n, 1)
 
-    def save_checkpoint(self, epoch, loss, is_best=False):
-        """utils/trainer.py:236-278 (same dict keys and file names)."""
+    def save_checkpoint(self, epoch, loss, is_best=False, best_loss=None, patience=None):
+        """utils/trainer.py:236-278 (same dict keys and file names; ``best_loss`` /
+        ``patience`` are extra keys so a resumed ``train`` continues its early stopping)."""
         if self.rank != 0:
             return
         ckpt = {"epoch": epoch, "model_state_dict": self.model.state_dict(),
                 "optimizer_state_dict": self.optimizer.state_dict(),
                 "scheduler_state_dict": self.scheduler.state_dict(), "loss": loss, "config": self.config}
+        if best_loss is not None:
+            ckpt["best_loss"], ckpt["patience"] = float(best_loss), int(patience or 0)
+        if self.scaler is not None:
+            ckpt["scaler_state_dict"] = self.scaler.state_dict()
         torch.save(ckpt, os.path.join(self.config["save_dir"], "latest_checkpoint.pth"))
         if is_best:
             torch.save(self.model.state_dict(),
@@ -188,8 +242,10 @@ class BaseTrainer:
 
     def load_checkpoint(self, path: str):
         """Resume from a ``save_checkpoint`` file (ours or the reference's: same keys, Adam
-        state in torch.optim.Adam's format): model, optimizer and ReduceLROnPlateau state.
-        Returns ``(epoch, loss)``; ``train(start_epoch=epoch)`` continues from there."""
+        state in torch.optim.Adam's format): model, optimizer and ReduceLROnPlateau state,
+        and the early-stopping state (ours: ``best_loss`` / ``patience``; the reference's
+        files: the saved ``loss`` as the best so far).  Returns ``(epoch, loss)``;
+        ``train(start_epoch=epoch)`` continues from there."""
         ckpt = torch.load(path, map_location=self.device, weights_only=True)
         self.model.load_state_dict(ckpt["model_state_dict"])
         self.model.engine().mark_dirty()
@@ -197,24 +253,48 @@ class BaseTrainer:
             self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
         if "scheduler_state_dict" in ckpt:
             self.scheduler.load_state_dict(ckpt["scheduler_state_dict"])
-        return int(ckpt.get("epoch", 0)), ckpt.get("loss")
+        if self.scaler is not None and "scaler_state_dict" in ckpt:
+            self.scaler.load_state_dict(ckpt["scaler_state_dict"])
+        loss = ckpt.get("loss")
+        best = ckpt.get("best_loss", loss if loss is not None else float("inf"))
+        self._resume = (float(best), int(ckpt.get("patience", 0)))
+        return int(ckpt.get("epoch", 0)), loss
 
-    def train(self, start_epoch: int = 0):
-        """Epoch loop with ReduceLROnPlateau and early stopping at patience 20 (:280-345)."""
-        best, patience = float("inf"), 0
+    def _mean_over_ranks(self, v):
+        """The epoch loss every rank acts on: the mean over ranks (so ReduceLROnPlateau and
+        early stopping take the same decisions everywhere and no rank leaves the loop alone)."""
+        if v is None or not self.distributed:
+            return v
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.model.engine().flat_p.device)
+        dist.all_reduce(t)
+        return float(t) / self.world_size
+
+    def train(self, start_epoch: int = 0, best_loss: Optional[float] = None):
+        """Epoch loop with ReduceLROnPlateau and early stopping at patience 20 (:280-345).
+        ``best_loss`` defaults to the value a loaded checkpoint carried (else inf)."""
+        best, patience = self._resume
+        if best_loss is not None:
+            best, patience = float(best_loss), 0
         for epoch in range(start_epoch, self.config["num_epochs"]):
-            train_loss = self.train_epoch()
-            val_loss = self.validate_epoch()
+            for ld in (self.train_loader, self.val_loader):
+                sampler = getattr(ld, "sampler", None)
+                if hasattr(sampler, "set_epoch"):
+                    sampler.set_epoch(epoch)
+            train_loss = self._mean_over_ranks(self.train_epoch())
+            if self.distributed:  # validate with rank 0's running statistics everywhere
+                dist.broadcast(self.model.engine().flat_bn, src=0)
+            val_loss = self._mean_over_ranks(self.validate_epoch())
             cur = val_loss if val_loss is not None else train_loss
             self.scheduler.step(cur)
             if cur < best:
                 best, patience = cur, 0
                 if self.config.get("save_dir"):
-                    self.save_checkpoint(epoch + 1, cur, is_best=True)
+                    self.save_checkpoint(epoch + 1, cur, is_best=True, best_loss=best, patience=patience)
             else:
                 patience += 1
             if patience >= 20:
                 break
+        self._resume = (best, patience)
         return best
 
 

@@ -33,7 +33,7 @@ def main():
             elif name == "fwd":
                 L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W)
             else:
-                L.call("pcms_stem_wgrad", x, dy, dw, ws, 5, N, D, H, W, 256)
+                L.call("pcms_stem_wgrad", x, dy, dw, ws, 5, N, D, H, W)
         for i in range(3):
             f(i)
         torch.cuda.synchronize()

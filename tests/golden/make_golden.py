@@ -46,7 +46,11 @@ CASES = {
     "cfg1_dice": (1, 1, (64, 64, 32), "ellipsoid", "dice", 1e-4),
     "odd_bcedice": (1, 2, (20, 18, 24), "bernoulli", "bce_dice", 1e-4),
     "c16_ncls2_dice": (2, 2, (16, 16, 16), "bernoulli", "dice", 1e-4),
+    # config 4 (zero_fill missing modalities, script/data_loader.py:320-322): per sample 1-2
+    # of the 5 channels all-zero (synthetic.make_batch(zero_fill=True), randperm(5)[:k])
+    "zf_bcedice": (1, 2, (32, 32, 16), "ellipsoid", "bce_dice", 1e-4),
 }
+ZERO_FILL = {"zf_bcedice"}
 SAMPLE_MAX = 4096
 
 
@@ -67,6 +71,7 @@ def sample(t: torch.Tensor):
 
 
 def run_case(name, n_classes, n, spatial, lab_kind, loss_kind, lr):
+    zf = name in ZERO_FILL
     from models.unet3d import UNet3D            # reference
     from utils.losses import BCEDiceLoss, DiceLoss  # reference
 
@@ -78,7 +83,7 @@ def run_case(name, n_classes, n, spatial, lab_kind, loss_kind, lr):
     model.train()
     losses = []
     for step in range(2):
-        b = synthetic.make_batch(n, spatial, seed=synthetic.step_seed(0, step), label=lab_kind)
+        b = synthetic.make_batch(n, spatial, seed=synthetic.step_seed(0, step), label=lab_kind, zero_fill=zf)
         x, y = b["image"], b["label"]
         if n_classes != 1:
             y = y.repeat(1, n_classes, 1, 1, 1)
@@ -105,7 +110,8 @@ def run_case(name, n_classes, n, spatial, lab_kind, loss_kind, lr):
                     out["b__" + k] = v.detach().numpy().copy()
             model.eval()
             with torch.no_grad():
-                x0 = synthetic.make_batch(n, spatial, seed=synthetic.step_seed(0, 0), label=lab_kind)["image"]
+                x0 = synthetic.make_batch(n, spatial, seed=synthetic.step_seed(0, 0), label=lab_kind,
+                                          zero_fill=zf)["image"]
                 out["logits_eval"] = model(x0).numpy().copy()
             model.train()
     out["loss0"], out["loss1"] = np.array(losses[0]), np.array(losses[1])
@@ -116,7 +122,7 @@ def run_case(name, n_classes, n, spatial, lab_kind, loss_kind, lr):
     opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-5)
     model.train()
     for step in range(2):
-        b = synthetic.make_batch(n, spatial, seed=synthetic.step_seed(0, step), label=lab_kind)
+        b = synthetic.make_batch(n, spatial, seed=synthetic.step_seed(0, step), label=lab_kind, zero_fill=zf)
         x, y = b["image"].double(), b["label"].double()
         if n_classes != 1:
             y = y.repeat(1, n_classes, 1, 1, 1)

@@ -16,7 +16,9 @@ CASES = {
     "cfg1_dice": (1, 1, (64, 64, 32), "ellipsoid", "dice", 1e-4),
     "odd_bcedice": (1, 2, (20, 18, 24), "bernoulli", "bce_dice", 1e-4),
     "c16_ncls2_dice": (2, 2, (16, 16, 16), "bernoulli", "dice", 1e-4),
+    "zf_bcedice": (1, 2, (32, 32, 16), "ellipsoid", "bce_dice", 1e-4),
 }
+ZERO_FILL = {"zf_bcedice"}  # config 4: 1-2 of the 5 modalities zeroed per sample
 
 
 def load(name: str) -> dict:
@@ -49,7 +51,7 @@ def synthetic():
 def batch(name: str, step: int = 0):
     ncls, n, spatial, lab, _, _ = CASES[name]
     syn = synthetic()
-    b = syn.make_batch(n, spatial, seed=syn.step_seed(0, step), label=lab)
+    b = syn.make_batch(n, spatial, seed=syn.step_seed(0, step), label=lab, zero_fill=name in ZERO_FILL)
     x, y = b["image"], b["label"]
     if ncls != 1:
         y = y.repeat(1, ncls, 1, 1, 1)

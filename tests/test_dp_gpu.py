@@ -1,0 +1,92 @@
+"""The real data-parallel Trainer.step on the GPU: two ranks, one process each,
+sharing cuda:0 over gloo with CUDA tensors (RCCL needs one GPU per rank; the 8-GPU RCCL run
+is the driver's).  It runs every piece of utils/trainer.py's distributed branch: rank-0
+BatchNorm-buffer broadcast, the engine's module-completion hook driving the bucketed
+all-reduce beside the backward, the 1/world mean folded into Adam, optionally the fused
+gradient clip.  Checked against ``oracle.dp_step_simulated`` (DDP broadcast_buffers
+semantics around the reference step, utils/trainer.py:183-192): per-replica losses, the mean
+gradient left in param.grad, BatchNorm buffers = rank 0's, Adam-step parameters."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PRE_BN_BIAS = ("conv.0.bias", "conv.3.bias")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(tmp_path, world, clip=0.0):
+    out = str(tmp_path / "dp.pt")
+    port = str(_port())
+    env = dict(os.environ, CLIP=str(clip))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "tools", "dp_worker.py"), str(r), str(world), port,
+                               out], env=env) for r in range(world)]
+    rcs = [p.wait(timeout=240) for p in procs]
+    assert rcs == [0] * world, rcs
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.parametrize("clip", [0.0, 1.0])
+def test_dp_trainer_step_two_ranks(tmp_path, clip):
+    from oracle import unet3d_cpu as ref
+    from pcms_amd.synthetic import make_batch, step_seed
+    world = 2
+    r = _run(tmp_path, world, clip)
+    torch.manual_seed(0)
+    sd = ref.init_params(5, 1)
+    keys = ref.param_keys(sd)
+    shards = []
+    for rk in range(world):
+        b = make_batch(2, (32, 32, 16), seed=step_seed(rk, 0), label="bernoulli")
+        shards.append((b["image"], b["label"]))
+    # the simulation's replica losses and mean gradient, computed the way dp_step_simulated does
+    losses, grads = [], None
+    for img, lab in shards:
+        rep = {k: v.detach().clone() for k, v in sd.items()}
+        for k in keys:
+            rep[k].requires_grad_(True)
+        l = ref.bce_dice_loss(ref.forward(rep, img, training=True), lab)
+        l.backward()
+        losses.append(float(l))
+        g = torch.cat([rep[k].grad.reshape(-1) for k in keys])
+        grads = g if grads is None else grads + g
+    mean_g = grads / world
+    for rk in range(world):
+        assert abs(r["losses"][rk][0] - losses[rk]) <= 1e-5, (rk, r["losses"][rk][0], losses[rk])
+    norm = float(mean_g.double().norm())
+    coef = min(1.0, clip / (norm + 1e-6)) if clip > 0 else 1.0
+    if clip > 0:
+        assert abs(r["norm"] - norm) <= 1e-3 * norm, (r["norm"], norm)
+        assert coef < 1.0  # the clip engaged
+    # param.grad holds the DDP mean (x the clip coefficient) after optimizer.step()
+    off = 0
+    for k in keys:
+        n = sd[k].numel()
+        got, exp = r["grad"][off:off + n].double(), (mean_g[off:off + n] * coef).double()
+        off += n
+        if k.endswith(PRE_BN_BIAS):
+            assert got.abs().max() < 1e-4 * coef + 1e-12, k
+            continue
+        rl = float((got - exp).norm() / exp.norm().clamp_min(1e-30))
+        assert rl <= 5e-2, (k, rl)
+    # Adam's first step moves each weight by ~lr * sign(g): within 2 lr of the simulation
+    _, _ = ref.dp_step_simulated(sd, shards, lr=1e-4, loss="bce_dice") if clip == 0 else (None, None)
+    if clip == 0:
+        pv = torch.cat([sd[k].detach().reshape(-1) for k in keys])
+        assert float((r["params"] - pv).abs().max()) <= 2.01e-4
+        bn = torch.cat([sd[k].reshape(-1) for k in sd if k.endswith(("running_mean", "running_var"))])
+        np.testing.assert_allclose(r["bn"].numpy(), bn.numpy(), rtol=1e-4, atol=1e-5)

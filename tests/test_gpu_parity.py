@@ -19,7 +19,7 @@ from tests import golden_util as gu
 pytestmark = pytest.mark.gpu
 
 PRE_BN_BIAS = ("conv.0.bias", "conv.3.bias")  # exact grad 0, reference has noise
-GRAD_RL2 = {"c16_bcedice": 5e-2, "cfg1_dice": 5e-3, "odd_bcedice": 5e-2, "c16_ncls2_dice": 5e-2}
+GRAD_RL2 = {"c16_bcedice": 5e-2, "cfg1_dice": 5e-3, "odd_bcedice": 5e-2, "c16_ncls2_dice": 5e-2, "zf_bcedice": 5e-2}
 
 
 def _build(name, precision, ckpt=False):
@@ -107,8 +107,23 @@ def test_fp32_parity_full_step(name, ckpt):
     m.eval()
     with torch.no_grad():
         le = m(x.cuda()).cpu().numpy()
+    # (i) eval mode after the step vs the reference's own post-step eval logits: the 18
+    # pre-BN conv biases move by ~lr there from rounding-noise gradients and are
+    # exactly 0-gradient here, which shifts eval logits (running stats do not absorb it) --
+    # a loose bar
     ev_err = np.abs(le - g["logits_eval"]).max()
     assert ev_err <= 1e-2 * max(1.0, np.abs(g["logits_eval"]).max()), ev_err
+    # (ii) the eval forward itself, on THIS model's post-step weights and running stats, vs
+    # the CPU oracle (pinned to the reference by tests/test_oracle_golden.py) run on the
+    # same state: the north-star bar, 1e-3 logits and identical masks where |ref| >= 1e-3
+    from oracle import unet3d_cpu as ref_mod
+    osd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        lo = ref_mod.forward(osd, x, training=False).numpy()
+    ev2 = np.abs(le - lo).max()
+    assert ev2 <= 1e-3, ev2
+    sure = np.abs(lo) >= 1e-3
+    assert np.array_equal((le > 0)[sure], (lo > 0)[sure])
     m.train()
     x1, y1 = gu.batch(name, 1)
     opt.zero_grad()
@@ -120,7 +135,7 @@ def test_fp32_parity_full_step(name, ckpt):
 
 
 @pytest.mark.parametrize("name,ckpt", [("c16_bcedice", False), ("cfg1_dice", False), ("odd_bcedice", False),
-                                       ("cfg1_dice", True)])
+                                       ("cfg1_dice", True), ("zf_bcedice", False)])
 def test_bf16_parity_step(name, ckpt):
     g = gu.load(name)
     m = _build(name, "bf16", ckpt)
@@ -175,11 +190,11 @@ def test_shape_mismatch_and_cpu_refusal():
 
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_decoder_checkpointing_matches_plain_step(precision):
-    """Decoder activation checkpointing against the plain step, both with
-    unsplit convs (``engine.unsplit``; split-K adds fp32 partials in arrival order): the
-    first forward is bit-identical (same loss), the gradients agree to backward-summation
-    noise, the BatchNorm running stats are updated exactly once per step (the recompute
-    leaves them alone), and checkpointing keeps fewer buffers."""
+    """Decoder activation checkpointing against the plain step at a shape
+    whose deep levels run split-K: every reduction sums in a fixed order, so the recompute
+    reproduces the forward bit for bit and the whole step -- losses, every gradient, the
+    BatchNorm running stats (updated exactly once per step: the recompute leaves them
+    alone) -- is bit-identical; checkpointing keeps fewer buffers."""
     from pcms_amd.optim import FlatAdam
     from pcms_amd.utils.losses import BCEDiceLoss
     from pcms_amd.models.unet3d import UNet3D
@@ -187,10 +202,9 @@ def test_decoder_checkpointing_matches_plain_step(precision):
     for ckpt in (False, True):
         torch.manual_seed(0)
         m = UNet3D(n_modalities=5, n_classes=1, precision=precision, checkpoint_decoder=ckpt).cuda()
-        m.engine().unsplit = True
         opt = FlatAdam(m, lr=1e-4, weight_decay=1e-5)
         crit = BCEDiceLoss()
-        losses, grads = [], None
+        losses, grads = [], []
         for step in range(2):
             gen = torch.Generator().manual_seed(77 + step)
             x = torch.rand(2, 5, 32, 32, 32, generator=gen).cuda()
@@ -199,23 +213,20 @@ def test_decoder_checkpointing_matches_plain_step(precision):
             opt.zero_grad()
             loss = crit(m(x), y)
             loss.backward()
-            if step == 0:
-                grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+            grads.append(m.engine().flat_g.detach().clone())
             opt.step()
             losses.append(float(loss))
         eng = m.engine()
+        S, N = eng.bufs["S"], eng.buf_key[0]
+        assert any(eng._splits(N, S[l], 64 << l, 64 << l) > 1 for l in range(5)), "no split-K level at this shape"
         nbuf = sum(1 for k in eng.bufs if k.startswith("d") or k.startswith("ck_"))
         runs.append((losses, grads, {k: v.detach().clone() for k, v in m.state_dict().items()}, nbuf))
     (l0, g0, s0, n0), (l1, g1, s1, n1) = runs
-    bf = precision == "bf16"
-    assert l0[0] == l1[0], (l0, l1)
-    assert abs(l0[1] - l1[1]) <= (1e-3 if bf else 1e-5), (l0, l1)
-    for k in g0:
-        rl2 = float((g1[k] - g0[k]).float().norm() / g0[k].float().norm().clamp_min(1e-30))
-        assert rl2 <= (2e-2 if bf else 1e-5) or k.endswith(PRE_BN_BIAS), (k, rl2)
+    assert l0 == l1, (l0, l1)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
     for k in s0:
         if k.endswith("num_batches_tracked"):
             assert int(s0[k]) == int(s1[k]) == 2, k
-        elif "running" in k:
-            assert torch.allclose(s0[k], s1[k], rtol=1e-2 if bf else 1e-5, atol=5e-3 if bf else 1e-6), k
+        assert torch.equal(s0[k], s1[k]), k
     assert n1 < n0
