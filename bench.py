@@ -2,10 +2,14 @@
 BCEDiceLoss, Adam) on MI355X — SURVEY.md §8(d), BASELINE.json config 2 (N=1) / config 3
 (N=8, launched by torch.distributed.run, one process per GPU, RCCL all-reduce).
 
-One "step" = Trainer.step on resident synthetic inputs: forward + loss + backward +
-(all-reduce) + Adam.  Prints ONE JSON line (rank 0) with the roofline of the stem conv
+One "step" = Trainer.step on a synthetic batch held in pinned host memory: the H2D copy
+(issued one batch ahead on the trainer's copy stream, SURVEY §8d's unit of work) + forward +
+loss + backward + (all-reduce) + Adam.  Each step is bracketed by a device synchronize (and a
+barrier across ranks); the step time is the max over ranks and ``value`` uses the MEDIAN of
+the K timed steps.  Prints ONE JSON line (rank 0) with the roofline of the stem conv
 (forward + weight-gradient kernels, HBM-bound, 578.9 MB algorithmic at N=2) measured with
-HIP events, and the CPU oracle timed on the host cores (rank 0, N=1 only).
+HIP events, the fp32 parity build's rate, and the CPU oracle timed on the host cores
+(rank 0, N=1 only: 1 warm-up + 3 timed steps at the config batch, median).
 """
 from __future__ import annotations
 
@@ -13,6 +17,7 @@ import argparse
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
@@ -39,6 +44,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--zero-fill", action="store_true", help="config 4: 1-2 modalities zeroed")
     ap.add_argument("--ckpt-decoder", action="store_true", help="config 5: decoder activation checkpointing")
+    ap.add_argument("--fp32-steps", type=int, default=5, help="timed steps of the fp32 parity build (0: skip)")
     return ap.parse_args()
 
 
@@ -113,28 +119,66 @@ def stem_roofline(tr, N, spatial, reps):
             traffic = rec["traffic_bytes_per_pair"]
     return {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
-            "kernel": "stem conv3d 5->64 fwd + wgrad (stem_fwd_kernel + stem_wgrad_kernel)",
+            "kernel": "stem conv3d 5->64 fwd + wgrad (stem_fwd_direct_kernel + stem_wgrad_stream_kernel)",
             "algorithmic_bytes": fwd_bytes + wg_bytes, "t_fwd_us": round(res["fwd"] * 1e6, 1),
             "t_wgrad_us": round(res["wgrad"] * 1e6, 1)}
 
 
-def cpu_baseline(spatial):
+def cpu_baseline(n, spatial):
     """The CPU oracle (a restatement of utils/trainer.py:179-195 on torch CPU fp32) timed on
-    this host: one BCEDice train step of ONE volume (bounded sample, ~10-30 s)."""
+    this host at the config batch: 1 warm-up + 3 timed BCEDice train steps, median."""
     from oracle import unet3d_cpu as ref
-    from pcms_amd.synthetic import make_batch
+    from pcms_amd.synthetic import make_batch, step_seed
     cores = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
     torch.set_num_threads(cores)
     torch.manual_seed(0)
     sd = ref.init_params(5, 1)
     step = ref.RefStep(sd, lr=1e-4, loss="bce_dice")
-    b = make_batch(1, spatial, seed=1234)
-    t0 = time.perf_counter()
-    step.step(b["image"], b["label"])
-    dt = time.perf_counter() - t0
-    return {"value": round(1.0 / dt, 4), "unit": "volumes/s", "cores": cores, "kind": "port",
-            "sample": f"1 train step (fwd+BCEDice+bwd+Adam), batch 1 x 5x{'x'.join(map(str, spatial))}, "
-                      f"torch CPU fp32, {dt:.1f} s"}
+    times = []
+    for i in range(4):
+        b = make_batch(n, spatial, seed=step_seed(0, i))
+        t0 = time.perf_counter()
+        step.step(b["image"], b["label"])
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times[1:])
+    return {"value": round(n / med, 4), "unit": "volumes/s", "cores": cores, "kind": "port",
+            "sample": f"1 warm-up + 3 timed train steps (fwd+BCEDice+bwd+Adam), batch {n} x "
+                      f"5x{'x'.join(map(str, spatial))}, torch CPU fp32, median {med:.1f} s/step"}
+
+
+def _pinned_batches(n, spatial, rank, count, zero_fill):
+    from pcms_amd.synthetic import make_batch, step_seed
+    out = []
+    for i in range(count):
+        b = make_batch(n, spatial, seed=step_seed(rank, i), zero_fill=zero_fill)
+        out.append({"image": b["image"].pin_memory(), "label": b["label"].pin_memory(), "case_id": b["case_id"]})
+    return out
+
+
+def timed_steps(tr, host_batches, warmup, steps, world):
+    """Per-step wall times (s), each bracketed by a synchronize (+ barrier), max over ranks."""
+    def loader():
+        while True:
+            yield from host_batches
+    it = tr._prefetched(loader())
+    for _ in range(warmup):
+        tr.step_async(next(it))
+    torch.cuda.synchronize()
+    ts, last = [], None
+    for _ in range(steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        last = tr.step_async(next(it))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ts.append(time.perf_counter() - t0)
+    tt = torch.tensor(ts, device="cuda", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return tt.cpu().tolist(), last
 
 
 def main():
@@ -145,8 +189,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    import pcms_amd
-    from pcms_amd.synthetic import make_batch, step_seed
+    import pcms_amd  # noqa: F401
     from pcms_amd.utils.trainer import Trainer
 
     spatial = tuple(int(v) for v in a.size.split(","))
@@ -154,50 +197,45 @@ def main():
     cfg = {"device": f"cuda:{local}", "learning_rate": 1e-4, "batch_size": a.batch, "num_epochs": 1,
            "loss": "bce_dice", "precision": a.precision, "checkpoint_decoder": a.ckpt_decoder}
     tr = Trainer(cfg)
-    batches = []
-    for i in range(2):
-        b = make_batch(a.batch, spatial, seed=step_seed(rank, i), zero_fill=a.zero_fill)
-        batches.append({"image": b["image"].cuda(), "label": b["label"].cuda()})
-    for i in range(a.warmup):
-        tr.step_async(batches[i % 2])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    last = None
-    for i in range(a.steps):
-        last = tr.step_async(batches[i % 2])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    host = _pinned_batches(a.batch, spatial, rank, 2, a.zero_fill)
+    ts, last = timed_steps(tr, host, a.warmup, a.steps, world)
     loss = float(last) if last is not None else float("nan")
-    dtt = torch.tensor([dt], device="cuda", dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(dtt, op=dist.ReduceOp.MAX)
-    dt = float(dtt)
-    vols = world * a.batch * a.steps
-    value = vols / dt
+    med = statistics.median(ts)
+    vols_step = world * a.batch
+    value = vols_step / med
     roof = stem_roofline(tr, a.batch, spatial, a.kernel_reps) if rank == 0 else None
+    # the fp32 parity build (the one that meets the 1e-3 logit bar) on the same batches
+    fp32 = None
+    if a.fp32_steps > 0 and a.precision != "fp32":
+        del tr
+        torch.cuda.empty_cache()
+        torch.manual_seed(0)
+        tr32 = Trainer(dict(cfg, precision="fp32"))
+        ts32, _ = timed_steps(tr32, host, 2, a.fp32_steps, world)
+        fp32 = round(vols_step / statistics.median(ts32), 3)
+        del tr32
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(spatial)
+        cpu = cpu_baseline(a.batch, spatial)
     if rank == 0:
         vox = spatial[0] * spatial[1] * spatial[2]
-        flops = FLOP_PER_VOL * vox / (128 * 128 * 64) * vols
+        flops = FLOP_PER_VOL * vox / (128 * 128 * 64) * vols_step
+        size = "x".join(map(str, spatial))
         out = {
-            "metric": "train volumes/sec (5ch 128x128x64)", "value": round(value, 3), "unit": "volumes/s",
-            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "metric": f"train volumes/sec (5ch {size})", "value": round(value, 3), "unit": "volumes/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(med * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.precision,
-            "data": "synthetic (U[0,1) images, ellipsoid labels; random-init weights, seed 0)",
-            "config": {"workload": f"UNet3D 5->1, {a.batch} x 5x{'x'.join(map(str, spatial))} per GPU, "
+            "data": "synthetic (U[0,1) images, ellipsoid labels; random-init weights, seed 0), pinned host "
+                    "batches copied H2D inside each step (prefetched one step ahead)",
+            "config": {"workload": f"UNet3D 5->1, {a.batch} x 5x{size} per GPU, "
                                    f"BCEDiceLoss, Adam(1e-4, wd 1e-5){', zero_fill' if a.zero_fill else ''}"
                                    f"{', decoder checkpointing' if a.ckpt_decoder else ''}",
-                       "global_batch": world * a.batch, "parallelism": f"dp{world}"},
+                       "global_batch": vols_step, "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu,
-            "mfma_util_step": round(flops / dt / MFMA_BF16_PEAK, 4), "final_loss": round(loss, 5),
+            "mfma_util_step": round(flops / med / MFMA_BF16_PEAK, 4), "final_loss": round(loss, 5),
+            "step_ms": {"median": round(med * 1e3, 3), "mean": round(statistics.mean(ts) * 1e3, 3),
+                        "min": round(min(ts) * 1e3, 3), "max": round(max(ts) * 1e3, 3)},
+            "fp32_parity_build_value": fp32,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -33,49 +33,58 @@ __device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
   return (kd * HH + kh) * HW + kw;
 }
 
-// Persistent stem forward, direct-store variant for 16-wide 512-voxel boxes (bd x bh = 32).
-// No C tile: the weight columns are ordered so that lane r_lane of a wave holds channels
-// (2 r_lane, 2 r_lane + 1) of each of its rows, so the 32 lanes of a half-wave write one
-// voxel's 64 channels (128 contiguous bytes) with ONE buffer_store_dword, addressed by a
-// per-lane voffset (2 variants), a wave-uniform soffset and an immediate offset: no VALU
-// address math, no LDS round trip, one barrier per box.  The halo arrives by buffer LDS-DMA
-// (out-of-range voffset = zero padding); weights stay in VGPRs; BatchNorm partials are
-// accumulated over all boxes of the workgroup (shifted sums) and written as ONE stats row
-// per workgroup (rows >= gridDim.x are zeroed: count 0).
+// Persistent stem forward for 16-wide 512-voxel boxes (bd x bh = 32): one 8-wave workgroup
+// per CU walks boxes b = blockIdx.x + k gridDim.x; wave w computes the 64 voxels [64 w, 64 w
+// + 64) of each box (2 M-tiles x 2 N-tiles of v_mfma_f32_32x32x16_bf16, K = 14 tap-pair steps).
+//  * Stores: the weight columns are ordered so that lane r_lane holds channels (2 r_lane,
+//    2 r_lane + 1) of its rows, so the 32 lanes of a half-wave write one voxel's 64 channels
+//    (128 contiguous bytes) with ONE buffer_store_dword (per-lane voffset, wave-uniform
+//    soffset, immediate offset: no VALU address math, no LDS round trip).
+//  * Halo: double-buffered, buffer LDS-DMA (out-of-range voffset = zero padding), the next
+//    box's halo in flight while this one computes; one barrier per box.
+//  * Weights: in LDS (28 KiB, k-halves swapped on column bit 4: conflict-free reads).
+//  * Staggered epilogue: waves 0-3 do each box's epilogue (BN sums, bf16 packing, stores)
+//    right after its MFMAs; waves 4-7 defer theirs to the start of the NEXT box, so on every
+//    SIMD one wave's MFMAs run beside the other wave's vector / store work instead of the
+//    two waves doing the same phase at once (MFMA and VALU pipes are separate).
+//  * BatchNorm partials: shifted sums over all boxes of the workgroup, ONE stats row per
+//    workgroup (rows >= gridDim.x are zeroed: count 0).
 constexpr int kSDHaloRows = kHaloMax;                         // 1152 rows (18 x 64)
 constexpr int kSDHaloBytes = kSDHaloRows * 16;
-constexpr int kSDLds = 2 * kSDHaloBytes + 8 * 64 * 3 * 4;     // halo x2 + stats reduction
+constexpr int kSDW = 2 * kSDHaloBytes;                        // weights [14][64][32 B]
+constexpr int kSDRed = kSDW + kStemSteps * 64 * 32;
+constexpr int kSDLds = kSDRed + 8 * 64 * 3 * 4;               // + stats reduction
 constexpr int kSDThr = 512;                                   // one 8-wave workgroup per CU
 
 template <int LBD, int LBH>
 __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
                                                                     uint32_t xbytes, uint32_t ybytes) {
-  constexpr int THR = kSDThr;
-  constexpr int kSDThreads = THR, NWV = THR / 64;
+  constexpr int NWV = kSDThr / 64;
   static_assert((1 << (LBD + LBH + 4)) == NWV * 64, "box = 64 voxels per wave");
   constexpr int bd = 1 << LBD, bh = 1 << LBH, bw = 16;
   constexpr int HH = bh + 2, HW = bw + 2, HV = (bd + 2) * HH * HW;
-  constexpr int NP = (HV + kSDThreads - 1) / kSDThreads;  // halo pieces per thread
+  constexpr int NP = (HV + kSDThr - 1) / kSDThr;  // halo pieces per thread
   static_assert(HV <= kSDHaloRows, "halo fits");
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* red = reinterpret_cast<float*>(lds + 2 * kSDHaloBytes);
+  float* red = reinterpret_cast<float*>(lds + kSDRed);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR math)
+  const bool late = wave >= 4;                                  // deferred-epilogue half
   const int r_lane = lane & 31, hsel = lane >> 5;
   const int D = p.D, H = p.H, W = p.W;
   const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x0, 0, xbytes, 0x00020000);
   const auto yr = __builtin_amdgcn_make_buffer_rsrc(p.y0, 0, ybytes, 0x00020000);
 
-  // weights: B fragments of all 14 k-steps in registers
-  s16x8_t wb[kStemSteps][2];
+  // weights -> LDS once (read after the first barrier): row (step, column) of 32 B, its two
+  // 16-B k-halves swapped when column bit 4 is set
   {
-    const bf16_t* wg = (const bf16_t*)p.w;
-#pragma unroll
-    for (int st = 0; st < kStemSteps; ++st) {
-      wb[st][0] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + r_lane) * 16 + hsel * 8);
-      wb[st][1] = *reinterpret_cast<const s16x8_t*>(wg + (st * 64 + 32 + r_lane) * 16 + hsel * 8);
+    const u32x4_t* wg = reinterpret_cast<const u32x4_t*>(p.w);
+    for (int i = tid; i < kStemSteps * 64 * 2; i += kSDThr) {
+      const int row = i >> 1, half = i & 1, col = row & 63;
+      *reinterpret_cast<u32x4_t*>(lds + kSDW + row * 32 + ((half ^ ((col >> 4) & 1)) * 16)) = wg[i];
     }
   }
+  const char* wl = lds + kSDW + r_lane * 32 + ((hsel ^ ((r_lane >> 4) & 1)) * 16);
   float bias_l[2] = {0.f, 0.f};
   if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
   // halo rows of the two 32-row MFMA tiles (perm32 layout)
@@ -90,7 +99,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   int prel[NP], pco[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-    const int hv = tid + i * kSDThreads;
+    const int hv = tid + i * kSDThr;
     const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
     prel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
     pco[i] = hv < HV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
@@ -117,7 +126,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
     const bool inner = d0 >= 1 && d0 + bd < D && h0 >= 1 && h0 + bh < H && w0 >= 1 && w0 + bw < W;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      if (wave * 64 + i * kSDThreads >= HV) break;  // whole wave past the halo (uniform)
+      if (wave * 64 + i * kSDThr >= HV) break;  // whole wave past the halo (uniform)
       uint32_t voff = (uint32_t)(base16 + prel[i]);
       const int c = pco[i];
       if (c < 0) {
@@ -126,56 +135,18 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
         if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (LDS_AS void*)(lds + buf * kSDHaloBytes + (wave * 64 + i * kSDThreads) * 16),
-                                           16, voff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (LDS_AS void*)(lds + buf * kSDHaloBytes + (wave * 64 + i * kSDThr) * 16),
+                                               16, voff, 0, 0, 0);
     }
   };
 
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2] = {0.f, 0.f};
   float cnt = 0.f;
   bool first = true;
-  int b = blockIdx.x;
-  if (b < nbox) stage(b, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
-    // halo(b) has landed for this wave (vmcnt above / at the loop end); barrier: for all
-    // waves, and every wave is done reading the buffer the next DMA overwrites
-    __syncthreads();
-    const int bn = b + gridDim.x;
-    if (bn < nbox) stage(bn, (it + 1) & 1);
-    const char* hl = lds + (it & 1) * kSDHaloBytes;
-    f32x16_t acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];
-    {
-      int hs16 = hsel * 16;
-      asm volatile("" : "+v"(hs16));
-      auto load_a = [&](int st, s16x8_t (&a)[2]) {
-        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
-        const int off16 = o0 * 16 + hs16 * (o1 - o0);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + off16);
-      };
-      s16x8_t abuf[2][2];
-      load_a(0, abuf[0]);
-#pragma unroll
-      for (int st = 0; st < kStemSteps; ++st) {
-        if (st + 1 < kStemSteps) load_a(st + 1, abuf[(st + 1) & 1]);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          acc[mt][0] = mfma(abuf[st & 1][mt], wb[st][0], acc[mt][0]);
-          acc[mt][1] = mfma(abuf[st & 1][mt], wb[st][1], acc[mt][1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // ---- epilogue: direct stores + shifted BN sums ----
+  // epilogue of one box: packed channel-pair stores + shifted BN sums
+  auto epilogue = [&](f32x16_t (&acc)[2][2], int bb) {
     int n, d0, h0, w0;
-    origin(b, n, d0, h0, w0);
+    origin(bb, n, d0, h0, w0);
     const bool full = d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
     if (first) {
 #pragma unroll
@@ -204,14 +175,79 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
           cnt += valid ? 1.f : 0.f;
         }
         __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so + rw * 128, 0);
-        s1[0] += e0; s2[0] += e0 * e0;
-        s1[1] += e1; s2[1] += e1 * e1;
+        s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
+        s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
       }
     }
     if (full) cnt += 32.f;
-    // the next halo's DMA was issued before this box's 32 stores
-    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  };
+
+  f32x16_t prev[2][2];
+  int pb = -1;  // box whose epilogue a late wave still owes
+  int b = blockIdx.x;
+  if (b < nbox) stage(b, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
+    // halo(b) has landed for this wave (vmcnt at the loop end); barrier: for all waves, and
+    // every wave is done reading the buffer the next DMA overwrites
+    __syncthreads();
+    const int bn = b + gridDim.x;
+    if (bn < nbox) stage(bn, (it + 1) & 1);
+    if (late && pb >= 0) epilogue(prev, pb);
+    const char* hl = lds + (it & 1) * kSDHaloBytes;
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];
+    {
+      int hs16 = hsel * 16;
+      asm volatile("" : "+v"(hs16));
+      auto load_a = [&](int st, s16x8_t (&a)[2]) {
+        const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
+        const int off16 = o0 * 16 + hs16 * (o1 - o0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(hl + hb16[mt] + off16);
+      };
+      auto load_b = [&](int st, s16x8_t (&w)[2]) {
+        w[0] = *reinterpret_cast<const s16x8_t*>(wl + st * 64 * 32);
+        w[1] = *reinterpret_cast<const s16x8_t*>(wl + (st * 64 + 32) * 32);
+      };
+      s16x8_t abuf[2][2], bbuf[2][2];
+      load_a(0, abuf[0]);
+      load_b(0, bbuf[0]);
+#pragma unroll
+      for (int st = 0; st < kStemSteps; ++st) {
+        if (st + 1 < kStemSteps) {
+          load_a(st + 1, abuf[(st + 1) & 1]);
+          load_b(st + 1, bbuf[(st + 1) & 1]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          acc[mt][0] = mfma(abuf[st & 1][mt], bbuf[st & 1][0], acc[mt][0]);
+          acc[mt][1] = mfma(abuf[st & 1][mt], bbuf[st & 1][1], acc[mt][1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (late) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) prev[i][j] = acc[i][j];
+      pb = b;
+    } else {
+      epilogue(acc, b);
+    }
+    // the next halo's DMA was issued before this box's 32 stores (a late wave: before the
+    // previous box's 32 stores, its only stores since; none in its first iteration)
+    if (late && it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
   }
+  if (late && pb >= 0) epilogue(prev, pb);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!p.stats) return;
   // per wave (lanes r_lane and r_lane + 32 share channels and K): S = sum d + n K,
   // M2 = sum d^2 - (sum d)^2 / n; then Chan across the 8 waves
@@ -285,9 +321,11 @@ template <int BD> struct SWGeom {
 };
 constexpr int kSWBD = 4;  // box depth (2-deep boxes in 6 slots measured slower)
 constexpr int kSWNS = kSWBD == 4 ? 3 : 6;
-constexpr int kSWLds = kSWNS * SWGeom<kSWBD>::Buf;
-static_assert(kSWLds >= 64 * 224 * 4, "flush tile fits in the ring");
-static_assert(kSWLds <= 160 * 1024, "ring fits in LDS");
+constexpr int kSWLaneStride = 20;                        // flush: floats per lane (16 used)
+constexpr int kSWRegion = 14 * 64 * kSWLaneStride * 4;   // one wave's 14 tiles, lane-major
+constexpr int kSWRing = kSWNS * SWGeom<kSWBD>::Buf;
+constexpr int kSWLds = kSWRing > 2 * kSWRegion ? kSWRing : 2 * kSWRegion;
+static_assert(kSWLds <= 160 * 1024, "ring / flush regions fit in LDS");
 
 template <int BD, int NS>
 __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t* x, const bf16_t* dy, float* part,
@@ -426,29 +464,53 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // flush: the 4 waves' partial tiles summed in LDS [co][224 cols] (fixed order)
-  float* red = reinterpret_cast<float*>(swl);
-  for (int pass = 0; pass < 4; ++pass) {
-    if (wave == pass) {
+  // flush, two stages: waves 0 / 1 store their 14 tiles lane-major into regions 0 / 1 (16 of
+  // every 20 floats per lane: conflict-free ds_write_b128), waves 2 / 3 add theirs into the
+  // same regions, then every thread writes region 0 + region 1 into the partial row (a
+  // fixed summation order: (w0 + w2) + (w1 + w3))
+  float* reg = reinterpret_cast<float*>(swl) + (wave & 1) * (kSWRegion / 4);
+  if (wave < 2) {
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
+    for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-        for (int j = 0; j < 7; ++j)
+      for (int j = 0; j < 7; ++j) {
+        float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int co = ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
-            float* dst = red + co * 224 + j * 32 + (lane & 31);
-            if (pass == 0) *dst = acc[ct][j][e];
-            else *dst += acc[ct][j][e];
-          }
-    }
-    __syncthreads();
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4_t*>(dst + 4 * q) =
+              (f32x4_t){acc[ct][j][4 * q], acc[ct][j][4 * q + 1], acc[ct][j][4 * q + 2], acc[ct][j][4 * q + 3]};
+      }
   }
-  const int total = 64 * cin_w * 27;
+  __syncthreads();
+  if (wave >= 2) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4_t v = *reinterpret_cast<f32x4_t*>(dst + 4 * q);
+          v += (f32x4_t){acc[ct][j][4 * q], acc[ct][j][4 * q + 1], acc[ct][j][4 * q + 2], acc[ct][j][4 * q + 3]};
+          *reinterpret_cast<f32x4_t*>(dst + 4 * q) = v;
+        }
+      }
+  }
+  __syncthreads();
+  // partial row [64 co][cin_w][27]: element (co, column 8 t + c) sits in tile (co >> 5, col >> 5),
+  // lane (col & 31) + 32 hs, register e, where (e & 3) + 8 (e >> 2) + 4 hs = co & 31
+  const float* r0 = reinterpret_cast<const float*>(swl);
+  const float* r1 = r0 + kSWRegion / 4;
+  const int per_co = cin_w * 27;
+  const int total = 64 * per_co;
   float* prow = part + (long)blockIdx.x * total;
   for (int i = tid; i < total; i += kSWT) {
-    const int t = i % 27, c = (i / 27) % cin_w, co = i / (27 * cin_w);
-    prow[i] = red[co * 224 + t * 8 + c];
+    const int co = i / per_co, rem = i - co * per_co;
+    const int c = rem / 27, t = rem - c * 27;
+    const int col = 8 * t + c;
+    const int cr = co & 31, hs = (cr >> 2) & 1, e = (cr & 3) + 4 * (cr >> 3);
+    prow[i] = r0[(((co >> 5) * 7 + (col >> 5)) * 64 + (col & 31) + 32 * hs) * kSWLaneStride + e] +
+              r1[(((co >> 5) * 7 + (col >> 5)) * 64 + (col & 31) + 32 * hs) * kSWLaneStride + e];
   }
 }
 
@@ -499,7 +561,10 @@ int pcms_stem_supported(int N, int D, int H, int W) {
 }
 
 // BatchNorm statistics rows pcms_stem_fwd writes
-int pcms_stem_fwd_rows(int N, int D, int H, int W) { return pcms_conv3_mblocks(N, D, H, W); }
+int pcms_stem_fwd_rows(int N, int D, int H, int W) {
+  const Box b = fwd_box(D, H, W);
+  return N * cdiv(D, 1 << b.lbd) * cdiv(H, 1 << b.lbh) * cdiv(W, 1 << b.lbw);
+}
 
 // x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_stem_fwd_rows
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,

@@ -1,0 +1,152 @@
+"""The step variants of the reference's other trainers:
+
+* grad clip: ``torch.nn.utils.clip_grad_norm_(params, max_norm=1.0)`` before Adam
+  (train_bph.py:166, train_bph_cv.py:311) -> pcms_grad_clip (fused norm, coefficient folded
+  into the Adam kernel, or applied in place by ``pcms_amd.amp.clip_grad_norm_``);
+* mixed precision: ``GradScaler('cuda')`` + ``scaler.scale(loss).backward();
+  scaler.step(opt); scaler.update()`` (train_bph_optimized.py:248-298);
+* K-fold splits: ``get_kfold_splits`` = sklearn KFold(shuffle, random_state=42)
+  (script/data_loader.py:468-497).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+
+def test_kfold_matches_sklearn():
+    from sklearn.model_selection import KFold
+    from pcms_amd.data import kfold_indices
+    for n, k in [(10, 5), (23, 5), (7, 3), (5, 5)]:
+        ours = kfold_indices(n, k)
+        ref = list(KFold(n_splits=k, shuffle=True, random_state=42).split(range(n)))
+        assert len(ours) == len(ref)
+        for (a_tr, a_va), (b_tr, b_va) in zip(ours, ref):
+            assert np.array_equal(a_tr, b_tr) and np.array_equal(a_va, b_va)
+    with pytest.raises(ValueError):
+        kfold_indices(3, 5)
+
+
+def test_get_kfold_splits_scans_case_list(tmp_path):
+    from pcms_amd.data import get_kfold_splits, write_nifti
+    adc = tmp_path / "BPH-PCA" / "BPH" / "ADC"
+    adc.mkdir(parents=True)
+    for i in range(6):
+        write_nifti(str(adc / f"case{i}.nii"), np.zeros((2, 2, 2), np.float32))
+    splits = get_kfold_splits(str(tmp_path), n_splits=3)
+    assert len(splits) == 3
+    assert sorted(np.concatenate([va for _, va in splits]).tolist()) == list(range(6))
+
+
+def _model_and_grads(seed=0):
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    torch.manual_seed(seed)
+    m = UNet3D(n_modalities=5, n_classes=1, precision="fp32").cuda()
+    opt = FlatAdam(m, lr=1e-4, weight_decay=1e-5)
+    gen = torch.Generator().manual_seed(5)
+    x = torch.rand(2, 5, 16, 16, 16, generator=gen).cuda()
+    y = (torch.rand(2, 1, 16, 16, 16, generator=gen) < 0.5).float().cuda()
+    opt.zero_grad()
+    BCEDiceLoss()(m(x), y).backward()
+    return m, opt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_norm", [1e-3, 1e6])
+def test_clip_grad_norm_matches_torch(max_norm):
+    """clip_grad_norm_ semantics: total 2-norm over every gradient, coefficient
+    min(1, max_norm / (norm + 1e-6)) applied in place.  The reference norm is taken in fp64
+    (torch's own fp32 per-tensor CPU norms carry ~1e-4 relative summation error over these
+    multi-million-element tensors; the kernel sums fp64 partials)."""
+    from pcms_amd.amp import clip_grad_norm_
+    m, _ = _model_and_grads()
+    g = [p.grad.detach().cpu().clone() for p in m.parameters()]
+    ref_norm = float(torch.cat([t.double().reshape(-1) for t in g]).norm())
+    coef = min(1.0, max_norm / (ref_norm + 1e-6))
+    # torch's own function on the same gradients agrees within its fp32 summation error
+    ref_params = [torch.zeros_like(t, requires_grad=True) for t in g]
+    for p, t in zip(ref_params, g):
+        p.grad = t.clone()
+    assert abs(float(torch.nn.utils.clip_grad_norm_(ref_params, max_norm=max_norm)) - ref_norm) <= 1e-3 * ref_norm
+    norm = clip_grad_norm_(m, max_norm)
+    torch.cuda.synchronize()
+    assert abs(float(norm) - ref_norm) <= 1e-6 * ref_norm
+    for p, t in zip(m.parameters(), g):
+        torch.testing.assert_close(p.grad.cpu(), t * coef, rtol=2e-6, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_trainer_clip_step_equals_clip_then_adam():
+    """Trainer(max_grad_norm=1.0).step == backward, clip_grad_norm_(1.0), Adam (the clip
+    coefficient folded into the Adam kernel instead of an extra pass)."""
+    from pcms_amd.amp import clip_grad_norm_
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    from pcms_amd.utils.trainer import Trainer
+    gen = torch.Generator().manual_seed(9)
+    batch = {"image": torch.rand(2, 5, 16, 16, 16, generator=gen),
+             "label": (torch.rand(2, 1, 16, 16, 16, generator=gen) < 0.5).float()}
+    cfg = {"device": "cuda", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1, "loss": "bce_dice",
+           "precision": "fp32", "max_grad_norm": 1.0}
+    torch.manual_seed(0)
+    tr = Trainer(cfg)
+    l0 = tr.step(batch)
+    torch.manual_seed(0)
+    from pcms_amd.models.unet3d import UNet3D
+    m = UNet3D(n_modalities=5, n_classes=1, precision="fp32").cuda()
+    opt = FlatAdam(m, lr=1e-4, weight_decay=1e-5)
+    opt.zero_grad()
+    loss = BCEDiceLoss()(m(batch["image"].cuda()), batch["label"].cuda())
+    loss.backward()
+    norm = clip_grad_norm_(m, 1.0)
+    opt.step()
+    assert float(loss) == l0
+    assert float(norm) > 1.0  # the clip engaged at init
+    assert float(tr.last_grad_norm) == pytest.approx(float(norm), rel=1e-6)
+    for (k, a), b in zip(tr.model.named_parameters(), m.parameters()):
+        torch.testing.assert_close(a, b, rtol=0, atol=1e-7, msg=k)
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-12, msg=k)
+
+
+@pytest.mark.gpu
+def test_grad_scaler_step_skip_and_scale_update():
+    from pcms_amd.amp import GradScaler
+    from pcms_amd.utils.trainer import Trainer
+    gen = torch.Generator().manual_seed(9)
+    batch = {"image": torch.rand(2, 5, 16, 16, 16, generator=gen),
+             "label": (torch.rand(2, 1, 16, 16, 16, generator=gen) < 0.5).float()}
+    base = {"device": "cuda", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1, "loss": "bce_dice",
+            "precision": "bf16"}
+    torch.manual_seed(0)
+    plain = Trainer(base)
+    torch.manual_seed(0)
+    amp = Trainer(dict(base, use_amp=True))
+    assert isinstance(amp.scaler, GradScaler) and amp.scaler.get_scale() == 2.0 ** 16
+    l_plain, l_amp = plain.step(batch), amp.step(batch)
+    assert l_plain == l_amp  # the returned loss is the unscaled one
+    # a power-of-two loss scale unscales exactly: same update as the unscaled step, up to
+    # the bf16 rounding of the scaled activation gradients
+    for (k, a), b in zip(plain.model.named_parameters(), amp.model.parameters()):
+        assert torch.allclose(a, b, rtol=0, atol=2.01e-4), k
+    assert amp.scaler.get_scale() == 2.0 ** 16
+    # an inf gradient: the step is skipped, the scale backs off
+    p_before = amp.model.engine().flat_p.clone()
+    sc = amp.scaler
+    eng = amp.model.engine()
+    amp.optimizer.zero_grad()
+    eng.flat_g[123] = float("inf")
+    sc.unscale_(amp.optimizer)
+    sc.step(amp.optimizer)
+    sc.update()
+    assert torch.equal(eng.flat_p, p_before)
+    assert sc.get_scale() == 2.0 ** 15
+    # growth after growth_interval clean steps
+    sc.growth_interval = 2
+    for _ in range(2):
+        amp.step(batch)
+    assert sc.get_scale() == 2.0 ** 16
+    assert math.isfinite(float(amp.last_grad_norm))
