@@ -129,8 +129,10 @@ int pcms_box_channel_sum(int dtype, const void* x, float* out, float* ws, int N,
                          int z0, int y0, int x0, int bd, int bh, int bw, hipStream_t s);
 
 /* ---- outc Conv3d(64, ncls, 1): models/unet3d.py:222,295 ---------------------------- */
-int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* logits,
-                  long nvox_per_n, int N, int ncls, hipStream_t s);
+/* act 0: logits; 1: sigmoid (UNet3D.predict, :298-318); 2: sigmoid > thr as 0 / 1 floats
+ * (UNet3D.inference, :320-344)                                                           */
+int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* out,
+                  long nvox_per_n, int N, int ncls, int act, float thr, hipStream_t s);
 /* da = dlogits . w (written); dw / db += (per-block partial rows in ws, fixed-order sum);
  * ws: pcms_head_bwd_ws_floats(...) fp32                                                  */
 int pcms_head_bwd_ws_floats(long nvox_per_n, int N, int ncls);
@@ -163,6 +165,9 @@ int pcms_grad_clip(float* g, long n, float gscale, float max_norm, int apply, do
 
 /* ---- misc -------------------------------------------------------------------------- */
 int pcms_add(int dtype, void* dst, const void* src, long n, hipStream_t s);
+/* NDHWC (Cs stored channels) -> NCDHW fp32 (first C channels): the sub-module outputs
+ * (DoubleConv3D / Down3D / Up3D called on their own, models/unet3d.py:42-158)          */
+int pcms_unpack_output(int dtype, const void* in, float* out, int N, int C, int Cs, long V, hipStream_t s);
 
 #ifdef __cplusplus
 }

@@ -51,7 +51,7 @@ SIGNATURES = {
     "pcms_convt_wgrad": "ippppiiiiiiiiiis",
     "pcms_box_channel_sum_ws_floats": "iiiiii",
     "pcms_box_channel_sum": "ipppiiiiiiiiiiis",
-    "pcms_head_fwd": "ippppliis",
+    "pcms_head_fwd": "ippppliiifs",
     "pcms_head_bwd_ws_floats": "lii",
     "pcms_head_bwd": "ipppppppliis",
     "pcms_loss_rows": "l",
@@ -61,6 +61,7 @@ SIGNATURES = {
     "pcms_grad_clip_ws_doubles": "",
     "pcms_grad_clip": "plffippps",
     "pcms_add": "ippls",
+    "pcms_unpack_output": "ippiiils",
 }
 
 _CT = {"i": ctypes.c_int, "l": ctypes.c_long, "d": ctypes.c_double, "f": ctypes.c_float,

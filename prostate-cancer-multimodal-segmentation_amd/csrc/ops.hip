@@ -339,10 +339,12 @@ __global__ void __launch_bounds__(256) rows_sum_kernel(const float* part, int ro
 }
 
 // ---------------- output head: logits (NCDHW fp32) = b + a . w ----------------
-// 8 lanes per voxel, 8 channels each (Cin = 64)
+// 8 lanes per voxel, 8 channels each (Cin = 64).  act 0: logits; 1: sigmoid(logits)
+// (UNet3D.predict, models/unet3d.py:298-318); 2: (sigmoid(logits) > thr) as 0 / 1
+// (UNet3D.inference, :320-344) -- the eval outputs leave the head kernel finished.
 template <typename T>
 __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, float* logits,
-                                long nvox_per_n, int N, int ncls) {
+                                long nvox_per_n, int N, int ncls, int act, float thr) {
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7;
   for (long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3; v < total;
@@ -362,7 +364,14 @@ __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, floa
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
       s += __shfl_xor(s, 4, 64);
-      if (sub == 0) logits[(n * ncls + k) * nvox_per_n + vv] = s + b[k];
+      if (sub == 0) {
+        float o = s + b[k];
+        if (act != 0) {
+          const float pr = 1.f / (1.f + expf(-o));
+          o = act == 1 ? pr : (pr > thr ? 1.f : 0.f);
+        }
+        logits[(n * ncls + k) * nvox_per_n + vv] = o;
+      }
     }
   }
 }
@@ -627,6 +636,18 @@ __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, i
   }
 }
 
+// ---------------- NDHWC (T, Cs stored channels) -> NCDHW fp32, first C channels ----------
+template <typename T>
+__global__ void unpack_output_kernel(const T* in, float* out, int N, int C, int Cs, long V) {
+  const long total = (long)N * C * V;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long v = i % V, nc = i / V;
+    const int c = (int)(nc % C);
+    const long n = nc / C;
+    out[i] = Elem<T>::ld(in + (n * V + v) * Cs + c);
+  }
+}
+
 template <typename T>
 __global__ void add_kernel(T* dst, const T* src, long nvec) {
   constexpr int VEC = Elem<T>::kVec;
@@ -767,12 +788,13 @@ int pcms_box_channel_sum(int dtype, const void* x, float* out, float* ws, int N,
   PCMS_CHECK_LAUNCH();
 }
 
-int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* logits, long nvox_per_n, int N,
-                  int ncls, hipStream_t s) {
+int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* out, long nvox_per_n, int N,
+                  int ncls, int act, float thr, hipStream_t s) {
   if ((long)N * nvox_per_n >= (1L << 31)) return -7;  // 32-bit index math in the kernel
+  if (act < 0 || act > 2) return -1;
   const int grid = grid_for((long)N * nvox_per_n * 8, TPB);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, w, b, logits, nvox_per_n, N, ncls);
-  else hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, w, b, logits, nvox_per_n, N, ncls);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
+  else hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -853,6 +875,14 @@ int pcms_split_epilogue(int dtype, const float* acc, int splits, const float* bi
   dim3 grid(cdiv(nvox, 64), C / 64);
   if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(TPB), 0, s, acc, splits, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox);
   else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(TPB), 0, s, acc, splits, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_unpack_output(int dtype, const void* in, float* out, int N, int C, int Cs, long V, hipStream_t s) {
+  if (C > Cs) return -1;
+  const int grid = grid_for((long)N * C * V, TPB);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(unpack_output_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)in, out, N, C, Cs, V);
+  else hipLaunchKernelGGL(unpack_output_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)in, out, N, C, Cs, V);
   PCMS_CHECK_LAUNCH();
 }
 

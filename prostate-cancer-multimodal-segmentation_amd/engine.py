@@ -396,7 +396,10 @@ class UNetEngine:
         return {"y1": b["ck_y1"][:n], "a1": b["ck_a1"][:n], "y2": b["ck_y2"][:n], "a2": b[f"d{l}_a2"]}
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x: torch.Tensor, training: bool) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, training: bool, act: int = 0, threshold: float = 0.5) -> torch.Tensor:
+        """The network on ``x`` (N, n_modalities, D, H, W).  ``act``: 0 logits, 1 sigmoid
+        probabilities (predict), 2 ``sigmoid > threshold`` masks (inference), all produced
+        by the head kernel."""
         if x.dim() != 5 or x.shape[1] != self.nmod:
             raise ValueError(f"expected input (N, {self.nmod}, D, H, W), got {tuple(x.shape)}")
         if x.device != self.device:
@@ -431,7 +434,8 @@ class UNetEngine:
             h = b[f"d{l}_a2"]
         logits = torch.empty((N, self.ncls, D, H, W), dtype=torch.float32, device=self.device)
         oc = self.model.outc
-        call("pcms_head_fwd", self.code, h, oc.weight, oc.bias, logits, D * H * W, N, self.ncls)
+        call("pcms_head_fwd", self.code, h, oc.weight, oc.bias, logits, D * H * W, N, self.ncls, int(act),
+             float(threshold))
         self.epoch += 1
         if training:
             self.saved_epoch = self.epoch

@@ -9,8 +9,10 @@ the same ``forward`` / ``predict`` / ``inference`` semantics (models/unet3d.py:2
 
 What differs is where it runs: ``forward`` executes the whole network on a ROCm device via
 ``pcms_amd.engine.UNetEngine`` (NDHWC bf16 by default, or fp32 with
-``precision="fp32"``); there is no CPU path.  The submodules are parameter containers for
-checkpoint compatibility — only ``UNet3D.forward`` is the hot path.
+``precision="fp32"``); there is no CPU path.  ``predict`` / ``inference`` get their
+sigmoid / threshold from the output-head kernel.  The sub-modules ``DoubleConv3D``,
+``Down3D`` and ``Up3D`` are callable on their own (forward, train or eval BatchNorm, through
+``pcms_amd.blocks``); training runs through ``UNet3D.forward`` as a whole.
 """
 from __future__ import annotations
 
@@ -19,6 +21,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
+from .. import blocks
 from ..engine import UNetEngine
 
 
@@ -36,8 +39,8 @@ class DoubleConv3D(nn.Module):
             nn.ReLU(inplace=True),
         )
 
-    def forward(self, x):  # pragma: no cover - container only
-        raise RuntimeError("pcms_amd executes the U-Net as a whole: call UNet3D.forward")
+    def forward(self, x):
+        return blocks.double_conv_forward(self, x)
 
 
 class Down3D(nn.Module):
@@ -47,8 +50,8 @@ class Down3D(nn.Module):
         super().__init__()
         self.maxpool_conv = nn.Sequential(nn.MaxPool3d(2), DoubleConv3D(in_channels, out_channels))
 
-    def forward(self, x):  # pragma: no cover
-        raise RuntimeError("pcms_amd executes the U-Net as a whole: call UNet3D.forward")
+    def forward(self, x):
+        return blocks.down_forward(self, x)
 
 
 class Up3D(nn.Module):
@@ -59,8 +62,8 @@ class Up3D(nn.Module):
         self.up = nn.ConvTranspose3d(in_channels, in_channels // 2, kernel_size=2, stride=2)
         self.conv = DoubleConv3D(in_channels, out_channels)
 
-    def forward(self, x1, x2):  # pragma: no cover
-        raise RuntimeError("pcms_amd executes the U-Net as a whole: call UNet3D.forward")
+    def forward(self, x1, x2):
+        return blocks.up_forward(self, x1, x2)
 
 
 class _UNetFunction(torch.autograd.Function):
@@ -114,6 +117,9 @@ class UNet3D(nn.Module):
         self.up3 = Up3D(f * 4, f * 2)
         self.up4 = Up3D(f * 2, f)
         self.outc = nn.Conv3d(f, n_classes, kernel_size=1)
+        for m in self.modules():  # storage type of the sub-modules' stand-alone forward
+            if isinstance(m, (DoubleConv3D, Down3D, Up3D)):
+                m.precision = precision
         self._init_weights()
         self._engine: Optional[UNetEngine] = None
 
@@ -155,17 +161,18 @@ class UNet3D(nn.Module):
             return eng.forward(x, training=self.training)
 
     def predict(self, x):
-        """eval + no_grad + sigmoid (models/unet3d.py:298-318)."""
+        """eval + no_grad + sigmoid (models/unet3d.py:298-318); the sigmoid runs in the head
+        kernel."""
         self.eval()
         with torch.no_grad():
-            return torch.sigmoid(self(x))
+            return self.engine().forward(x, training=False, act=1)
 
     def inference(self, x, threshold: float = 0.5):
-        """Binary mask ``sigmoid(logits) > threshold`` as float (models/unet3d.py:320-344)."""
+        """Binary mask ``sigmoid(logits) > threshold`` as float (models/unet3d.py:320-344),
+        thresholded in the head kernel."""
         self.eval()
         with torch.no_grad():
-            probs = torch.sigmoid(self(x))
-            return (probs > threshold).float()
+            return self.engine().forward(x, training=False, act=2, threshold=threshold)
 
 
 def load_weights(model: UNet3D, checkpoint) -> UNet3D:

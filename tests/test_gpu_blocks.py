@@ -1,0 +1,199 @@
+"""Stand-alone sub-modules, the head activations and the predict / validate pipelines on the
+HIP kernels, against the CPU oracle (oracle/unet3d_cpu.py) in fp32.
+
+* ``DoubleConv3D(x)``, ``Down3D(x)``, ``Up3D(x1, x2)`` called on their own
+  (models/unet3d.py:42-55, 85-96, 124-158), train BatchNorm (batch statistics + running-stat
+  update) and eval BatchNorm, including Up3D's asymmetric pad (:143-151);
+* ``UNet3D.predict`` (sigmoid in the head kernel) and ``inference`` (strict ``>`` threshold),
+  models/unet3d.py:298-344;
+* ``ModelPredictor`` (script/predict.py) and ``ModelValidator``'s JSON report
+  (script/validate_model.py:247-274).
+
+Tolerance: fp32 storage, 1e-3 absolute on unit-scale activations (the conv kernels sum 27*Cin
+products in a different order than the CPU's); masks must agree except where the oracle's
+probability sits within 1e-4 of the threshold.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet3d_cpu as ref
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-3
+
+
+def _sd(module, prefix):
+    return {prefix + "." + k: v.detach().cpu().clone() for k, v in module.state_dict().items()}
+
+
+def _bn_buffers(module):
+    return {k: v.detach().cpu() for k, v in module.state_dict().items()
+            if k.endswith(("running_mean", "running_var", "num_batches_tracked"))}
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_double_conv_matches_oracle(training):
+    from pcms_amd.models.unet3d import DoubleConv3D
+    torch.manual_seed(0)
+    m = DoubleConv3D(5, 64)
+    m.precision = "fp32"
+    with torch.no_grad():  # non-trivial running stats for eval mode
+        for bn in (m.conv[1], m.conv[4]):
+            bn.running_mean.uniform_(-0.1, 0.1)
+            bn.running_var.uniform_(0.5, 2.0)
+    m = m.cuda().train(training)
+    sd = _sd(m, "blk")
+    x = torch.rand(2, 5, 8, 6, 10)
+    y = m(x.cuda())
+    y_ref = ref._dconv(sd, "blk", x, training)
+    assert y.shape == y_ref.shape
+    torch.testing.assert_close(y.cpu(), y_ref, rtol=0, atol=ATOL)
+    for k, v in _bn_buffers(m).items():
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == int(sd["blk." + k]), k
+        else:
+            torch.testing.assert_close(v, sd["blk." + k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_down_matches_oracle(training):
+    from pcms_amd.models.unet3d import Down3D
+    torch.manual_seed(1)
+    m = Down3D(64, 128)
+    m.precision = "fp32"
+    m = m.cuda().train(training)
+    sd = _sd(m, "d")
+    x = torch.randn(2, 64, 8, 8, 9)  # odd W: MaxPool3d floors
+    y = m(x.cuda())
+    y_ref = ref._dconv(sd, "d.maxpool_conv.1", torch.nn.functional.max_pool3d(x, 2), training)
+    assert y.shape == y_ref.shape == (2, 128, 4, 4, 4)
+    torch.testing.assert_close(y.cpu(), y_ref, rtol=0, atol=ATOL)
+    torch.testing.assert_close(m.maxpool_conv[1].conv[1].running_mean.cpu(),
+                               sd["d.maxpool_conv.1.conv.1.running_mean"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("training,skip", [(True, (8, 8, 8)), (False, (9, 8, 10))])
+def test_up_matches_oracle(training, skip):
+    from pcms_amd.models.unet3d import Up3D
+    torch.manual_seed(2)
+    m = Up3D(128, 64)
+    m.precision = "fp32"
+    m = m.cuda().train(training)
+    sd = _sd(m, "u")
+    x1 = torch.randn(2, 128, 4, 4, 4)
+    x2 = torch.randn(2, 64, *skip)
+    y = m(x1.cuda(), x2.cuda())
+    y_ref = ref._up(sd, "u", x1, x2, training)
+    assert y.shape == y_ref.shape == (2, 64) + skip
+    torch.testing.assert_close(y.cpu(), y_ref, rtol=0, atol=ATOL)
+
+
+def test_blocks_bf16_close_and_forward_only():
+    from pcms_amd.models.unet3d import DoubleConv3D
+    torch.manual_seed(3)
+    m = DoubleConv3D(64, 64).cuda().train()
+    m.precision = "bf16"
+    sd = _sd(m, "b")
+    x = torch.rand(1, 64, 8, 8, 8)
+    y = m(x.cuda())
+    y_ref = ref._dconv(sd, "b", x, True)
+    assert float((y.cpu() - y_ref).abs().max()) < 0.1  # bf16 storage of every activation
+    with pytest.raises(NotImplementedError):
+        m(x.cuda().requires_grad_())
+
+
+def _net(seed=4):
+    from pcms_amd.models.unet3d import UNet3D
+    torch.manual_seed(seed)
+    m = UNet3D(n_modalities=5, n_classes=1, precision="fp32")
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm3d):
+                mod.running_mean.uniform_(-0.05, 0.05)
+                mod.running_var.uniform_(0.5, 1.5)
+    return m.cuda()
+
+
+def test_predict_and_inference_head_kernel():
+    m = _net()
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    x = torch.rand(2, 5, 16, 16, 16)
+    p = m.predict(x.cuda()).cpu()
+    p_ref = ref.predict(sd, x)
+    torch.testing.assert_close(p, p_ref, rtol=0, atol=ATOL)
+    assert float(p.min()) >= 0.0 and float(p.max()) <= 1.0
+    for thr in (0.5, float(p_ref.median())):
+        mask = m.inference(x.cuda(), threshold=thr).cpu()
+        mask_ref = ref.inference(sd, x, threshold=thr)
+        assert set(mask.unique().tolist()) <= {0.0, 1.0}
+        differ = mask != mask_ref
+        assert bool(((p_ref[differ] - thr).abs() < 1e-4).all()), int(differ.sum())
+    assert not m.training
+
+
+def test_predictor_pipeline(tmp_path):
+    from pcms_amd.data import read_nifti, read_nifti_header, write_nifti
+    from pcms_amd.predict import MODALITIES, ModelPredictor, load_multimodal_images, preprocess_image
+    m = _net(5)
+    ckpt = tmp_path / "best_model_epoch_1.pth"
+    torch.save(m.state_dict(), ckpt)
+    rng = np.random.default_rng(0)
+    case = tmp_path / "case0"
+    for i, mod in enumerate(MODALITIES):
+        (case / mod).mkdir(parents=True)
+        if mod == "T2 fs":
+            continue  # missing modality -> zero fill
+        img = rng.random((16, 16, 16), dtype=np.float32) * (i + 1) * 100
+        if mod == "DWI":
+            img[:] = 7.0  # constant -> zeros
+        write_nifti(str(case / mod / "a.nii"), img, spacing=(0.5, 0.6, 3.0))
+    image, names = load_multimodal_images(str(case))
+    assert names == MODALITIES and image.shape == (5, 16, 16, 16)
+    assert float(image[0].min()) == 0.0 and float(image[0].max()) == 1.0
+    assert not image[1].any() and not image[3].any()
+    t = preprocess_image(image)
+    assert t.shape == (1, 5, 16, 16, 16) and t.dtype == torch.float32
+    pr = ModelPredictor(str(ckpt), device="cuda", precision="fp32")
+    prob = pr.predict(t)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    np.testing.assert_allclose(prob, ref.predict(sd, t)[0, 0].numpy(), rtol=0, atol=ATOL)
+    out = tmp_path / "prediction.nii"
+    pr.save_prediction(prob, str(out), reference_image_path=str(case / "ADC" / "a.nii"))
+    saved = read_nifti(str(out))
+    assert saved.dtype == np.uint8 and np.array_equal(saved, (prob > 0.5).astype(np.uint8))
+    assert read_nifti_header(str(out))["spacing"][:3] == pytest.approx((0.5, 0.6, 3.0))
+
+
+def test_model_validator_report(tmp_path):
+    from pcms_amd.utils.metrics import ModelValidator
+    m = _net(6)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    ckpt = tmp_path / "ckpt.pth"
+    torch.save({"epoch": 3, "model_state_dict": m.state_dict()}, ckpt)
+    gen = torch.Generator().manual_seed(1)
+    batches = []
+    for i in range(2):
+        x = torch.rand(2, 5, 16, 16, 16, generator=gen)
+        y = (ref.predict(sd, x) > 0.5).float()
+        y[:, :, :4] = 1.0 - y[:, :, :4]  # imperfect labels
+        batches.append({"image": x, "label": y, "case_id": [f"c{2 * i}", f"c{2 * i + 1}"]})
+    v = ModelValidator({"device": "cuda", "precision": "fp32", "model_path": str(ckpt),
+                        "save_dir": str(tmp_path / "out")}, test_loader=batches)
+    dice, iou = v.validate()
+    rep = json.loads((tmp_path / "out" / "validation_results.json").read_text())
+    assert set(rep) == {"timestamp", "avg_dice", "avg_iou", "case_count", "case_results"}
+    assert rep["case_count"] == 4 and [c["case_id"] for c in rep["case_results"]] == ["c0", "c1", "c2", "c3"]
+    assert rep["avg_dice"] == pytest.approx(dice) and rep["avg_iou"] == pytest.approx(iou)
+    for b in batches:
+        mask = ref.inference(sd, b["image"])
+        for i in range(2):
+            c = next(c for c in rep["case_results"] if c["case_id"] == b["case_id"][i])
+            p, t = mask[i].reshape(-1), b["label"][i].reshape(-1)
+            inter = float((p * t).sum())
+            assert c["dice"] == pytest.approx(2 * inter / (float(p.sum() + t.sum()) + 1e-8), abs=2e-3)
+            assert c["iou"] == pytest.approx(inter / (float(p.sum() + t.sum()) - inter + 1e-8), abs=2e-3)

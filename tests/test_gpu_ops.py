@@ -409,7 +409,11 @@ def test_head(dt, code, tol, ncls):
     V = S[0] * S[1] * S[2]
     logits = torch.empty(N, ncls, *S, device=DEV)
     ad = ndhwc(a).to(DEV)
-    L.call("pcms_head_fwd", code, ad, w.reshape(ncls, 64).to(DEV), b.to(DEV), logits, V, N, ncls)
+    L.call("pcms_head_fwd", code, ad, w.reshape(ncls, 64).to(DEV), b.to(DEV), logits, V, N, ncls, 0, 0.5)
+    probs = torch.empty_like(logits)
+    mask = torch.empty_like(logits)
+    L.call("pcms_head_fwd", code, ad, w.reshape(ncls, 64).to(DEV), b.to(DEV), probs, V, N, ncls, 1, 0.5)
+    L.call("pcms_head_fwd", code, ad, w.reshape(ncls, 64).to(DEV), b.to(DEV), mask, V, N, ncls, 2, 0.5)
     da = torch.empty_like(ad)
     dw = torch.zeros(ncls, 64, device=DEV)
     db = torch.zeros(ncls, device=DEV)
@@ -421,6 +425,8 @@ def test_head(dt, code, tol, ncls):
     torch.cuda.synchronize()
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
     close(logits.cpu(), out.detach(), 1e-5, "head fwd")
+    close(probs.cpu(), torch.sigmoid(out.detach()), 1e-6, "head sigmoid (predict)")
+    assert torch.equal(mask.cpu(), (torch.sigmoid(logits.cpu()) > 0.5).float())
     close(ncdhw(da.cpu()), ar.grad, tol, "head dgrad")
     close(dw.cpu(), wr.grad.reshape(ncls, 64), 1e-5, "head wgrad")
     close(db.cpu(), br.grad, 1e-5, "head bias grad")
