@@ -32,11 +32,14 @@ int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long 
 int pcms_conv3_chunk(int dtype);                  /* input channels per K-chunk        */
 int pcms_conv3_mblocks(int N, int D, int H, int W);/* general-kernel M blocks (an upper
                                                       bound on the BN partial rows)      */
-/* BN partial rows an unsplit pcms_conv3_fwd over sources (c0, c1) writes: the big-box
- * bf16 kernel (8x8x16 boxes, 16-channel chunks, >= pcms_conv3_big_min_boxes boxes) writes
- * one row per box, the general kernel pcms_conv3_mblocks rows                           */
-int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1);
+/* BN partial rows an unsplit pcms_conv3_fwd over sources (c0, c1) writes: the persistent
+ * big-box bf16 kernel (8x8x16 boxes, 16-channel chunks, >= pcms_conv3_big_min_boxes boxes)
+ * writes one row per box slot (min(boxes, workgroups / (Cout / 64))), the general kernel
+ * pcms_conv3_mblocks rows                                                               */
+int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout);
 int pcms_conv3_big_min_boxes(int v);               /* set (v > 0) / query; returns old */
+int pcms_conv3_big_max_wgs(int v);                 /* persistent grid cap: set (v >= 0,
+                                                      0 = one per CU) / query; old      */
 /* master W [Cout][Cin][3][3][3] fp32 -> kernel pack; flip=1 builds the dgrad pack      */
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s);
 // Both packs of one conv (forward and dgrad, as pcms_conv3_pack flip 0 / 1) from one read of w.

@@ -19,8 +19,9 @@ SIGNATURES = {
     "pcms_pack_input": "ippiilis",
     "pcms_conv3_chunk": "i",
     "pcms_conv3_mblocks": "iiii",
-    "pcms_conv3_fwd_rows": "iiiiiii",
+    "pcms_conv3_fwd_rows": "iiiiiiii",
     "pcms_conv3_big_min_boxes": "i",
+    "pcms_conv3_big_max_wgs": "i",
     "pcms_conv3_pack": "ippiiis",
     "pcms_conv3_pack2": "ipppiis",
     "pcms_conv3_splits": "iii",

@@ -65,7 +65,7 @@ class _Runner:
         call("pcms_conv3_pack", self.code, conv.weight.detach(), wpack, cout, conv.in_channels, 0)
         nvox = N * S[0] * S[1] * S[2]
         y = self.buf(nvox * cout)
-        rows = query("pcms_conv3_fwd_rows", self.code, N, *S, c0, c1)
+        rows = query("pcms_conv3_fwd_rows", self.code, N, *S, c0, c1, cout)
         stats = torch.empty(rows * (cout * 2 + 1), dtype=torch.float32, device=self.dev)
         call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, wpack, conv.bias, y, None, cout, None,
              stats if training else None, 0, N, *S, cout, 1)

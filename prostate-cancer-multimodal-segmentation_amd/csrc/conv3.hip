@@ -876,41 +876,50 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* 
 
 // ------------------------------------------------------------------------------------
 // Big-box forward / dgrad (bf16; the level-0/1 hot case: D % 8 == H % 8 == 0, W % 16 == 0,
-// input channels in 16-channel chunks).  One 4-wave workgroup per CU computes an
-// 8 x 8 x 16 = 1024-voxel box x 64 output channels.  Wave w owns voxel rows
-// [256 w, 256 w + 256) = 8 M-tiles, so every B fragment (weights, L2-resident) feeds 8 MFMAs,
-// half the weight traffic per MFMA of conv3_fwd_kernel.  The 10 x 10 x 18 halo of a chunk
-// (32-B rows; the two 16-B halves swapped on odd row octets, so 16 consecutive rows hit 16
-// distinct bank groups) is double-buffered: the next chunk's halo streams in by buffer
-// LDS-DMA, one piece per thread and tap over the first 15 taps of the current chunk, and A
-// fragments of tap t + 1 are read while tap t's 16 MFMAs run.  Output columns are channel
-// pairs (column j of N-tile nt = channel 2 j + nt): each accumulator register pair stores as
-// one packed bf16x2, a store instruction writes two 128-B voxel rows.  BatchNorm partials:
-// one stats row per box (sum, M2 about the row mean; counts after the [rows][Cout][2] block).
+// input channels in 16-channel chunks), PERSISTENT: one 4-wave workgroup per CU, one grid of
+// at most #CU workgroups; workgroup (slot, cob) computes 8 x 8 x 16 = 1024-voxel boxes
+// slot, slot + nslot, ... for its 64 output channels.  Wave w owns voxel rows
+// [256 w, 256 w + 256) = 8 M-tiles, so every B fragment (weights, L2-resident) feeds 8 MFMAs.
+// The 10 x 10 x 18 halo of a chunk (32-B rows; the two 16-B halves swapped on odd row octets,
+// so 16 consecutive rows hit 16 distinct bank groups) is double-buffered: the next chunk's
+// halo -- the NEXT BOX's first chunk during a box's last chunk -- streams in by buffer
+// LDS-DMA, one piece per thread and tap over the first 15 taps, and A fragments of tap t + 1
+// are read while tap t's 16 MFMAs run; B loads run Dist taps ahead across chunk and box
+// boundaries.  So only the first box of a workgroup waits for its operands; every later box
+// starts on a landed halo.  Epilogue per box: + bias, bf16 pairs staged through a wave-private
+// 8 KiB LDS slice (two M-tiles at a time) and written back as 16-B stores of whole 128-B
+// channel rows (32 store instructions per wave and box, issued without waiting: the B waits
+// of the next box's first taps count them).  BatchNorm partials: per wave a running Chan
+// merge over its boxes (count, mean, M2 per channel); one stats row per slot at the end.
 // ------------------------------------------------------------------------------------
 constexpr int kBgThreads = 256;
 constexpr int kBgHH = 10, kBgHW = 18;
-// BD = box depth: 8 (1024 voxels, 8 M-tiles per wave, one workgroup per CU) or 4 (512
-// voxels, 4 M-tiles per wave, two workgroups per CU that cover each other's prologue,
-// chunk barriers and store tail)
-template <int BD> struct BgGeom {
-  static constexpr int MT = BD;                                           // M-tiles per wave
-  static constexpr int Halo = (BD + 2) * kBgHH * kBgHW;                   // rows x 32 B
-  static constexpr int Pieces = (2 * Halo + kBgThreads - 1) / kBgThreads; // DMA pieces / thread
-  static constexpr int Buf = Pieces * kBgThreads * 16;                    // (tail pad)
-  static constexpr int Lds = 2 * Buf + 4 * 64 * 3 * 4;                    // + stats merge
-  static constexpr int PerCU = BD == 8 ? 1 : 2;
-  static constexpr int Dist = BD == 8 ? 8 : 2;  // B prefetch distance (taps); (Dist + 1) | 27
-  static_assert(27 % (Dist + 1) == 0, "B ring index must continue across chunks");
-};
-constexpr int kBgBD = 8;  // box depth (depth 4 with 2 workgroups per CU measured slower)
+constexpr int kBgBD = 8;                                                  // box depth
+constexpr int kBgMT = 8;                                                  // M-tiles per wave
+constexpr int kBgHalo = (kBgBD + 2) * kBgHH * kBgHW;                      // rows x 32 B
+constexpr int kBgPieces = (2 * kBgHalo + kBgThreads - 1) / kBgThreads;    // DMA pieces / thread
+constexpr int kBgBuf = kBgPieces * kBgThreads * 16;                       // (tail pad)
+constexpr int kBgStage = 64 * 128;                                        // per-wave store slice
+constexpr int kBgRed = 4 * 64 * 3 * 4;                                    // BN moments
+constexpr int kBgLds = 2 * kBgBuf + 4 * kBgStage + kBgRed + 64 * 4;       // + bias
+constexpr int kBgDist = 8;                 // B prefetch distance (taps); (Dist + 1) | 27
+constexpr int kBgEpiStores = kBgMT * 4;    // 16-B stores per wave and box
+static_assert(27 % (kBgDist + 1) == 0, "B ring index must continue across chunks");
+static_assert(kBgLds <= 160 * 1024, "LDS");
 
 // hidden 16-B global load (the compiler's waitcnt pass does not count it): retired by
 // vm_wait2<N>, which also orders the register's readers after the wait
 __device__ __forceinline__ void gload16(s16x8_t& dst, const void* ptr) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(ptr) : "memory");
 }
+// the same through a buffer descriptor (bounds-checked: out of range reads zeros), one VGPR
+// byte offset per address, immediate offset Imm
+template <int Imm> __device__ __forceinline__ void bload16(s16x8_t& dst, i32x4_t rsrc, uint32_t voff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3" : "=v"(dst) : "v"(voff), "s"(rsrc), "n"(Imm)
+               : "memory");
+}
 template <int N> __device__ __forceinline__ void vm_wait2(s16x8_t& a, s16x8_t& b) {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
 template <class F, int... I>
@@ -929,13 +938,18 @@ template <int P, int Dist> constexpr int bg_wait(int t) {
   return n;
 }
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// an opaque copy: values derived from it are recomputed where used instead of being hoisted
+// out of the box loop (and spilled: a spill reload is a vector-memory load whose wait would
+// also drain the hidden B loads and halo DMA in flight)
+__device__ __forceinline__ int opaque(int v) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
 
-
-template <int BD>
-__global__ void __launch_bounds__(kBgThreads, BgGeom<BD>::PerCU) conv3_fwd_big_kernel(Conv3Params p, uint32_t x0bytes,
-                                                                                     uint32_t x1bytes) {
-  typedef BgGeom<BD> Gm;
-  constexpr int MT = Gm::MT;
+__global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Params p, uint32_t x0bytes,
+                                                                     uint32_t x1bytes) {
+  constexpr int MT = kBgMT;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -945,44 +959,40 @@ __global__ void __launch_bounds__(kBgThreads, BgGeom<BD>::PerCU) conv3_fwd_big_k
   // channel block fastest, so the workgroups sharing a halo (and neighbouring boxes) share L2
   const int G = gridDim.x;
   const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-  const int cob = lg % ncob, box = lg / ncob, nbox = G / ncob;
-  int q = box;
-  const int bwi = q % p.nbw; q /= p.nbw;
-  const int bhi = q % p.nbh; q /= p.nbh;
-  const int bdi = q % p.nbd;
-  const int n = q / p.nbd;
-  const int d0 = bdi * BD, h0 = bhi * 8, w0 = bwi * 16;
+  const int cob = lg % ncob, slot = lg / ncob, nslot = G / ncob;
+  const int nbox = p.N * p.nbd * p.nbh * p.nbw;
   const int co_base = cob * 64;
+  auto origin = [&](int box, int& n, int& d0, int& h0, int& w0) {
+    int q = box;
+    const int bwi = q % p.nbw; q /= p.nbw;
+    const int bhi = q % p.nbh; q /= p.nbh;
+    const int bdi = q % p.nbd;
+    n = q / p.nbd;
+    d0 = bdi * kBgBD; h0 = bhi * 8; w0 = bwi * 16;
+  };
 
-  // this thread's halo pieces: (voxel << 1 | logical 16-B half), -1 = zero (padding, tail)
-  int pv[Gm::Pieces];
-#pragma unroll
-  for (int j = 0; j < Gm::Pieces; ++j) {
-    const int pc = tid + j * kBgThreads;
-    const int hv = pc >> 1;
-    int e = -1;
-    if (hv < Gm::Halo) {
-      const int hw_ = hv % kBgHW, t_ = hv / kBgHW, hh_ = t_ % kBgHH, hd_ = t_ / kBgHH;
-      const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
-      if ((unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H && (unsigned)gw < (unsigned)p.W)
-        e = ((((n * p.D + gd) * p.H + gh) * p.W + gw) << 1) | ((pc & 1) ^ ((hw_ >> 3) & 1));
-    }
-    pv[j] = e;
-  }
   const i32x4_t xr0 = buffer_desc(p.x0, x0bytes);
   const i32x4_t xr1 = buffer_desc(p.x1 ? p.x1 : p.x0, x1bytes);
   const uint32_t lds0 = lds_addr(lds);
-  // live = false (past the last chunk): the piece is still issued (the vmcnt arithmetic is
-  // the same for every chunk) but reads out of range = zeros into the idle buffer
-  auto stage_piece = [&](int chunk, int buf, int j, bool live) {
+  // live = false (past the last box): the piece is still issued (the vmcnt arithmetic is the
+  // same for every chunk) but reads out of range = zeros into the idle buffer
+  auto stage_piece = [&](int n, int d0, int h0, int w0, int chunk, int buf, int j, bool live) {
     const int c = chunk * 16;
     const bool first = c < p.c0;  // workgroup-uniform: the chunk lies in x0 or in x1
     const uint32_t stride = first ? p.c0 : p.c1;
     const uint32_t cofs = first ? c : c - p.c0;
-    const int e = pv[j];
-    const uint32_t voff = (e < 0 || !live) ? kOOB
-                                           : ((uint32_t)(e >> 1) * stride + cofs + (uint32_t)(e & 1) * 8u) * 2u;
-    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds0 + buf * Gm::Buf + (wave * 64 + j * kBgThreads) * 16);
+    // piece j of this thread: halo row hv = pc / 2, logical 16-B half (pc & 1) swapped on odd
+    // row octets (recomputed per chunk: a few VALU against 432 MFMAs, no registers held)
+    const int pc = opaque(tid) + j * kBgThreads;
+    const int hv = pc >> 1;
+    const int hw_ = hv % kBgHW, t_ = hv / kBgHW, hh_ = t_ % kBgHH, hd_ = t_ / kBgHH;
+    const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+    uint32_t voff = kOOB;
+    if (live && hv < kBgHalo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
+        (unsigned)gw < (unsigned)p.W)
+      voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs +
+              (uint32_t)((pc & 1) ^ ((hw_ >> 3) & 1)) * 8u) * 2u;
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
     dma16(first ? xr0 : xr1, lb, voff, 0);
   };
 
@@ -990,165 +1000,211 @@ __global__ void __launch_bounds__(kBgThreads, BgGeom<BD>::PerCU) conv3_fwd_big_k
   // is box voxel (2 wave + mt / 4, 2 (mt % 4) + prow / 16, prow % 16).  The half swizzle
   // depends on the halo w coordinate only, so for each kw the (kd, kh) part of a tap is a
   // constant row offset (kd * 10 + kh) * 18 * 32 bytes folded into the ds_read immediate.
-  const int prow = perm32(r_lane);
-  int hb32[MT], swk[3];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int rd = (BD / 4) * wave + (mt >> 2), rh = 2 * (mt & 3) + (prow >> 4);
-    hb32[mt] = ((rd * kBgHH + rh) * kBgHW + (prow & 15)) * 32;
-  }
-#pragma unroll
-  for (int kw = 0; kw < 3; ++kw) swk[kw] = kw * 32 + ((hsel ^ ((((prow & 15) + kw) >> 3) & 1)) << 4);
-  // B fragment: packed [Cin/32][27][Cout][32]; 16-channel chunk c = half (c & 1) of c >> 1
+  // One base register per kw (recomputed per chunk); the M-tile and (kd, kh) parts are
+  // ds_read immediates.
   // B fragments (weights, packed [Cin/32][27][Cout][32]; 16-channel chunk c = half c & 1 of
   // 32-chunk c >> 1) come through hidden loads Dist taps ahead: vector-memory returns are
   // in order, so a wait on B(t) also retires every halo piece issued before it; the pieces
   // get >= Dist taps to arrive from HBM before anything waits on them.
-  const bf16_t* wp = (const bf16_t*)p.w;
+  // B address: (chunk, tap) byte offset (uniform) + one per-lane byte offset, through a
+  // descriptor over the whole pack
   const int nchunk = p.Cin >> 4;
-  auto load_b = [&](s16x8_t (&dst)[2], int chunk, int tap) {
-    chunk = min(chunk, nchunk - 1);  // past the last chunk: a harmless reload (fixed counts)
-    const bf16_t* wt = wp + ((long)((chunk >> 1) * 27 + tap) * Cout + co_base + 2 * r_lane) * 32 + (chunk & 1) * 16 +
-                       hsel * 8;
-    gload16(dst[0], wt);
-    gload16(dst[1], wt + 32);
+  const uint32_t tap_bytes = (uint32_t)Cout * 64u;
+  const i32x4_t wr = buffer_desc(p.w, (uint32_t)(p.Cin >> 5) * 27u * tap_bytes);
+  auto load_b = [&](s16x8_t (&dst)[2], int chunk, int tap, uint32_t boff) {
+    const uint32_t off = boff + (uint32_t)((chunk >> 1) * 27 + tap) * tap_bytes + (uint32_t)(chunk & 1) * 32u;
+    bload16<0>(dst[0], wr, off);
+    bload16<64>(dst[1], wr, off);
   };
 
-  f32x16_t acc[MT][2];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // epilogue constants: output columns are channel pairs (column j of N-tile nt = channel
+  // 2 j + nt); two-pointer output split at cy0 (workgroup-uniform)
+  // (bias and the running BatchNorm moments live in LDS between boxes, not in registers)
+  float* red = reinterpret_cast<float*>(lds + 2 * kBgBuf + 4 * kBgStage);  // [wave][64][3]
+  float* bls = red + 4 * 64 * 3;                                           // [64]
+  if (tid < 64) bls[tid] = p.bias ? p.bias[co_base + tid] : 0.f;
+  const bool to0 = co_base < p.cy0;
+  const long ys = to0 ? p.cy0 : Cout - p.cy0;
+  const int yc0 = to0 ? co_base : co_base - p.cy0;
+  // output through a descriptor too (stores out of range are dropped; the host checks
+  // every byte offset fits 31 bits)
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+      to0 ? p.y0 : p.y1, (short)0, (int)(p.nvox * ys * 2), 0x00020000);
+  char* stg = lds + 2 * kBgBuf + wave * kBgStage;
+  int nbdone = 0;  // boxes merged into the running moments (uniform: kept in an SGPR)
 
+  f32x16_t acc[MT][2];
+  s16x8_t bset[kBgDist + 1][2];
+  int box = slot;
+  int n, d0, h0, w0;
+  origin(box, n, d0, h0, w0);
 #pragma unroll
-  for (int j = 0; j < Gm::Pieces; ++j) stage_piece(0, 0, j, true);
-  s16x8_t bset[Gm::Dist + 1][2];
+  for (int j = 0; j < kBgPieces; ++j) stage_piece(n, d0, h0, w0, 0, 0, j, true);
 #pragma unroll
-  for (int t = 0; t < Gm::Dist; ++t) load_b(bset[t], 0, t);
+  for (int t = 0; t < kBgDist; ++t) load_b(bset[t], 0, t, (uint32_t)((co_base + 2 * r_lane) * 64 + hsel * 16));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int chunk = 0; chunk < nchunk; ++chunk) {
-    const int buf = chunk & 1;
-    const bool more = chunk + 1 < nchunk;
-    const char* hl = lds + buf * Gm::Buf;
-    auto read_a = [&](s16x8_t (&dst)[MT], int tap) {
-      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-      const char* base = hl + swk[kw] + (kd * kBgHH + kh) * kBgHW * 32;
+  int buf = 0;
+  while (true) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) dst[mt] = *reinterpret_cast<const s16x8_t*>(base + hb32[mt]);
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    const int nbx = box + nslot;
+    const bool has_next = nbx < nbox;
+    int nn = n, nd0 = d0, nh0 = h0, nw0 = w0;
+    if (has_next) origin(nbx, nn, nd0, nh0, nw0);
+    // one chunk: 27 taps.  Chunk 0 (peeled, Slack): B(t < Dist) were issued before the
+    // previous box's 32 epilogue stores, so those waits count them as well; in a workgroup's
+    // first box the prologue's vmcnt(0) already retired B(t < Dist), the looser count is safe.
+    auto run_chunk = [&](int chunk, auto slack_tag) {
+      constexpr bool Slack = decltype(slack_tag)::value;
+      const bool last = chunk + 1 == nchunk;
+      const bool live = !last || has_next;
+      const int sn = last ? nn : n, sd = last ? nd0 : d0, sh = last ? nh0 : h0, sw = last ? nw0 : w0;
+      const int schunk = last ? 0 : chunk + 1;
+      const char* hl = lds + buf * kBgBuf;
+      const int lo = opaque(lane);
+      const int prow = perm32(lo & 31), hs = lo >> 5;
+      const int hbase = ((2 * wave * kBgHH + (prow >> 4)) * kBgHW + (prow & 15)) * 32;
+      int swk[3];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) swk[kw] = hbase + kw * 32 + ((hs ^ ((((prow & 15) + kw) >> 3) & 1)) << 4);
+      const uint32_t boff = (uint32_t)((co_base + 2 * (lo & 31)) * 64 + hs * 16);
+      auto read_a1 = [&](int tap, int mt) {
+        const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+        return *reinterpret_cast<const s16x8_t*>(hl + swk[kw] + (kd * kBgHH + kh) * kBgHW * 32 +
+                                                 ((mt >> 2) * kBgHH + 2 * (mt & 3)) * kBgHW * 32);
+      };
+      // A fragments roll through one register set: right after M-tile mt's two MFMAs of tap t
+      // its fragment of tap t + 1 is read (14 MFMAs of slack before its first use)
+      s16x8_t a[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) a[mt] = read_a1(0, mt);
+      // per tap: B(tap + D) (the set index runs on across chunks: (D + 1) | 27), one halo
+      // piece of the next chunk (taps < 15); wait for B(tap); 16 MFMAs
+      static_for<27>([&](auto tc) {
+        constexpr int tap = decltype(tc)::value;
+        constexpr int tn = tap + kBgDist;
+        if constexpr (tn < 27) load_b(bset[tn % (kBgDist + 1)], chunk, tn, boff);
+        else load_b(bset[tn % (kBgDist + 1)], schunk, tn - 27, boff);
+        if constexpr (tap < kBgPieces) stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, tap, live);
+        s16x8_t(&b)[2] = bset[tap % (kBgDist + 1)];
+        constexpr int extra = (Slack && tap < kBgDist) ? kBgEpiStores : 0;
+        vm_wait2<bg_wait<kBgPieces, kBgDist>(tap) + extra>(b[0], b[1]);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc[mt][0] = mfma(a[mt], b[0], acc[mt][0]);
+          acc[mt][1] = mfma(a[mt], b[1], acc[mt][1]);
+          if constexpr (tap + 1 < 27) a[mt] = read_a1(tap + 1, mt);
+        }
+      });
+      // the next chunk's halo has landed (the newest piece is followed by the B loads of the
+      // remaining taps) and every wave is done with buf.  After a box's last chunk retire
+      // everything: the epilogue needs registers, and the compiler may move (or, after the
+      // workgroup's last box, reuse) the destinations of the next box's B loads -- they
+      // must hold landed data by then (costs one L2 round trip per box).
+      if (!last) vm_wait<2 * (27 - kBgPieces)>();
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      buf ^= 1;
     };
-    s16x8_t a[2][MT];
-    read_a(a[0], 0);
-    // per tap: B(tap + D) (the set index runs on across chunks: (D + 1) | 27), one halo piece
-    // of the next chunk (taps < 15), A of tap + 1; wait for B(tap); this tap's 16 MFMAs
-    static_for<27>([&](auto tc) {
-      constexpr int tap = decltype(tc)::value;
-      constexpr int tn = tap + Gm::Dist;
-      if constexpr (tn < 27) load_b(bset[tn % (Gm::Dist + 1)], chunk, tn);
-      else load_b(bset[tn % (Gm::Dist + 1)], chunk + 1, tn - 27);
-      if constexpr (tap < Gm::Pieces) stage_piece(chunk + 1, buf ^ 1, tap, more);
-      constexpr int cur = tap & 1;
-      if constexpr (tap + 1 < 27) read_a(a[cur ^ 1], tap + 1);
-      s16x8_t(&b)[2] = bset[tap % (Gm::Dist + 1)];
-      vm_wait2<bg_wait<Gm::Pieces, Gm::Dist>(tap)>(b[0], b[1]);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[cur][mt], b[nt], acc[mt][nt]);
-    });
-    // the next chunk's halo has landed (the newest piece is followed by the B loads of the
-    // remaining taps) and every wave is done with buf; after the last chunk retire everything
-    if (more) vm_wait<2 * (27 - Gm::Pieces)>();
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+    run_chunk(0, std::true_type{});
+    for (int chunk = 1; chunk < nchunk; ++chunk) run_chunk(chunk, std::false_type{});
 
-  // ---- epilogue: + bias, packed channel-pair stores (two-pointer output split at cy0)
-  const int cpair = co_base + 2 * r_lane;
-  float bias0 = 0.f, bias1 = 0.f;
-  if (p.bias) {
-    bias0 = p.bias[cpair];
-    bias1 = p.bias[cpair + 1];
-  }
-  const bool to0 = co_base < p.cy0;
-  bf16_t* yb = to0 ? (bf16_t*)p.y0 : (bf16_t*)p.y1;
-  const long ys = to0 ? p.cy0 : Cout - p.cy0;
-  const int yc = to0 ? cpair : cpair - p.cy0;
-  const long plane = (long)p.H * p.W;
-  const long vbase = (((long)n * p.D + d0) * p.H + h0) * p.W + w0;
-  float s1[2] = {0.f, 0.f};
+    // ---- epilogue of this box, two M-tiles at a time: + bias, bf16 pairs into the wave's
+    // LDS slice (row = 32 mm + C row, 128 B of 32 channel pairs), read back as 8 x 16 B per
+    // lane = whole 128-B channel rows, 16-B stores.  BatchNorm moments in the same pass,
+    // shifted by K (the running mean; the bias before the first box): box mean K + S1 / n,
+    // M2 = S2 - S1^2 / n, Chan-merged into the running moments.
+    // (lane-dependent offsets from an opaque lane copy: box-invariant, the compiler would
+    // hoist them out of the box loop and spill them)
+    const int lane_o = opaque(lane);
+    const long plane = (long)p.H * p.W;
+    const long vbase = (((long)n * p.D + d0) * p.H + h0) * p.W + w0;
+    char* wst = stg + (lane_o & 31) * 4 + (lane_o >> 5) * 512;
+    float* rme = red + (wave * 64 + 2 * (lane_o & 31)) * 3;  // [ch][mean, M2, n] x 2 channels
+    const float bias0 = bls[2 * (lane_o & 31)], bias1 = bls[2 * (lane_o & 31) + 1];
+    const float rn = (float)nbdone * (32.f * MT);
+    const float K0 = nbdone ? rme[0] : bias0, K1 = nbdone ? rme[3] : bias1;
+    const float c0s = bias0 - K0, c1s = bias1 - K1;  // d = acc + bias - K
+    float S1[2] = {0.f, 0.f}, S2[2] = {0.f, 0.f};
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int pr = perm32((e & 3) + 8 * (e >> 2) + 4 * hsel);
-    const long vrow = vbase + (long)(pr >> 4) * p.W + (pr & 15);
+    for (int pass = 0; pass < MT / 2; ++pass) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int rd = (BD / 4) * wave + (mt >> 2), rh = 2 * (mt & 3);
-      const long vox = vrow + (long)rd * plane + (long)rh * p.W;
-      const float v0 = acc[mt][0][e] + bias0, v1 = acc[mt][1][e] + bias1;
-      *reinterpret_cast<uint32_t*>(yb + vox * ys + yc) = pack_bf16x2(v0, v1);
-      s1[0] += v0;
-      s1[1] += v1;
+      for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = mm * 32 + (e & 3) + 8 * (e >> 2);
+          const float v0 = acc[2 * pass + mm][0][e], v1 = acc[2 * pass + mm][1][e];
+          *reinterpret_cast<uint32_t*>(wst + row * 128) = pack_bf16x2(v0 + bias0, v1 + bias1);
+          const float e0 = v0 + c0s, e1 = v1 + c1s;
+          S1[0] += e0;
+          S1[1] += e1;
+          S2[0] = fmaf(e0, e0, S2[0]);
+          S2[1] = fmaf(e1, e1, S2[1]);
+        }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int row = k * 8 + (lane_o >> 3), c16 = lane_o & 7;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(stg + row * 128 + c16 * 16);
+        const int mt = 2 * pass + (row >> 5), pr = perm32(row & 31);
+        const int rd = 2 * wave + (mt >> 2), rh = 2 * (mt & 3) + (pr >> 4), rw = pr & 15;
+        const long vox = vbase + (long)rd * plane + (long)rh * p.W + rw;
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0, 0);
+      }
+      asm volatile("" ::: "memory");
     }
-  }
-  if (!p.stats) return;
-  // BatchNorm partials: per-wave mean, squared deviations about it (corrected by
-  // (sum d)^2 / n), Chan merge over the 4 waves
-  constexpr float nw = 32.f * MT;
-  float mw[2], s2[2] = {0.f, 0.f}, sd[2] = {0.f, 0.f};
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    s1[nt] += __shfl_xor(s1[nt], 32, 64);
-    mw[nt] = s1[nt] / nw;
-  }
-  const float sh[2] = {bias0 - mw[0], bias1 - mw[1]};  // d = acc + bias - mean
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e)
+    {
+      constexpr float nb = 32.f * MT;  // voxels per wave and box
+      const float nnew = rn + nb;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const float d = acc[mt][nt][e] + sh[nt];
-        s2[nt] = fmaf(d, d, s2[nt]);
-        sd[nt] += d;
+        const float s1 = S1[nt] + __shfl_xor(S1[nt], 32, 64);
+        const float s2 = S2[nt] + __shfl_xor(S2[nt], 32, 64);
+        const float K = nt ? K1 : K0;
+        const float mbox = K + s1 / nb;
+        const float m2b = fmaxf(s2 - s1 * s1 / nb, 0.f);
+        const float rmean = nbdone ? rme[3 * nt] : 0.f, rm2 = nbdone ? rme[3 * nt + 1] : 0.f;
+        const float delta = mbox - rmean;
+        if ((lane_o >> 5) == 0) {
+          rme[3 * nt] = rmean + delta * (nb / nnew);
+          rme[3 * nt + 1] = rm2 + m2b + delta * delta * (rn * nb / nnew);
+          rme[3 * nt + 2] = nnew;
+        }
       }
-  float* red = reinterpret_cast<float*>(lds + 2 * Gm::Buf);
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    s2[nt] += __shfl_xor(s2[nt], 32, 64);
-    sd[nt] += __shfl_xor(sd[nt], 32, 64);
-    s2[nt] -= sd[nt] * sd[nt] / nw;
-    if (hsel == 0) {
-      float* rp = red + (wave * 64 + 2 * r_lane + nt) * 3;
-      rp[0] = s1[nt];
-      rp[1] = s2[nt];
-      rp[2] = nw;
+      ++nbdone;
     }
+    if (!has_next) break;
+    box = nbx;
+    n = nn; d0 = nd0; h0 = nh0; w0 = nw0;
   }
+
+  if (!p.stats) return;
+  // one stats row per slot: Chan merge of the 4 waves' running moments (mean, M2, n)
   __syncthreads();
   if (tid < 64) {
     float S = 0.f, Nn = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      S += red[(w * 64 + tid) * 3];
+      S += red[(w * 64 + tid) * 3] * red[(w * 64 + tid) * 3 + 2];
       Nn += red[(w * 64 + tid) * 3 + 2];
     }
     const float m = S / Nn;
-    float M2 = 0.f, sdd = 0.f;
+    float M2 = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const float c = red[(w * 64 + tid) * 3 + 2];
-      const float d = red[(w * 64 + tid) * 3] / c - m;
+      const float d = red[(w * 64 + tid) * 3] - m;
       M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
-      sdd += c * d;
     }
-    M2 -= sdd * sdd / Nn;
-    float* st = p.stats + ((long)box * Cout + co_base + tid) * 2;
+    float* st = p.stats + ((long)slot * Cout + co_base + tid) * 2;
     st[0] = S;
     st[1] = M2;
-    if (tid == 0 && cob == 0) p.stats[(long)nbox * Cout * 2 + box] = Nn;
+    if (tid == 0 && cob == 0) p.stats[(long)nslot * Cout * 2 + slot] = Nn;
   }
 }
 
@@ -1157,11 +1213,20 @@ __global__ void __launch_bounds__(kBgThreads, BgGeom<BD>::PerCU) conv3_fwd_big_k
 // big-box forward: bf16, whole 8x8x16 boxes, 16-channel chunks of both sources, enough boxes
 // to give every CU one (pcms_conv3_big_min_boxes), every byte offset inside a 32-bit voffset
 static int g_big_min_boxes = 256;
+static int g_big_max_wgs = 0;  // persistent grid cap (0: one workgroup per CU)
 static bool big_fwd_ok(int dtype, int N, int D, int H, int W, int c0, int c1) {
   if (dtype != PCMS_BF16 || D % kBgBD || H % 8 || W % 16 || c0 % 16 || c1 % 16 || c0 < 16) return false;
   const long nvox = (long)N * D * H * W;
   if ((long)N * (D / kBgBD) * (H / 8) * (W / 16) < g_big_min_boxes) return false;
   return nvox < (1L << 30) && nvox * std::max(c0, c1) * 2 < (long)kOOB;
+}
+// (the output descriptor additionally needs nvox * Cout * 2 < 2^31: checked at launch)
+// box slots of the persistent grid (= BatchNorm stats rows): each slot's workgroups (one
+// per 64-channel block) walk boxes slot, slot + nslot, ...
+static int big_slots(int N, int D, int H, int W, int Cout) {
+  const int nbox = N * (D / kBgBD) * (H / 8) * (W / 16);
+  const int G = g_big_max_wgs > 0 ? g_big_max_wgs : device_cus();
+  return std::max(1, std::min(nbox, G / (Cout / 64)));
 }
 
 extern "C" {
@@ -1174,8 +1239,9 @@ int pcms_conv3_mblocks(int N, int D, int H, int W) {
 }
 
 // BatchNorm partial rows an unsplit pcms_conv3_fwd with these sources writes
-int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1) {
-  if (big_fwd_ok(dtype, N, D, H, W, c0, c1)) return N * (D / kBgBD) * (H / 8) * (W / 16);
+int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout) {
+  if (Cout % 64 == 0 && big_fwd_ok(dtype, N, D, H, W, c0, c1) && (long)N * D * H * W * Cout * 2 < (long)kOOB)
+    return big_slots(N, D, H, W, Cout);
   return pcms_conv3_mblocks(N, D, H, W);
 }
 
@@ -1184,6 +1250,14 @@ int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1) {
 int pcms_conv3_big_min_boxes(int v) {
   const int old = g_big_min_boxes;
   if (v > 0) g_big_min_boxes = v;
+  return old;
+}
+
+// Workgroup cap of the persistent big-box grid (tests lower it so each workgroup walks
+// several boxes); 0 restores one per CU, v < 0 only queries.  Returns the previous value.
+int pcms_conv3_big_max_wgs(int v) {
+  const int old = g_big_max_wgs;
+  if (v >= 0) g_big_max_wgs = v;
   return old;
 }
 
@@ -1254,13 +1328,13 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   p.lbd = b.lbd; p.lbh = b.lbh; p.lbw = b.lbw;
   p.nbd = cdiv(D, 1 << b.lbd); p.nbh = cdiv(H, 1 << b.lbh); p.nbw = cdiv(W, 1 << b.lbw);
   if (splits > 1) p.yacc = yacc;
-  if (splits == 1 && !accumulate && big_fwd_ok(dtype, N, D, H, W, c0, c1)) {
+  if (splits == 1 && !accumulate && big_fwd_ok(dtype, N, D, H, W, c0, c1) &&
+      (long)N * D * H * W * Cout * 2 < (long)kOOB) {
     p.nbd = D / kBgBD; p.nbh = H / 8; p.nbw = W / 16;
-    const int nbox = N * p.nbd * p.nbh * p.nbw;
     const long nvox = (long)N * D * H * W;
-    constexpr int lds = BgGeom<kBgBD>::Lds;
-    (void)hipFuncSetAttribute((const void*)conv3_fwd_big_kernel<kBgBD>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(conv3_fwd_big_kernel<kBgBD>, dim3(nbox * (Cout / 64)), dim3(kBgThreads), lds, s, p,
+    const int nslot = big_slots(N, D, H, W, Cout);
+    (void)hipFuncSetAttribute((const void*)conv3_fwd_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kBgLds);
+    hipLaunchKernelGGL(conv3_fwd_big_kernel, dim3(nslot * (Cout / 64)), dim3(kBgThreads), kBgLds, s, p,
                        (uint32_t)(nvox * c0 * 2), (uint32_t)(nvox * c1 * 2));
     PCMS_CHECK_LAUNCH();
   }

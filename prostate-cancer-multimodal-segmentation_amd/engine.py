@@ -354,7 +354,7 @@ class UNetEngine:
         elif splits == 1:
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
-            rows = query("pcms_conv3_fwd_rows", self.code, N, *S, c0, c1)
+            rows = query("pcms_conv3_fwd_rows", self.code, N, *S, c0, c1, cs.cout)
         else:
             acc = b["yacc"]
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,

@@ -88,7 +88,7 @@ def test_conv3_fwd(dt, code, tol, N, cin, cout, S, split):
     L.call("pcms_conv3_pack", code, w.to(DEV), wpack, cout, cin_real, 0)
     y = torch.empty(N, *S, cout, dtype=dt, device=DEV)
     nvox = N * S[0] * S[1] * S[2]
-    rows = L.query("pcms_conv3_fwd_rows", code, N, *S, cin, 0)
+    rows = L.query("pcms_conv3_fwd_rows", code, N, *S, cin, 0, cout)
     stats = torch.zeros(max(rows, L.query("pcms_split_epilogue_rows", nvox)) * (cout * 2 + 1), device=DEV)
     if split == 1:
         L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, None, stats, 0,
@@ -194,18 +194,23 @@ def test_conv3_dual_source_and_dgrad_split_output(dt, code, tol):
     close(ncdhw(gu.cpu()), xr.grad[:, cs:], tol, "dgrad up part")
 
 
-@pytest.mark.parametrize("N,c0,c1,cout,cy0,S", [
-    (1, 64, 0, 64, 64, (8, 8, 16)),         # one box
-    (2, 32, 32, 128, 64, (16, 8, 32)),      # dual source, two-pointer output, 2 channel blocks
-    (1, 16, 48, 64, 64, (8, 16, 16)),       # chunks split unevenly between the sources
-    (1, 128, 0, 192, 128, (16, 16, 16)),    # odd number of 64-channel blocks, split output
+@pytest.mark.parametrize("N,c0,c1,cout,cy0,S,wgs", [
+    (1, 64, 0, 64, 64, (8, 8, 16), 0),         # one box
+    (2, 32, 32, 128, 64, (16, 8, 32), 0),      # dual source, two-pointer output, 2 channel blocks
+    (1, 16, 48, 64, 64, (8, 16, 16), 0),       # chunks split unevenly between the sources
+    (1, 128, 0, 192, 128, (16, 16, 16), 0),    # odd number of 64-channel blocks, split output
+    (2, 64, 0, 64, 64, (16, 16, 32), 3),       # persistent: 3 slots walk 16 boxes (6, 5, 5)
+    (2, 32, 32, 128, 64, (16, 16, 32), 4),     # 2 slots x 2 channel blocks, 8 boxes each
+    (1, 64, 64, 64, 64, (16, 24, 16), 5),      # dual source, 5 slots over 6 boxes (2 + 1 x 4)
 ])
-def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S):
-    """Big-box bf16 forward (8x8x16 boxes, 16-channel chunks, channel-pair stores) vs
-    torch conv3d on the same bf16 inputs; BN partial moments; the min-box threshold is
-    lowered so these small grids reach it."""
+def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S, wgs):
+    """Persistent big-box bf16 forward (8x8x16 boxes, 16-channel chunks, LDS-staged 16-B
+    stores) vs torch conv3d on the same bf16 inputs; BN partial moments (one row per box
+    slot, running merge over the slot's boxes).  The min-box threshold is lowered so these
+    small grids reach it; ``wgs`` caps the grid so every workgroup walks several boxes."""
     L = _lib()
     old = L.query("pcms_conv3_big_min_boxes", 1)
+    old_w = L.query("pcms_conv3_big_max_wgs", wgs)
     try:
         dt = torch.bfloat16
         g = torch.Generator().manual_seed(c0 + 5 * c1 + cout)
@@ -220,8 +225,9 @@ def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S):
         y0 = torch.empty(N, *S, cy0, dtype=dt, device=DEV)
         y1 = torch.empty(N, *S, max(cout - cy0, 8), dtype=dt, device=DEV)
         nvox = N * S[0] * S[1] * S[2]
-        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, c0, c1)
-        assert rows in [N * (S[0] // bd) * (S[1] // 8) * (S[2] // 16) for bd in (4, 8)]  # big-box path taken
+        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, c0, c1, cout)
+        nbox = N * (S[0] // 8) * (S[1] // 8) * (S[2] // 16)
+        assert rows == (nbox if wgs == 0 else min(nbox, wgs // (cout // 64)))  # big-box path taken
         stats = torch.zeros(rows * (cout * 2 + 1), device=DEV)
         L.call("pcms_conv3_fwd", 1, ndhwc(x0).to(DEV), c0, ndhwc(x1).to(DEV) if c1 else None, c1, wp, b.to(DEV),
                y0, y1 if cout > cy0 else None, cy0, None, stats, 0, N, *S, cout, 1)
@@ -236,6 +242,7 @@ def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S):
         close(var, yref.var(1, unbiased=False), 1e-3, "big-box stats var")
     finally:
         L.query("pcms_conv3_big_min_boxes", old)
+        L.query("pcms_conv3_big_max_wgs", old_w)
 
 
 @pytest.mark.parametrize("dt,code,tol", DTS)

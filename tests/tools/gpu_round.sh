@@ -20,8 +20,8 @@ if [[ " $STEPS " == *" bench "* ]]; then
 fi
 if [[ " $STEPS " == *" prof "* ]]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OLDPWD/gpurun_out/${TAG}_prof -o prof -- \
-    python3 $OLDPWD/bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OLDPWD/gpurun_out/${TAG}_prof.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OLDPWD/gpurun_out/${TAG}_prof -o prof -- \
+    python3 $OLDPWD/bench.py --steps 5 --warmup 2 --no-cpu-baseline --fp32-steps 0 ${BENCH_ARGS:-} > $OLDPWD/gpurun_out/${TAG}_prof.log 2>&1
   rc=$?; echo "prof rc=$rc"
   exit $rc
 fi

@@ -1,0 +1,107 @@
+"""Per-launch timing of one training step at a BASELINE config (HIP events around every
+library call the engine makes, median over the recorded steps), with FLOPs and the MFMA
+fraction for the conv launches.  Diagnostic tool for profiles/ (not a test)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+PEAK = 2.5e15
+
+
+def flops(name, a):
+    if name == "pcms_conv3_fwd":
+        return 2 * 27 * (a[2] + a[4]) * a[17] * a[13] * a[14] * a[15] * a[16]
+    if name == "pcms_conv3_wgrad":
+        return 2 * 27 * (a[2] + a[4]) * a[12] * a[8] * a[9] * a[10] * a[11]
+    if name == "pcms_stem_fwd":
+        return 2 * 27 * 5 * 64 * a[5] * a[6] * a[7] * a[8]
+    if name == "pcms_stem_wgrad":
+        return 2 * 27 * 5 * 64 * a[5] * a[6] * a[7] * a[8]
+    if name in ("pcms_convt_fwd", "pcms_convt_wgrad"):
+        return 2 * 8 * a[9] * a[10] * a[5] * a[6] * a[7] * a[8]
+    if name == "pcms_convt_dgrad":
+        return 2 * 8 * a[8] * a[9] * a[4] * a[5] * a[6] * a[7]
+    return 0
+
+
+def desc(name, a):
+    if name == "pcms_conv3_fwd":
+        return f"{a[2]}+{a[4]}->{a[17]} {a[14]}x{a[15]}x{a[16]} sp{a[18]}" + (" dgrad" if a[6] is None else "")
+    if name == "pcms_conv3_wgrad":
+        return f"{a[2]}+{a[4]}->{a[12]} {a[9]}x{a[10]}x{a[11]}"
+    if name == "pcms_convt_dgrad":
+        return f"{a[8]}->{a[9]} {a[5]}x{a[6]}x{a[7]}"
+    if name in ("pcms_convt_fwd", "pcms_convt_wgrad"):
+        return f"{a[9]}->{a[10]} {a[6]}x{a[7]}x{a[8]}"
+    return ""
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--size", default="128,128,64")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import pcms_amd  # noqa: F401
+    from pcms_amd import engine as E
+    from pcms_amd.synthetic import make_batch
+    from pcms_amd.utils.trainer import Trainer
+    spatial = tuple(int(v) for v in a.size.split(","))
+    torch.manual_seed(0)
+    tr = Trainer({"device": "cuda", "learning_rate": 1e-4, "batch_size": a.batch, "num_epochs": 1,
+                  "loss": "bce_dice", "precision": "bf16"})
+    b = make_batch(a.batch, spatial, seed=1)
+    batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
+    for _ in range(3):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    orig = E.call
+    rec = []
+
+    def timed(name, *args):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = orig(name, *args)
+        e.record()
+        rec.append((name, args, s, e))
+        return r
+    mods = [m for k, m in sys.modules.items() if k.startswith("pcms_amd") and getattr(m, "call", None) is orig]
+    for m in mods:
+        m.call = timed
+    per = []
+    for _ in range(a.steps):
+        rec.clear()
+        tr.step(batch)
+        torch.cuda.synchronize()
+        per.append([(n, ar, s.elapsed_time(e) * 1e3) for n, ar, s, e in rec])
+    for m in mods:
+        m.call = orig
+    rows = []
+    for i, (n, ar, _) in enumerate(per[0]):
+        us = statistics.median(p[i][2] for p in per)
+        f = flops(n, ar)
+        rows.append({"i": i, "name": n, "desc": desc(n, ar), "us": round(us, 1), "gflop": round(f / 1e9, 2),
+                     "mfma_frac": round(f / (us * 1e-6) / PEAK, 3) if f else None})
+    tot = sum(r["us"] for r in rows)
+    by = {}
+    for r in rows:
+        by[r["name"]] = by.get(r["name"], 0) + r["us"]
+    print(f"sum of launches {tot / 1e3:.2f} ms")
+    for k, v in sorted(by.items(), key=lambda kv: -kv[1]):
+        print(f"  {k:28s} {v / 1e3:7.3f} ms")
+    for r in sorted(rows, key=lambda r: -r["us"])[:60]:
+        print(f"{r['i']:4d} {r['name']:22s} {r['desc']:34s} {r['us']:8.1f} us  {r['gflop']:8.1f} GF  {r['mfma_frac']}")
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"batch": a.batch, "size": spatial, "rows": rows}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
