@@ -155,6 +155,21 @@ int pcms_loss_bwd(const float* x, const float* t, long M, const double* sums, fl
  * coefficient x AMP unscale, from pcms_grad_clip).  When s != 1, s * g is written back to g. */
 int pcms_adam(float* p, float* g, float* m, float* v, long n, float step_size, float b1, float b2,
               float eps, float wd, float bc2_sqrt, float gscale, const float* gmul, hipStream_t s);
+/* The same update split three ways so the weight packs come out of the same pass (bf16
+ * build): conv weights by table rows int64[8] = {flat offset, Cout, Cin, fwd pack, dgrad
+ * pack, first tile, 0, 0} (one 32 x 32 tile per block, Cout % 32 == Cin % 32 == 0) writing
+ * both pcms_conv3_pack2 packs; ConvTranspose3d weights by rows {offset, Cin, Cout, fwd pack,
+ * dgrad pack, first tile, 0, 0} writing both pcms_convt_pack packs; every other parameter
+ * through [begin, end) element ranges (int64 pairs).  Identical per-element arithmetic.   */
+int pcms_adam_pack_conv3(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                         float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                         const float* gmul, hipStream_t s);
+int pcms_adam_pack_convt(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                         float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                         const float* gmul, hipStream_t s);
+int pcms_adam_ranges(float* p, float* g, float* m, float* v, const long long* ranges, int nranges, long max_len,
+                     float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                     const float* gmul, hipStream_t s);
 
 /* ---- torch.nn.utils.clip_grad_norm_(params, max_norm): train_bph.py:166,
  * train_bph_cv.py:311 ------------------------------------------------------------------

@@ -59,6 +59,9 @@ SIGNATURES = {
     "pcms_loss_fwd": "pplfffppps",
     "pcms_loss_bwd": "pplpfffpps",
     "pcms_adam": "pppplfffffffps",
+    "pcms_adam_pack_conv3": "pppppiifffffffps",
+    "pcms_adam_pack_convt": "pppppiifffffffps",
+    "pcms_adam_ranges": "pppppilfffffffps",
     "pcms_grad_clip_ws_doubles": "",
     "pcms_grad_clip": "plffippps",
     "pcms_add": "ippls",

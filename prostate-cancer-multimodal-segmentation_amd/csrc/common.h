@@ -110,6 +110,27 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// One Adam element update (torch.optim.Adam, coupled weight decay): g_eff = g * s (written
+// back when s != 1), shared by the flat Adam kernel and the fused Adam + weight-pack kernels
+// so every path performs the identical fp32 operation sequence.
+struct AdamCoef {
+  float step_size, b1, b2, eps, wd, bc2_sqrt, gscale;
+};
+__device__ __forceinline__ float adam_update(float& p, float& g, float& m, float& v, const AdamCoef& c, float s) {
+  float gi = g;
+  if (s != 1.f) {
+    gi *= s;
+    g = gi;
+  }
+  const float pi = p;
+  if (c.wd != 0.f) gi = gi + c.wd * pi;
+  m = m + (1.f - c.b1) * (gi - m);                  // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * c.b2 + (1.f - c.b2) * gi * gi;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+  const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
+  p = pi - c.step_size * (m / denom);
+  return p;
+}
+
 #define PCMS_CHECK_LAUNCH() return (int)hipGetLastError()
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -874,6 +874,65 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* 
   }
 }
 
+// Adam + both bf16 packs in one pass over the conv weights (the flat master is read once per
+// step instead of once for Adam and once more for the packs).  One block per (conv, 32 co x
+// 32 ci) tile of a table entry [off, Cout, Cin, fwd pack, dgrad pack, first tile, -, -]
+// (int64 each): the tile's 32 contiguous 864-float runs w[co][ci0..ci0+32][27] are updated
+// in place (p, m, v, and g when scaled), the new weights converted to bf16 into LDS, and both
+// packs written as in pack_conv3_bf16_both_kernel.
+__global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* Gr, float* Mo, float* Vo,
+                                                              const long long* tab, int ntab, AdamCoef c,
+                                                              const float* gmul) {
+  __shared__ __attribute__((aligned(16))) uint16_t tb[32 * 864];
+  int ei = 0;
+  while (ei + 1 < ntab && tab[8 * (ei + 1) + 5] <= (long long)blockIdx.x) ++ei;
+  const long long* e = tab + 8 * ei;
+  const long off = (long)e[0];
+  const int Cout = (int)e[1], Cin = (int)e[2];
+  bf16_t* fwd = reinterpret_cast<bf16_t*>(e[3]);
+  bf16_t* dgr = reinterpret_cast<bf16_t*>(e[4]);
+  const int local = blockIdx.x - (int)e[5];
+  const int j0 = (local % (Cout / 32)) * 32, chunk = local / (Cout / 32);
+  const float s = gmul ? c.gscale * gmul[0] : c.gscale;
+  for (int i = 0; i < 27; ++i) {
+    const int q4 = threadIdx.x + i * 256, run = q4 / 216, q = q4 % 216;
+    const long idx = off + ((long)(j0 + run) * Cin + chunk * 32) * 27 + 4 * q;
+    f32x4_t pv = *reinterpret_cast<const f32x4_t*>(P + idx), gv = *reinterpret_cast<const f32x4_t*>(Gr + idx);
+    f32x4_t mv = *reinterpret_cast<const f32x4_t*>(Mo + idx), vv = *reinterpret_cast<const f32x4_t*>(Vo + idx);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float pk = pv[k], gk = gv[k], mk = mv[k], vk = vv[k];
+      adam_update(pk, gk, mk, vk, c, s);
+      pv[k] = pk; gv[k] = gk; mv[k] = mk; vv[k] = vk;
+    }
+    *reinterpret_cast<f32x4_t*>(P + idx) = pv;
+    *reinterpret_cast<f32x4_t*>(Mo + idx) = mv;
+    *reinterpret_cast<f32x4_t*>(Vo + idx) = vv;
+    if (s != 1.f) *reinterpret_cast<f32x4_t*>(Gr + idx) = gv;
+    uint2 o;
+    o.x = pack_bf16x2(pv[0], pv[1]);
+    o.y = pack_bf16x2(pv[2], pv[3]);
+    *reinterpret_cast<uint2*>(tb + run * 864 + 4 * q) = o;
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < 27 * 128; g += 256) {
+    const int t = g >> 7, co = (g >> 2) & 31, k8 = (g & 3) * 8;
+    u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (uint32_t)tb[co * 864 + (k8 + 2 * i) * 27 + t] | ((uint32_t)tb[co * 864 + (k8 + 2 * i + 1) * 27 + t] << 16);
+    *reinterpret_cast<u32x4_t*>(fwd + (((long)chunk * 27 + t) * Cout + j0 + co) * 32 + k8) = o;
+  }
+  for (int g = threadIdx.x; g < 27 * 128; g += 256) {
+    const int t = g >> 7, ci = (g >> 2) & 31, k8 = (g & 3) * 8, ts = 26 - t;
+    u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (uint32_t)tb[(k8 + 2 * i) * 864 + ci * 27 + ts] | ((uint32_t)tb[(k8 + 2 * i + 1) * 864 + ci * 27 + ts] << 16);
+    *reinterpret_cast<u32x4_t*>(dgr + (((long)(j0 >> 5) * 27 + t) * Cin + chunk * 32 + ci) * 32 + k8) = o;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Big-box forward / dgrad (bf16; the level-0/1 hot case: D % 8 == H % 8 == 0, W % 16 == 0,
 // input channels in 16-channel chunks), PERSISTENT: one 4-wave workgroup per CU, one grid of
@@ -1272,6 +1331,17 @@ int pcms_conv3_pack2(int dtype, const float* w, void* fwd, void* dgrad, int Cout
   }
   const int rc = pcms_conv3_pack(dtype, w, fwd, Cout, Cin, 0, s);
   return rc ? rc : pcms_conv3_pack(dtype, w, dgrad, Cout, Cin, 1, s);
+}
+
+// Adam over the conv weights of a table (see adam_pack_conv3_kernel; every entry has
+// Cout % 32 == Cin % 32 == 0 and 16-B aligned offsets), writing both bf16 packs.
+int pcms_adam_pack_conv3(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                         float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                         const float* gmul, hipStream_t s) {
+  if (ntab <= 0 || ntiles <= 0) return 0;
+  const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
+  hipLaunchKernelGGL(adam_pack_conv3_kernel, dim3(ntiles), dim3(256), 0, s, p, g, m, v, table, ntab, c, gmul);
+  PCMS_CHECK_LAUNCH();
 }
 
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s) {

@@ -416,6 +416,67 @@ __global__ void convt_pack_kernel(const float* w, T* out, int Cin, int Cout, int
   }
 }
 
+// Adam + both bf16 ConvTranspose3d packs in one pass (cf. adam_pack_conv3_kernel).  Table
+// entry [off, Cin, Cout, fwd pack, dgrad pack, first tile, -, -] (int64); one block per
+// (32 ci x 32 co) tile: the 32 contiguous 256-float runs w[ci][co0..co0+32][8] are updated,
+// converted to bf16 into LDS, and written as
+//   fwd   [t][co][ci]   (64-B runs of 32 ci)
+//   dgrad [ci][t][co]   (64-B runs of 32 co)
+__global__ void __launch_bounds__(256) adam_pack_convt_kernel(float* P, float* Gr, float* Mo, float* Vo,
+                                                              const long long* tab, int ntab, AdamCoef c,
+                                                              const float* gmul) {
+  __shared__ __attribute__((aligned(16))) uint16_t tb[32 * 256];  // [ci][co][t]
+  int ei = 0;
+  while (ei + 1 < ntab && tab[8 * (ei + 1) + 5] <= (long long)blockIdx.x) ++ei;
+  const long long* e = tab + 8 * ei;
+  const long off = (long)e[0];
+  const int Cin = (int)e[1], Cout = (int)e[2];
+  bf16_t* fwd = reinterpret_cast<bf16_t*>(e[3]);
+  bf16_t* dgr = reinterpret_cast<bf16_t*>(e[4]);
+  const int local = blockIdx.x - (int)e[5];
+  const int co0 = (local % (Cout / 32)) * 32, ci0 = (local / (Cout / 32)) * 32;
+  const float s = gmul ? c.gscale * gmul[0] : c.gscale;
+  for (int i = 0; i < 8; ++i) {
+    const int q4 = threadIdx.x + i * 256, run = q4 >> 6, q = q4 & 63;
+    const long idx = off + ((long)(ci0 + run) * Cout + co0) * 8 + 4 * q;
+    f32x4_t pv = *reinterpret_cast<const f32x4_t*>(P + idx), gv = *reinterpret_cast<const f32x4_t*>(Gr + idx);
+    f32x4_t mv = *reinterpret_cast<const f32x4_t*>(Mo + idx), vv = *reinterpret_cast<const f32x4_t*>(Vo + idx);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float pk = pv[k], gk = gv[k], mk = mv[k], vk = vv[k];
+      adam_update(pk, gk, mk, vk, c, s);
+      pv[k] = pk; gv[k] = gk; mv[k] = mk; vv[k] = vk;
+    }
+    *reinterpret_cast<f32x4_t*>(P + idx) = pv;
+    *reinterpret_cast<f32x4_t*>(Mo + idx) = mv;
+    *reinterpret_cast<f32x4_t*>(Vo + idx) = vv;
+    if (s != 1.f) *reinterpret_cast<f32x4_t*>(Gr + idx) = gv;
+    uint2 o;
+    o.x = pack_bf16x2(pv[0], pv[1]);
+    o.y = pack_bf16x2(pv[2], pv[3]);
+    *reinterpret_cast<uint2*>(tb + run * 256 + 4 * q) = o;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 8 * 32 * 4; k += 256) {  // fwd: (t, co, 8-ci group)
+    const int grp = k & 3, co = (k >> 2) & 31, t = k >> 7;
+    u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (uint32_t)tb[(grp * 8 + 2 * i) * 256 + co * 8 + t] |
+             ((uint32_t)tb[(grp * 8 + 2 * i + 1) * 256 + co * 8 + t] << 16);
+    *reinterpret_cast<u32x4_t*>(fwd + ((long)t * Cout + co0 + co) * Cin + ci0 + grp * 8) = o;
+  }
+  for (int k = threadIdx.x; k < 32 * 8 * 4; k += 256) {  // dgrad: (ci, t, 8-co group)
+    const int grp = k & 3, t = (k >> 2) & 7, ci = k >> 5;
+    u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      o[i] = (uint32_t)tb[ci * 256 + (grp * 8 + 2 * i) * 8 + t] |
+             ((uint32_t)tb[ci * 256 + (grp * 8 + 2 * i + 1) * 8 + t] << 16);
+    *reinterpret_cast<u32x4_t*>(dgr + ((long)(ci0 + ci) * 8 + t) * Cout + co0 + grp * 8) = o;
+  }
+}
+
 UpGeom make_geom(int N, int Din, int Hin, int Win, int Do, int Ho, int Wo) {
   UpGeom g;
   g.N = N; g.Din = Din; g.Hin = Hin; g.Win = Win; g.Do = Do; g.Ho = Ho; g.Wo = Wo;
@@ -426,6 +487,17 @@ UpGeom make_geom(int N, int Din, int Hin, int Win, int Do, int Ho, int Wo) {
 }  // namespace
 
 extern "C" {
+
+// Adam over the ConvTranspose3d weights of a table (Cin % 32 == Cout % 32 == 0), writing both
+// bf16 packs (pcms_convt_pack layouts).
+int pcms_adam_pack_convt(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                         float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                         const float* gmul, hipStream_t s) {
+  if (ntab <= 0 || ntiles <= 0) return 0;
+  const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
+  hipLaunchKernelGGL(adam_pack_convt_kernel, dim3(ntiles), dim3(256), 0, s, p, g, m, v, table, ntab, c, gmul);
+  PCMS_CHECK_LAUNCH();
+}
 
 int pcms_convt_pack(int dtype, const float* w, void* out, int Cin, int Cout, int dgrad, hipStream_t s) {
   const long total = (long)Cin * Cout * 8;

@@ -505,24 +505,31 @@ __global__ void loss_bwd_kernel(const float* x, const float* t, long M, const do
 // g_eff = g * s, s = gscale * (*gmul if gmul) (the data-parallel 1/world mean, the gradient-
 // clip coefficient, the AMP unscale); when s != 1 the scaled gradient is also written back,
 // so param.grad afterwards holds what torch's clip_grad_norm_ / DDP mean would leave there.
-__global__ void adam_kernel(float* p, float* g, float* m, float* v, long n, float step_size, float b1,
-                            float b2, float eps, float wd, float bc2_sqrt, float gscale, const float* gmul) {
-  const float s = gmul ? gscale * gmul[0] : gscale;
+__global__ void adam_kernel(float* p, float* g, float* m, float* v, long n, AdamCoef c, const float* gmul) {
+  const float s = gmul ? c.gscale * gmul[0] : c.gscale;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gi = g[i];
-    if (s != 1.f) {
-      gi *= s;
-      g[i] = gi;
-    }
-    const float pi = p[i];
-    if (wd != 0.f) gi = gi + wd * pi;
-    float mi = m[i];
-    mi = mi + (1.f - b1) * (gi - mi);               // exp_avg.lerp_(grad, 1 - beta1)
-    float vi = v[i] * b2 + (1.f - b2) * gi * gi;    // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
+    adam_update(pi, gi, mi, vi, c, s);
+    if (s != 1.f) g[i] = gi;
     m[i] = mi;
     v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = pi - step_size * (mi / denom);
+    p[i] = pi;
+  }
+}
+
+// The same over a list of [begin, end) element ranges of the flat buffers (the parameters the
+// fused Adam + weight-pack kernels do not cover): blockIdx.y = range.
+__global__ void adam_ranges_kernel(float* p, float* g, float* m, float* v, const long long* ranges, AdamCoef c,
+                                   const float* gmul) {
+  const float s = gmul ? c.gscale * gmul[0] : c.gscale;
+  const long b = ranges[2 * blockIdx.y], e = ranges[2 * blockIdx.y + 1];
+  for (long i = b + blockIdx.x * (long)blockDim.x + threadIdx.x; i < e; i += (long)gridDim.x * blockDim.x) {
+    float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
+    adam_update(pi, gi, mi, vi, c, s);
+    if (s != 1.f) g[i] = gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
   }
 }
 
@@ -845,7 +852,18 @@ int pcms_loss_bwd(const float* x, const float* t, long M, const double* sums, fl
 // step_size = lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)  (host fp64 -> fp32)
 int pcms_adam(float* p, float* g, float* m, float* v, long n, float step_size, float b1, float b2, float eps,
               float wd, float bc2_sqrt, float gscale, const float* gmul, hipStream_t s) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, TPB, 16384)), dim3(TPB), 0, s, p, g, m, v, n, step_size, b1, b2, eps, wd, bc2_sqrt, gscale, gmul);
+  const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, TPB, 16384)), dim3(TPB), 0, s, p, g, m, v, n, c, gmul);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_adam_ranges(float* p, float* g, float* m, float* v, const long long* ranges, int nranges, long max_len,
+                     float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                     const float* gmul, hipStream_t s) {
+  if (nranges <= 0) return 0;
+  const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
+  hipLaunchKernelGGL(adam_ranges_kernel, dim3(grid_for(max_len, TPB, 2048), nranges), dim3(TPB), 0, s, p, g, m, v,
+                     ranges, c, gmul);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -105,6 +105,8 @@ class UNetEngine:
         self._flat_ptrs = None
         self._packed_version = -1
         self._dirty = True
+        self._packs_fresh = False  # the fused Adam wrote every conv / ConvT pack (not the stem's)
+        self._adam_plan = None
         self.bufs = None
         self.buf_key = None
         self.epoch = 0
@@ -161,6 +163,7 @@ class UNetEngine:
         self.flat_p, self.flat_g, self.flat_bn = flat, gflat, bflat
         self._flat_ptrs = [p.data_ptr() for p in params]
         self._dirty = True
+        self._adam_plan = None
         self.grad_ranges = module_grad_ranges(self.model)
 
     def _grads_done(self, module: str):
@@ -209,12 +212,80 @@ class UNetEngine:
                 p.grad = view
             off += n
 
-    def mark_dirty(self):
+    def mark_dirty(self, packs_fresh: bool = False):
+        """The master weights changed.  ``packs_fresh``: the fused Adam (adam_plan) already
+        wrote the conv and ConvT packs from the new weights; only the stem's remain."""
         self._dirty = True
+        self._packs_fresh = packs_fresh and self._packed_version == self.flat_p._version
+
+    def adam_plan(self):
+        """Fused Adam + weight-pack plan of the bf16 build (FlatAdam.step): device tables of
+        the conv / ConvT weights whose packs the Adam kernels write (int64 rows, see
+        include/pcms_hip.h pcms_adam_pack_conv3) and the [begin, end) ranges of every other
+        parameter.  None for the fp32 build."""
+        if self.code != BF16:
+            return None
+        if self._adam_plan is not None:
+            return self._adam_plan
+        self._ensure_packs()
+        base = self.flat_p.data_ptr()
+
+        def offset(t):
+            return (t.data_ptr() - base) // 4
+
+        fused = []
+        conv_rows, tiles = [], 0
+        for i, cs in enumerate(self.convs):
+            w = cs.mod.weight
+            if i == 0 or cs.cin % 32 or cs.cout % 32 or offset(w) % 4:
+                continue
+            conv_rows.append([offset(w), cs.cout, cs.cin, cs.fwd.data_ptr(), cs.dgrad.data_ptr(), tiles, 0, 0])
+            tiles += (cs.cout // 32) * (cs.cin // 32)
+            fused.append((offset(w), w.numel()))
+        ct_rows, ct_tiles = [], 0
+        for i, up in enumerate(self.ups):
+            w = up.weight
+            cin, cout = up.in_channels, up.out_channels
+            if cin % 32 or cout % 32 or offset(w) % 4:
+                continue
+            f, d = self.convt_packs[i]
+            ct_rows.append([offset(w), cin, cout, f.data_ptr(), d.data_ptr(), ct_tiles, 0, 0])
+            ct_tiles += (cin // 32) * (cout // 32)
+            fused.append((offset(w), w.numel()))
+        ranges, pos = [], 0
+        for off, n in sorted(fused):
+            if off > pos:
+                ranges.append([pos, off])
+            pos = off + n
+        if pos < self.flat_p.numel():
+            ranges.append([pos, self.flat_p.numel()])
+        dev = self.device
+
+        def tab(rows):
+            return torch.tensor(rows if rows else [[0] * 8], dtype=torch.int64, device=dev)
+        self._adam_plan = {
+            "conv": tab(conv_rows), "nconv": len(conv_rows), "conv_tiles": tiles,
+            "convt": tab(ct_rows), "nconvt": len(ct_rows), "convt_tiles": ct_tiles,
+            "ranges": torch.tensor(ranges if ranges else [[0, 0]], dtype=torch.int64, device=dev),
+            "nranges": len(ranges), "max_len": max([e - b for b, e in ranges], default=0),
+        }
+        return self._adam_plan
 
     def _ensure_packs(self):
         v = self.flat_p._version
         if not self._dirty and v == self._packed_version:
+            return
+        if self._packs_fresh and v == self._packed_version:
+            # the fused Adam rewrote every conv / ConvT pack: only the stem's are left
+            cs = self.convs[0]
+            if cs.dgrad is None:
+                call("pcms_conv3_pack", self.code, cs.mod.weight, cs.fwd, cs.cout, cs.cin, 0)
+            else:
+                call("pcms_conv3_pack2", self.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
+            if self.stem_fast:
+                call("pcms_stem_pack", cs.mod.weight, self.stem_pack, self.nmod)
+            self._dirty = False
+            self._packs_fresh = False
             return
         ck = query("pcms_conv3_chunk", self.code)
         for i, cs in enumerate(self.convs):
@@ -243,6 +314,7 @@ class UNetEngine:
             call("pcms_convt_pack", self.code, up.weight, d, cin, cout, 1)
         self._packed_version = self.flat_p._version
         self._dirty = False
+        self._packs_fresh = False
 
     # ------------------------------------------------------------------ buffers
     def _levels(self, D, H, W):

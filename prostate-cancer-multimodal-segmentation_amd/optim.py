@@ -30,6 +30,7 @@ class FlatAdam(torch.optim.Optimizer):
         # clip coefficient / AMP unscale), both folded into the single Adam pass
         self.grad_scale = 1.0
         self.grad_mul = None
+        self.fused_packs = True  # bf16 build: Adam writes the conv / ConvT packs (engine.adam_plan)
         self._m = None
         self._v = None
 
@@ -55,13 +56,22 @@ class FlatAdam(torch.optim.Optimizer):
         b1, b2 = g["betas"]
         bc1 = 1.0 - b1 ** self.step_count
         bc2 = 1.0 - b2 ** self.step_count
-        call("pcms_adam", eng.flat_p, eng.flat_g, m, v, eng.flat_p.numel(), g["lr"] / bc1, b1, b2, g["eps"],
-             g["weight_decay"], math.sqrt(bc2), float(self.grad_scale), self.grad_mul)
+        coef = (g["lr"] / bc1, b1, b2, g["eps"], g["weight_decay"], math.sqrt(bc2), float(self.grad_scale))
+        plan = eng.adam_plan() if self.fused_packs else None
+        if plan is not None:
+            # bf16 build: the conv / ConvT weight packs come out of the Adam pass itself
+            P = (eng.flat_p, eng.flat_g, m, v)
+            call("pcms_adam_pack_conv3", *P, plan["conv"], plan["nconv"], plan["conv_tiles"], *coef, self.grad_mul)
+            call("pcms_adam_pack_convt", *P, plan["convt"], plan["nconvt"], plan["convt_tiles"], *coef,
+                 self.grad_mul)
+            call("pcms_adam_ranges", *P, plan["ranges"], plan["nranges"], plan["max_len"], *coef, self.grad_mul)
+        else:
+            call("pcms_adam", eng.flat_p, eng.flat_g, m, v, eng.flat_p.numel(), *coef, self.grad_mul)
         # one-shot multipliers of this step's gradient (the kernel wrote the scaled gradient
         # back into param.grad)
         self.grad_scale = 1.0
         self.grad_mul = None
-        eng.mark_dirty()
+        eng.mark_dirty(packs_fresh=plan is not None)
         return loss
 
     def zero_grad(self, set_to_none: bool = True):

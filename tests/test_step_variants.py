@@ -150,3 +150,46 @@ def test_grad_scaler_step_skip_and_scale_update():
         amp.step(batch)
     assert sc.get_scale() == 2.0 ** 16
     assert math.isfinite(float(amp.last_grad_norm))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gscale", [1.0, 0.5])
+def test_fused_adam_packs_match_flat_adam(gscale):
+    """bf16 build: the fused Adam (pcms_adam_pack_conv3 / _convt / _ranges, engine.adam_plan)
+    matches the flat Adam kernel (same per-element arithmetic; the compiler may contract it
+    differently, so to 1e-6 relative), and the conv / ConvT weight packs it writes are
+    bit-identical to the pack kernels run on the updated master."""
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    gen = torch.Generator().manual_seed(2)
+    x = torch.rand(2, 5, 16, 16, 16, generator=gen).cuda()
+    y = (torch.rand(2, 1, 16, 16, 16, generator=gen) < 0.5).float().cuda()
+    runs = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        m = UNet3D(n_modalities=5, n_classes=1).cuda()
+        opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
+        opt.fused_packs = fused
+        opt.zero_grad()
+        BCEDiceLoss()(m(x), y).backward()
+        opt.grad_scale = gscale
+        opt.step()
+        eng = m.engine()
+        eng._ensure_packs()
+        torch.cuda.synchronize()
+        runs.append((eng, opt))
+    (e0, o0), (e1, o1) = runs
+    plan = e1.adam_plan()
+    assert plan["nconv"] == 17 and plan["nconvt"] == 4
+    for a, b in ((e0.flat_p, e1.flat_p), (e0.flat_g, e1.flat_g), (o0._m, o1._m), (o0._v, o1._v)):
+        torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-12)
+    packs = [t.clone() for cs in e1.convs for t in (cs.fwd, cs.dgrad) if t is not None]
+    packs += [t.clone() for i in range(4) for t in e1.convt_packs[i]]
+    e1.mark_dirty()
+    e1._ensure_packs()  # full repack from the fused step's master
+    fresh = [t for cs in e1.convs for t in (cs.fwd, cs.dgrad) if t is not None]
+    fresh += [t for i in range(4) for t in e1.convt_packs[i]]
+    torch.cuda.synchronize()
+    for a, b in zip(packs, fresh):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
