@@ -1097,6 +1097,12 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   int box = slot;
   int n, d0, h0, w0;
   origin(box, n, d0, h0, w0);
+  // Short boxes (4 chunks): every CU would reach its box boundary -- the vmcnt(0), the 128 KiB
+  // store burst and the next halo's first pieces -- at the same moment; starting slot s
+  // (s % 4) x ~16k cycles late spreads those bursts (measured 517 -> 433 us at level 0,
+  // 64 -> 64; no effect with 8+ chunks, so not applied there).
+  if (nchunk <= 4)
+    for (int i = 0; i < 2 * (slot & 3); ++i) __builtin_amdgcn_s_sleep(127);
 #pragma unroll
   for (int j = 0; j < kBgPieces; ++j) stage_piece(n, d0, h0, w0, 0, 0, j, true);
 #pragma unroll

@@ -50,6 +50,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) big_exp_kernel(Conv3Params p, u
         (unsigned)gw < (unsigned)p.W)
       voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs +
               (uint32_t)((pc & 1) ^ ((hw_ >> 3) & 1)) * 8u) * 2u;
+    if constexpr ((F & 32) != 0) voff = voff == kOOB ? kOOB : (voff & 0xFFFFFu);  // halo from 1 MiB (L2-resident)
     const uint32_t lb = __builtin_amdgcn_readfirstlane(lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
     dma16(first ? xr0 : xr1, lb, voff, 0);
   };
@@ -96,6 +97,14 @@ __global__ void __launch_bounds__(kBgThreads, 1) big_exp_kernel(Conv3Params p, u
   int box = slot;
   int n, d0, h0, w0;
   origin(box, n, d0, h0, w0);
+  if constexpr ((F & 64) != 0) {
+    // desynchronise: odd slots start ~half a box later (store bursts of neighbouring CUs
+    // no longer coincide)
+    // p.accumulate = (modulus << 8) | sleeps per step: slot s waits (s % modulus) * sleeps
+    const int mod = p.accumulate >> 8, units = p.accumulate & 255;
+    const int k = mod > 0 ? (slot % mod) * units : 0;
+    for (int i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(127);
+  }
 #pragma unroll
   for (int j = 0; j < kBgPieces; ++j) stage_piece(n, d0, h0, w0, 0, 0, j, true);
 #pragma unroll
@@ -276,6 +285,8 @@ __global__ void __launch_bounds__(kBgThreads, 1) big_exp_kernel(Conv3Params p, u
 extern "C" int exp_big(int F, const void* x0, int c0, const void* x1, int c1, const void* w, const float* bias,
                        void* y, float* stats, int N, int D, int H, int W, int Cout, int wgs, hipStream_t s) {
   Conv3Params p = {};
+  p.accumulate = wgs >> 16;  // delay config (F & 64)
+  wgs &= 0xffff;
   p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1; p.w = w; p.bias = bias; p.y0 = y; p.y1 = nullptr; p.cy0 = Cout;
   p.stats = stats; p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = c0 + c1; p.Cout = Cout;
   p.nvox = (long)N * D * H * W;
@@ -299,6 +310,10 @@ extern "C" int exp_big(int F, const void* x0, int c0, const void* x1, int c1, co
     case 15: launch(big_exp_kernel<15>); break;
     case 16: launch(big_exp_kernel<16>); break;
     case 23: launch(big_exp_kernel<23>); break;
+    case 32: launch(big_exp_kernel<32>); break;
+    case 36: launch(big_exp_kernel<36>); break;
+    case 64: launch(big_exp_kernel<64>); break;
+    case 68: launch(big_exp_kernel<68>); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -11,7 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 NAMES = {0: "product", 1: "no halo HBM", 2: "B one line", 3: "no halo + B one line", 4: "no stores",
          7: "no halo/B/stores", 8: "no A reads", 15: "no halo/B/stores/A", 16: "no MFMA",
-         23: "no halo/B/stores/MFMA"}
+         23: "no halo/B/stores/MFMA", 32: "halo from 1 MiB (L2 hits)", 36: "halo L2 hits, no stores",
+         64: "odd slots start half a box late", 68: "desync + no stores"}
 
 
 def main():
@@ -45,11 +46,13 @@ def main():
         same = torch.equal(y.view(torch.int16), y2.view(torch.int16))
         print(f"== {c0}+{c1}->{cout}: F=0 rc {rc} equal to product: {same}", flush=True)
         flop = 2.0 * nvox * cout * cin * 27
-        for F in NAMES:
+        runs = [(int(f), 0) for f in os.environ.get("FLAGS", "").split(",") if f] or [(f, 0) for f in NAMES]
+        runs += [(64, int(d, 0)) for d in os.environ.get("DELAYS", "").split(",") if d]
+        for F, dly in runs:
             def run(i):
                 a, b = xs[i % 3]
                 return ex.exp_big(F, P(a), c0, P(b) if c1 else None, c1, P(wp), P(bias), P(y2), P(stats),
-                                  N, D, H, W, cout, 0, st())
+                                  N, D, H, W, cout, dly << 16, st())
             for i in range(3):
                 run(i)
             torch.cuda.synchronize()
@@ -60,7 +63,8 @@ def main():
             e1.record()
             e1.synchronize()
             t = e0.elapsed_time(e1) / 20 * 1e-3
-            print(f"   F={F:2d} {NAMES[F]:28s} {t * 1e6:8.1f} us  {flop / t / 1e12:7.1f} TF/s", flush=True)
+            label = NAMES[F] if not dly else f"delay (slot % {dly >> 8}) x {dly & 255} sleeps"
+            print(f"   F={F:2d} {label:34s} {t * 1e6:8.1f} us  {flop / t / 1e12:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
