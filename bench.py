@@ -92,13 +92,16 @@ def stem_roofline(tr, N, spatial, reps):
         for i in range(3):
             fn(sets[i % 3])
         torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        for i in range(reps):
-            fn(sets[i % 3])
-        ev1.record()
-        ev1.synchronize()
-        res[name] = ev0.elapsed_time(ev1) / reps * 1e-3  # s per launch
+        trials = []
+        for _ in range(3):  # median of 3 averages of `reps` back-to-back launches
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for i in range(reps):
+                fn(sets[i % 3])
+            ev1.record()
+            ev1.synchronize()
+            trials.append(ev0.elapsed_time(ev1) / reps * 1e-3)  # s per launch
+        res[name] = statistics.median(trials)
     es = 2 if code == 1 else 4
     # algorithmic bytes: X (5 ch) + W + Y  /  X + dY + dW
     xb = nvox * 5 * es
@@ -111,7 +114,7 @@ def stem_roofline(tr, N, spatial, reps):
     # rocprofv3 passes, gfx950 FETCH correction: tests/kexp/pmc_stem_traffic.sh), committed
     # for the shape they were measured on; null for any other shape
     traffic = None
-    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_stem_traffic.json")
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2_stem_traffic.json")
     if os.path.exists(tf):
         with open(tf) as f:
             rec = json.load(f)

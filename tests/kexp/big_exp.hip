@@ -51,6 +51,10 @@ __global__ void __launch_bounds__(kBgThreads, 1) big_exp_kernel(Conv3Params p, u
       voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs +
               (uint32_t)((pc & 1) ^ ((hw_ >> 3) & 1)) * 8u) * 2u;
     if constexpr ((F & 32) != 0) voff = voff == kOOB ? kOOB : (voff & 0xFFFFFu);  // halo from 1 MiB (L2-resident)
+    // contiguous pieces (what a 16-channel-blocked layout would fetch: every wave
+    // instruction one 1 KiB run), same byte count and LDS placement, wrong data
+    if constexpr ((F & 128) != 0)
+      voff = voff == kOOB ? kOOB : (((uint32_t)((n * p.D + d0) * p.H + h0) * 1024u + (uint32_t)pc * 16u + (uint32_t)chunk * 4096u) % (x0bytes - 16u)) & ~15u;
     const uint32_t lb = __builtin_amdgcn_readfirstlane(lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
     dma16(first ? xr0 : xr1, lb, voff, 0);
   };
@@ -313,6 +317,8 @@ extern "C" int exp_big(int F, const void* x0, int c0, const void* x1, int c1, co
     case 32: launch(big_exp_kernel<32>); break;
     case 36: launch(big_exp_kernel<36>); break;
     case 64: launch(big_exp_kernel<64>); break;
+    case 128: launch(big_exp_kernel<128>); break;
+    case 132: launch(big_exp_kernel<132>); break;
     case 68: launch(big_exp_kernel<68>); break;
     default: return -1;
   }

@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 NAMES = {0: "product", 1: "no halo HBM", 2: "B one line", 3: "no halo + B one line", 4: "no stores",
          7: "no halo/B/stores", 8: "no A reads", 15: "no halo/B/stores/A", 16: "no MFMA",
          23: "no halo/B/stores/MFMA", 32: "halo from 1 MiB (L2 hits)", 36: "halo L2 hits, no stores",
-         64: "odd slots start half a box late", 68: "desync + no stores"}
+         64: "odd slots start half a box late", 68: "desync + no stores",
+         128: "contiguous 1 KiB halo runs", 132: "contiguous halo, no stores"}
 
 
 def main():
