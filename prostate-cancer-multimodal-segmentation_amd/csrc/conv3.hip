@@ -689,10 +689,31 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           }
         }
         __syncthreads();
-        for (int i = tid; i < 32 * 32 * 27; i += kWThreads) {
-          const int col = i / 864, r = i % 864;  // r = ci * 27 + tap
-          const int co = co_base + ct * 32 + col;
-          if (co < p.Cout && r < nci * 27) p.dw[((long)co * p.cw + ci_base) * 27 + r] += tile[i];
+        if (nci == 32) {
+          // whole 32 x 864-float runs: 16-B read-modify-writes, all of a thread's loads in
+          // flight before the first add (a dependent load -> add -> store chain per element
+          // made the deep levels latency-bound)
+          constexpr int kQ = 32 * 216, kPer = (kQ + kWThreads - 1) / kWThreads;
+          f32x4_t g[kPer];
+#pragma unroll
+          for (int k = 0; k < kPer; ++k) {
+            const int q4 = tid + k * kWThreads, row = q4 / 216, q = q4 % 216;
+            if (q4 < kQ)
+              g[k] = *reinterpret_cast<const f32x4_t*>(p.dw + ((long)(co_base + ct * 32 + row) * p.cw + ci_base) * 27 + 4 * q);
+          }
+#pragma unroll
+          for (int k = 0; k < kPer; ++k) {
+            const int q4 = tid + k * kWThreads, row = q4 / 216, q = q4 % 216;
+            if (q4 < kQ)
+              *reinterpret_cast<f32x4_t*>(p.dw + ((long)(co_base + ct * 32 + row) * p.cw + ci_base) * 27 + 4 * q) =
+                  g[k] + *reinterpret_cast<const f32x4_t*>(tile + row * 864 + 4 * q);
+          }
+        } else {
+          for (int i = tid; i < 32 * 32 * 27; i += kWThreads) {
+            const int col = i / 864, r = i % 864;  // r = ci * 27 + tap
+            const int co = co_base + ct * 32 + col;
+            if (co < p.Cout && r < nci * 27) p.dw[((long)co * p.cw + ci_base) * 27 + r] += tile[i];
+          }
         }
       }
       return;

@@ -252,6 +252,7 @@ def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S, wgs):
     (2, 64, 64, 64, (8, 8, 8)),
     (2, 128, 0, 128, (4, 4, 4)),
     (2, 256, 0, 64, (1, 2, 1)),
+    (1, 64, 64, 128, (4, 8, 8)),        # one box: the unsplit direct flush (16-B RMW of dw)
 ])
 def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
     L = _lib()
@@ -268,6 +269,8 @@ def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
     # the stored input may carry zero pad channels (stem: 5 of 8); dw has the weight's Cin
     guard = 4096
     dw_full = torch.zeros(cout * cin_real * 27 + guard, device=DEV)
+    init = torch.randn(cout * cin_real * 27, generator=g)  # dw accumulates (+=)
+    dw_full[:-guard] = init.to(DEV)
     ws = torch.empty(L.query("pcms_conv3_wgrad_ws_floats", code, N, *S, c0, c1, cout, 256), device=DEV)
     xs = ndhwc(x).to(DEV)
     if c1:
@@ -278,7 +281,7 @@ def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
                256)
     torch.cuda.synchronize()
     assert dw_full[-guard:].abs().max().item() == 0.0, "wgrad wrote past the weight gradient"
-    got = dw_full[:-guard].cpu().view(cout, cin_real, 3, 3, 3)
+    got = (dw_full[:-guard].cpu() - init).view(cout, cin_real, 3, 3, 3)
     close(got, wr.grad, 1e-4 if code else 2e-5, "wgrad")
 
 
