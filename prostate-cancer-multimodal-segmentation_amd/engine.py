@@ -192,10 +192,13 @@ class UNetEngine:
             torch.cuda.current_stream(self.device).wait_stream(self._side_stream)
             self._side_used = False
 
-    def sync_params(self):
+    def sync_params(self, full: bool = True):
         """Re-flatten if a module op (``.to()``, ``.cuda()``, param reassignment) replaced
-        storage, and make every ``param.grad`` a view of the flat gradient again."""
-        if [p.data_ptr() for p in self.params] != self._flat_ptrs or list(self.model.parameters()) != self.params:
+        storage, and make every ``param.grad`` a view of the flat gradient again.
+        ``full=False`` (the calls inside one step after the forward's full check) skips the
+        module walk that detects replaced Parameter objects."""
+        if [p.data_ptr() for p in self.params] != self._flat_ptrs or (
+                full and list(self.model.parameters()) != self.params):
             self._flatten()
             return
         off = 0
@@ -562,7 +565,7 @@ class UNetEngine:
         if self.saved_epoch != self.epoch:
             raise RuntimeError("UNet3D backward must follow its own training forward (the engine keeps "
                                "only the activations of the latest forward)")
-        self.sync_params()
+        self.sync_params(full=False)
         b = self.bufs
         S, C = b["S"], b["C"]
         N = self.buf_key[0]

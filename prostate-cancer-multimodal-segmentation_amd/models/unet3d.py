@@ -134,14 +134,14 @@ class UNet3D(nn.Module):
                 nn.init.constant_(m.bias, 0)
 
     # -------------------------------------------------------------- engine plumbing
-    def engine(self) -> UNetEngine:
+    def engine(self, full_sync: bool = True) -> UNetEngine:
         dev = self.outc.weight.device
         eng = self._engine
         if eng is None or eng.device != dev:
             eng = UNetEngine(self, dev, self.precision)
             self.__dict__["_engine"] = eng
         else:
-            eng.sync_params()
+            eng.sync_params(full=full_sync)
         eng.act_ckpt = self.checkpoint_decoder
         return eng
 

@@ -50,7 +50,7 @@ class FlatAdam(torch.optim.Optimizer):
         if len(self.param_groups) != 1:
             raise ValueError("FlatAdam supports a single parameter group")
         g = self.param_groups[0]
-        eng = self.model.engine()
+        eng = self.model.engine(full_sync=False)
         m, v = self._moments(eng)
         self.step_count += 1
         b1, b2 = g["betas"]
@@ -78,7 +78,7 @@ class FlatAdam(torch.optim.Optimizer):
         eng = self.model._engine
         if eng is not None:
             eng.flat_g.zero_()
-            eng.sync_params()
+            eng.sync_params(full=False)
         else:
             for p in self.model.parameters():
                 p.grad = None

@@ -138,7 +138,8 @@ class BaseTrainer:
         AMP variant has to decide whether to skip the update)."""
         images = batch["image"].to(self.device, non_blocking=True)
         labels = batch["label"].to(self.device, non_blocking=True)
-        self.model.train()
+        if not self.model.training:  # (the engine follows UNet3D.training only)
+            self.model.train()
         self.optimizer.zero_grad()
         if self.distributed:
             eng, sync = self._grad_sync()
