@@ -89,7 +89,7 @@ def stem_roofline(tr, N, spatial, reps):
 
     res = {}
     for name, fn in (("fwd", fwd), ("wgrad", wgrad)):
-        for i in range(3):
+        for i in range(reps):  # warm-up: one untimed batch of launches
             fn(sets[i % 3])
         torch.cuda.synchronize()
         trials = []
