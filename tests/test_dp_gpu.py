@@ -90,3 +90,33 @@ def test_dp_trainer_step_two_ranks(tmp_path, clip):
         assert float((r["params"] - pv).abs().max()) <= 2.01e-4
         bn = torch.cat([sd[k].reshape(-1) for k in sd if k.endswith(("running_mean", "running_var"))])
         np.testing.assert_allclose(r["bn"].numpy(), bn.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_dp_trainer_train_loop_two_ranks(tmp_path):
+    """Trainer.train() end to end on two ranks: the ranks agree on the averaged
+    losses (so ReduceLROnPlateau and early stopping take the same decisions), on the final
+    parameters and BatchNorm buffers, and only rank 0 writes checkpoints."""
+    from pcms_amd.data import DEFAULT_MODALITIES, write_nifti
+    rng = np.random.default_rng(0)
+    data = tmp_path / "data"
+    for i in range(4):
+        for m in DEFAULT_MODALITIES:
+            d = data / "BPH-PCA" / "BPH" / m
+            d.mkdir(parents=True, exist_ok=True)
+            write_nifti(str(d / f"c{i}.nii"), (rng.random((16, 16, 16)) * 10).astype(np.float32))
+        ld = data / "BPH-PCA" / "ROI(BPH+PCA)" / "BPH"
+        ld.mkdir(parents=True, exist_ok=True)
+        lab = np.zeros((16, 16, 16), np.uint8)
+        lab[4:10, 5:11, 3:9] = 1
+        write_nifti(str(ld / f"c{i}.nii"), lab)
+    save = tmp_path / "ckpt"
+    out = str(tmp_path / "train.pt")
+    env = dict(os.environ, MODE="train", DATA=str(data), SAVE=str(save))
+    port = str(_port())
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "tools", "dp_worker.py"), str(r), "2", port, out],
+                              env=env) for r in range(2)]
+    assert [p.wait(timeout=240) for p in procs] == [0, 0]
+    ranks = torch.load(out, weights_only=True)["ranks"]
+    assert ranks[0] == ranks[1]
+    assert np.isfinite(ranks[0]["best"])
+    assert (save / "latest_checkpoint.pth").exists()

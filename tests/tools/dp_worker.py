@@ -23,6 +23,8 @@ def main():
     torch.manual_seed(0)
     cfg = {"device": "cuda:0", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1, "loss": "bce_dice",
            "precision": "fp32", "dp_bucket_elems": 4 << 20, "max_grad_norm": float(os.environ.get("CLIP", "0")) or None}
+    if os.environ.get("MODE") == "train":
+        return train_mode(rank, world, out, Trainer)
     tr = Trainer(cfg)
     assert tr.distributed and tr.world_size == world
     losses = []
@@ -40,6 +42,29 @@ def main():
     if rank == 0:
         torch.save({"losses": allp, "grad": eng.flat_g.cpu(), "params": eng.flat_p.cpu(), "bn": eng.flat_bn.cpu(),
                     "norm": None if tr.last_grad_norm is None else float(tr.last_grad_norm)}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def train_mode(rank, world, out, Trainer):
+    """Trainer.train() end to end under data parallelism: per-rank DistributedSampler shards,
+    epoch losses averaged over ranks before ReduceLROnPlateau / early stopping, validation
+    with rank 0's BatchNorm buffers, checkpoints written by rank 0 only."""
+    torch.manual_seed(0)
+    cfg = {"device": "cuda:0", "learning_rate": 1e-3, "batch_size": 1, "num_epochs": 2, "loss": "bce_dice",
+           "precision": "fp32", "data_dir": os.environ["DATA"], "validation": True, "target_size": (32, 32, 32),
+           "save_dir": os.environ["SAVE"], "dp_bucket_elems": 4 << 20}
+    tr = Trainer(cfg)
+    assert tr.distributed and len(tr.train_loader) == 2  # 4 cases, 2 per rank
+    best = tr.train()
+    eng = tr.model.engine()
+    torch.cuda.synchronize()
+    rec = {"best": best, "lr": tr.optimizer.param_groups[0]["lr"], "p_sum": float(eng.flat_p.double().sum()),
+           "bn_sum": float(eng.flat_bn.double().sum())}
+    allr = [None] * world
+    dist.all_gather_object(allr, rec)
+    if rank == 0:
+        torch.save({"ranks": allr}, out)
     dist.barrier()
     dist.destroy_process_group()
 
