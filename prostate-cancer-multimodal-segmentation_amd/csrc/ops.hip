@@ -585,6 +585,7 @@ __global__ void scale_kernel(float* g, long n, const float* mul) {
 
 // fp32 split-K slabs [splits][nvox][C] -> sum in split order + bias, store T, BN partial
 // sums; 64 voxels per block row
+constexpr int kMaxSplitSlabs = 16;  // slabs loaded together (more: summed one by one after)
 template <typename T>
 __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, int splits, const float* bias, T* y0,
                                                              T* y1, int cy0, float* stats, int C, long nvox) {
@@ -603,8 +604,17 @@ __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, i
     const long v = v0 + vl + i * NV;
     xs[i] = 0.f;
     if (v >= nvox) continue;
-    float x = acc[v * C + c];  // the split slabs in split order: a fixed summation order
-    for (int sp = 1; sp < splits; ++sp) x += acc[((long)sp * nvox + v) * C + c];
+    // the split slabs in split order (a fixed summation order); all of a voxel's slab loads
+    // are issued before the first add (a load -> add chain per slab was latency-bound)
+    float part[kMaxSplitSlabs];
+#pragma unroll
+    for (int sp = 0; sp < kMaxSplitSlabs; ++sp)
+      if (sp < splits) part[sp] = acc[((long)sp * nvox + v) * C + c];
+    float x = part[0];
+#pragma unroll
+    for (int sp = 1; sp < kMaxSplitSlabs; ++sp)
+      if (sp < splits) x += part[sp];
+    for (int sp = kMaxSplitSlabs; sp < splits; ++sp) x += acc[((long)sp * nvox + v) * C + c];
     x += bc;
     T* dst = c < cy0 ? y0 + v * cy0 + c : y1 + v * (C - cy0) + (c - cy0);
     Elem<T>::st(dst, x);
