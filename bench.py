@@ -4,11 +4,13 @@ BCEDiceLoss, Adam) on MI355X — SURVEY.md §8(d), BASELINE.json config 2 (N=1) 
 
 One "step" = Trainer.step on a synthetic batch held in pinned host memory: the H2D copy
 (issued one batch ahead on the trainer's copy stream, SURVEY §8d's unit of work) + forward +
-loss + backward + (all-reduce) + Adam.  Each step is bracketed by a device synchronize (and a
-barrier across ranks); the step time is the max over ranks and ``value`` uses the MEDIAN of
-the K timed steps.  Prints ONE JSON line (rank 0) with the roofline of the stem conv
-(forward + weight-gradient kernels, HBM-bound, 578.9 MB algorithmic at N=2) measured with
-HIP events, the fp32 parity build's rate, and the CPU oracle timed on the host cores
+loss + backward + (all-reduce) + Adam.  The K timed steps run back to back between a barrier +
+device synchronize on both sides; per-step times are HIP events recorded on the compute
+stream at every step boundary, max over ranks, and ``value`` uses their MEDIAN (the wall time
+of the K steps is reported beside it).  Prints ONE JSON line (rank 0) with the roofline of the stem conv
+(forward + weight-gradient kernels, HBM-bound, 578.9 MB algorithmic at N=2), their launch
+durations measured with HIP events on the launch stream inside the timed steps, the fp32
+parity build's rate, and the CPU oracle timed on the host cores
 (rank 0, N=1 only: 1 warm-up + 3 timed steps at the config batch, median).
 """
 from __future__ import annotations
@@ -48,9 +50,12 @@ def parse():
     return ap.parse_args()
 
 
-def stem_roofline(tr, N, spatial, reps):
-    """Time the stem conv (5->64, k3) forward and weight-gradient launches with HIP events
-    on the launch stream, rotating 3 buffer sets (> 256 MiB Infinity Cache)."""
+def stem_roofline(tr, N, spatial, reps, in_step=None):
+    """Roofline of the stem conv (5->64, k3) forward + weight-gradient kernels.  ``in_step``:
+    their average launch durations (s) measured with HIP events on the launch stream inside
+    the timed training steps (the engine's ``kernel_timer``) -- what is reported.  Without
+    them (a shape or build the stem kernels do not run), separate back-to-back launches on
+    rotating buffer sets are timed instead."""
     from pcms_amd import _lib as L
     eng = tr.model.engine()
     code = eng.code
@@ -59,7 +64,7 @@ def stem_roofline(tr, N, spatial, reps):
     cs = eng.convs[0]
     T = eng.tdtype
     sets = []
-    for i in range(3):
+    for i in range(0 if in_step and len(in_step) == 2 else 3):
         xin = torch.rand(nvox * eng.cp, device="cuda").to(T)
         y = torch.empty(nvox * 64, dtype=T, device="cuda")
         dy = torch.randn(nvox * 64, device="cuda").to(T)
@@ -87,8 +92,10 @@ def stem_roofline(tr, N, spatial, reps):
         else:
             L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
 
-    res = {}
+    res = dict(in_step) if in_step else {}
     for name, fn in (("fwd", fwd), ("wgrad", wgrad)):
+        if name in res:
+            continue
         for i in range(reps):  # warm-up: one untimed batch of launches
             fn(sets[i % 3])
         torch.cuda.synchronize()
@@ -124,7 +131,9 @@ def stem_roofline(tr, N, spatial, reps):
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
             "kernel": "stem conv3d 5->64 fwd + wgrad (stem_fwd_direct_kernel + stem_wgrad_stream_kernel)",
             "algorithmic_bytes": fwd_bytes + wg_bytes, "t_fwd_us": round(res["fwd"] * 1e6, 1),
-            "t_wgrad_us": round(res["wgrad"] * 1e6, 1)}
+            "t_wgrad_us": round(res["wgrad"] * 1e6, 1),
+            "timing": "HIP events around each launch inside the timed steps" if in_step else
+                      f"{reps} back-to-back launches, median of 3"}
 
 
 def cpu_baseline(n, spatial):
@@ -159,7 +168,11 @@ def _pinned_batches(n, spatial, rank, count, zero_fill):
 
 
 def timed_steps(tr, host_batches, warmup, steps, world):
-    """Per-step wall times (s), each bracketed by a synchronize (+ barrier), max over ranks."""
+    """K steps back to back, bracketed by a barrier + device synchronize on both sides (the
+    host enqueues ahead of the GPU, as a training loop without per-step host syncs does).
+    Per-step times come from HIP events recorded on the compute stream at every step
+    boundary; returns (per-step seconds, max over ranks), the wall time of the K steps, and
+    the last loss."""
     def loader():
         while True:
             yield from host_batches
@@ -167,21 +180,29 @@ def timed_steps(tr, host_batches, warmup, steps, world):
     for _ in range(warmup):
         tr.step_async(next(it))
     torch.cuda.synchronize()
-    ts, last = [], None
-    for _ in range(steps):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+    timer = tr.model.engine().kernel_timer
+    if timer is not None:
+        timer.clear()  # only the timed steps' launches count
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record()
+    last = None
+    for i in range(steps):
         last = tr.step_async(next(it))
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        ts.append(time.perf_counter() - t0)
-    tt = torch.tensor(ts, device="cuda", dtype=torch.float64)
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    ts = [evs[i].elapsed_time(evs[i + 1]) * 1e-3 for i in range(steps)]
+    tt = torch.tensor(ts + [wall], device="cuda", dtype=torch.float64)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    return tt.cpu().tolist(), last
+    tt = tt.cpu().tolist()
+    return tt[:-1], tt[-1], last
 
 
 def main():
@@ -201,12 +222,21 @@ def main():
            "loss": "bce_dice", "precision": a.precision, "checkpoint_decoder": a.ckpt_decoder}
     tr = Trainer(cfg)
     host = _pinned_batches(a.batch, spatial, rank, 2, a.zero_fill)
-    ts, last = timed_steps(tr, host, a.warmup, a.steps, world)
+    tr.model.engine().kernel_timer = {}
+    ts, wall, last = timed_steps(tr, host, a.warmup, a.steps, world)
+    timer = tr.model.engine().kernel_timer
+    tr.model.engine().kernel_timer = None
+    in_step = {}
+    for key, name in (("fwd", "stem_fwd"), ("wgrad", "stem_wgrad")):
+        evs = timer.get(name, [])
+        if evs:
+            in_step[key] = statistics.mean(e0.elapsed_time(e1) for e0, e1 in evs) * 1e-3
     loss = float(last) if last is not None else float("nan")
     med = statistics.median(ts)
     vols_step = world * a.batch
     value = vols_step / med
-    roof = stem_roofline(tr, a.batch, spatial, a.kernel_reps) if rank == 0 else None
+    roof = stem_roofline(tr, a.batch, spatial, a.kernel_reps, in_step if len(in_step) == 2 else None) \
+        if rank == 0 else None
     # the fp32 parity build (the one that meets the 1e-3 logit bar) on the same batches
     fp32 = None
     if a.fp32_steps > 0 and a.precision != "fp32":
@@ -214,7 +244,7 @@ def main():
         torch.cuda.empty_cache()
         torch.manual_seed(0)
         tr32 = Trainer(dict(cfg, precision="fp32"))
-        ts32, _ = timed_steps(tr32, host, 2, a.fp32_steps, world)
+        ts32, _, _ = timed_steps(tr32, host, 2, a.fp32_steps, world)
         fp32 = round(vols_step / statistics.median(ts32), 3)
         del tr32
     cpu = None
@@ -237,7 +267,10 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "mfma_util_step": round(flops / med / MFMA_BF16_PEAK, 4), "final_loss": round(loss, 5),
             "step_ms": {"median": round(med * 1e3, 3), "mean": round(statistics.mean(ts) * 1e3, 3),
-                        "min": round(min(ts) * 1e3, 3), "max": round(max(ts) * 1e3, 3)},
+                        "min": round(min(ts) * 1e3, 3), "max": round(max(ts) * 1e3, 3),
+                        "wall_per_step": round(wall / a.steps * 1e3, 3),
+                        "timing": "HIP events on the compute stream at every step boundary, K steps "
+                                  "back to back between a barrier + synchronize on both sides"},
             "fp32_parity_build_value": fp32,
         }
         print(json.dumps(out), flush=True)

@@ -121,6 +121,7 @@ class UNetEngine:
         self.act_ckpt = False
         self.wgrad_target = 256  # conv weight-gradient workgroups: one round of 1 WG per CU (fewer partial rows to reduce than 512)
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
+        self.kernel_timer = None  # dict name -> [(start, end) events] (bench.py roofline timing)
         self.wgrad_side_stream = False  # ablation: weight gradients on a side stream (measured 119.9 vs 121.6 vol/s: off)
         self._side_stream = None
         self._side_used = False
@@ -165,6 +166,20 @@ class UNetEngine:
         self._dirty = True
         self._adam_plan = None
         self.grad_ranges = module_grad_ranges(self.model)
+
+    @contextlib.contextmanager
+    def _timed(self, name: str):
+        """HIP events around one library call on the current stream when ``kernel_timer`` (a
+        dict name -> list) is set: bench.py times the stem kernels inside its timed steps."""
+        t = self.kernel_timer
+        if t is None:
+            yield
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        yield
+        e1.record()
+        t.setdefault(name, []).append((e0, e1))
 
     def _grads_done(self, module: str):
         """A module's backward is complete: join the weight-gradient stream (its dW kernels and
@@ -424,7 +439,8 @@ class UNetEngine:
         splits = self._splits(N, S, c0 + c1, cs.cout)
         st = b["stats"] if training and not recompute else None
         if cs is self.convs[0] and self.stem_sup & 1:
-            call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2])
+            with self._timed("stem_fwd"):
+                call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2])
             rows = query("pcms_stem_fwd_rows", N, *S)
         elif splits == 1:
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
@@ -534,7 +550,8 @@ class UNetEngine:
         self._bn_bwd(blk.b0, gA, acts["y1"], gZ, nvox)
         with self._side():
             if blk is self.enc[0] and self.stem_sup & 2:
-                call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
+                with self._timed("stem_wgrad"):
+                    call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
             else:
                 call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gZ, blk.c0.mod.weight.grad, b["dwt"], N,
                      *S, blk.c0.cout, blk.c0.cin, self.wgrad_target)
