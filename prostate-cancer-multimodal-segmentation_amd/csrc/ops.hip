@@ -144,16 +144,33 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_reduce_kernel(
     sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j];
     sg[j] = 0.f; sgx[j] = 0.f;
   }
-  for (long v = (long)blockIdx.x * VL + vl; v < nvox; v += (long)gridDim.x * VL) {
-    float dv[VEC], yv[VEC];
-    load16<T>(da + v * C + c0, dv);
-    load16<T>(y + v * C + c0, yv);
+  // four voxel rows' loads in flight per trip, accumulated in the same voxel order as one
+  // at a time (identical sums)
+  const long stride = (long)gridDim.x * VL;
+  long v = (long)blockIdx.x * VL + vl;
+  auto acc1 = [&](const float (&dv)[VEC], const float (&yv)[VEC]) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float g = (yv[j] * sc[j] + sh[j] > 0.f) ? dv[j] : 0.f;
       sg[j] += g;
       sgx[j] += g * ((yv[j] - mu[j]) * is[j]);
     }
+  };
+  for (; v + 3 * stride < nvox; v += 4 * stride) {
+    float dv[4][VEC], yv[4][VEC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      load16<T>(da + (v + u * stride) * C + c0, dv[u]);
+      load16<T>(y + (v + u * stride) * C + c0, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc1(dv[u], yv[u]);
+  }
+  for (; v < nvox; v += stride) {
+    float dv[VEC], yv[VEC];
+    load16<T>(da + v * C + c0, dv);
+    load16<T>(y + v * C + c0, yv);
+    acc1(dv, yv);
   }
 #pragma unroll
   for (int j = 0; j < VEC; ++j) {

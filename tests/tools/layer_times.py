@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--size", default="128,128,64")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--wgrad-target", type=int, default=0, help="engine.wgrad_target override")
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
     from pcms_amd import engine as E
@@ -57,6 +58,8 @@ def main():
     torch.manual_seed(0)
     tr = Trainer({"device": "cuda", "learning_rate": 1e-4, "batch_size": a.batch, "num_epochs": 1,
                   "loss": "bce_dice", "precision": "bf16"})
+    if a.wgrad_target:
+        tr.model.engine().wgrad_target = a.wgrad_target
     b = make_batch(a.batch, spatial, seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
     for _ in range(3):
