@@ -131,6 +131,22 @@ __device__ __forceinline__ float adam_update(float& p, float& g, float& m, float
   return p;
 }
 
+// sum of n <= 16 values src[0], src[step], ... in that order, all loads issued before the
+// first add (a load -> add chain per row was latency-bound); longer: 16 at a time
+__device__ __forceinline__ float sum_rows16(const float* src, long step, int n) {
+  float sum = 0.f;
+  for (int base = 0; base < n; base += 16) {
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (base + r < n) v[r] = src[(long)(base + r) * step];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (base + r < n) sum += v[r];
+  }
+  return sum;
+}
+
 #define PCMS_CHECK_LAUNCH() return (int)hipGetLastError()
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

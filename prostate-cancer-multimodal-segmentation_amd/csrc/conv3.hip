@@ -753,10 +753,7 @@ __global__ void __launch_bounds__(256) wgrad_group_sum_kernel(float* part, int S
   const long e = blockIdx.x * 256L + threadIdx.x;
   if (e >= E) return;
   const int r0 = blockIdx.y * 16, r1 = min(S, r0 + 16);
-  float* src = part + (long)r0 * E + e;
-  float sum = 0.f;
-  for (int r = r0; r < r1; ++r, src += E) sum += *src;
-  part[(long)r0 * E + e] = sum;
+  part[(long)r0 * E + e] = sum_rows16(part + (long)r0 * E + e, E, r1 - r0);
 }
 // Stage 2: dw [Cout][Cw][27] (torch OIDHW, the weight's own input-channel count Cw <= Cin;
 // stem: 5 of 8) += sum of R rows spaced `stride` rows apart.  Block = (co, 32 channels): the
@@ -771,8 +768,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, in
     const int t = e >> 5, c = e & 31, ci = ci0 + c;
     float sum = 0.f;
     if (ci < Cw) {
-      const float* src = part + ((long)t * Cout + co) * Cin + ci;
-      for (int r = 0; r < R; ++r, src += rstep) sum += *src;
+      sum = sum_rows16(part + ((long)t * Cout + co) * Cin + ci, rstep, R);
     }
     tile[t][c] = sum;
   }

@@ -382,10 +382,7 @@ __global__ void __launch_bounds__(256) convt_group_sum(float* ws, int S, long E)
   const long e = blockIdx.x * 256L + threadIdx.x;
   if (e >= E) return;
   const int r0 = blockIdx.y * 16, r1 = min(S, r0 + 16);
-  float* src = ws + (long)r0 * E + e;
-  float sum = 0.f;
-  for (int r = r0; r < r1; ++r, src += E) sum += *src;
-  ws[(long)r0 * E + e] = sum;
+  ws[(long)r0 * E + e] = sum_rows16(ws + (long)r0 * E + e, E, r1 - r0);
 }
 // Stage 2: dw [Cin][Cout][8] (torch ConvTranspose3d layout, +=) = sum of R rows of
 // [Cin][8][Cout] spaced `stride` rows apart.  Block = (ci, 32 co): [8][32] tiles read as
@@ -396,10 +393,7 @@ __global__ void __launch_bounds__(256) convt_wgrad_reduce(const float* ws, int R
   const int ci = blockIdx.x, co0 = blockIdx.y * 32;
   const long rstep = (long)stride * 8 * Cin * Cout;
   const int e = threadIdx.x, t = e >> 5, c = e & 31;
-  const float* src = ws + ((long)ci * 8 + t) * Cout + co0 + c;
-  float sum = 0.f;
-  for (int r = 0; r < R; ++r, src += rstep) sum += *src;
-  tile[t][c] = sum;
+  tile[t][c] = sum_rows16(ws + ((long)ci * 8 + t) * Cout + co0 + c, rstep, R);
   __syncthreads();
   dw[((long)ci * Cout + co0) * 8 + e] += tile[e & 7][e >> 3];
 }

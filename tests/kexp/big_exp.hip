@@ -230,7 +230,9 @@ __global__ void __launch_bounds__(kBgThreads, 1) big_exp_kernel(Conv3Params p, u
         const int mt = 2 * pass + (row >> 5), pr = perm32(row & 31);
         const int rd = 2 * wave + (mt >> 2), rh = 2 * (mt & 3) + (pr >> 4), rw = pr & 15;
         const long vox = vbase + (long)rd * plane + (long)rh * p.W + rw;
-        if constexpr (!(F & 4)) __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0, 0);
+        if constexpr (!(F & 4))
+          __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0,
+                                                 (F & 256) ? 16 : (F & 512) ? 2 : 0);
         else if (v[0] == 0x12345678u && v[1] == 0x9abcdef0u) __builtin_amdgcn_raw_buffer_store_b128(v, yr, 0, 0, 0);
       }
       asm volatile("" ::: "memory");
@@ -318,6 +320,8 @@ extern "C" int exp_big(int F, const void* x0, int c0, const void* x1, int c1, co
     case 36: launch(big_exp_kernel<36>); break;
     case 64: launch(big_exp_kernel<64>); break;
     case 128: launch(big_exp_kernel<128>); break;
+    case 256: launch(big_exp_kernel<256>); break;
+    case 512: launch(big_exp_kernel<512>); break;
     case 132: launch(big_exp_kernel<132>); break;
     case 68: launch(big_exp_kernel<68>); break;
     default: return -1;

@@ -13,7 +13,8 @@ NAMES = {0: "product", 1: "no halo HBM", 2: "B one line", 3: "no halo + B one li
          7: "no halo/B/stores", 8: "no A reads", 15: "no halo/B/stores/A", 16: "no MFMA",
          23: "no halo/B/stores/MFMA", 32: "halo from 1 MiB (L2 hits)", 36: "halo L2 hits, no stores",
          64: "odd slots start half a box late", 68: "desync + no stores",
-         128: "contiguous 1 KiB halo runs", 132: "contiguous halo, no stores"}
+         128: "contiguous 1 KiB halo runs", 132: "contiguous halo, no stores",
+         256: "output stores sc1 (drop from L2)", 512: "output stores nt"}
 
 
 def main():
