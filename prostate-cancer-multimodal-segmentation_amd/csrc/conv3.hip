@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   constexpr int BUFBYTES = DYBYTES + XBYTES;
   extern __shared__ __attribute__((aligned(16))) char wlds[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hsel = lane >> 5;
   const int cot = wave & 1;           // co tile (32 rows of the 64-wide dy tile)
   const int tg = wave >> 1;           // taps tg, tg+4, ...
@@ -574,6 +574,71 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     }
   };
 
+  // bf16 with a compile-time box (w = 8 or 16): the k loop fully unrolled.  Every fragment
+  // address is a per-lane base (per box buffer) + an immediate: the dy half swap depends on the
+  // lane's voxel inside a 16-voxel step only, a step starts a w-row, and the lane's voxels
+  // (vl, vl + 4) lie in one w-row (vl % 8 < 4), so its halo rows are a lane constant plus the
+  // step's compile-time row.  The
+  // fragments of step s + 1 are read while step s's MFMAs run (two register sets), so the
+  // LDS latency is behind the MFMAs instead of in front of each pair.  Taps wave + 8 j, j < 3
+  // for every wave; the fourth (waves 0-2: taps 24-26) in a uniform branch at the step's end,
+  // its fragment also one step ahead (one code path: no per-variant register allocation).
+  auto compute_fixed = [&](const char* buf) __attribute__((always_inline)) {
+    constexpr int LD = LBW >= 3 ? LBD : 0, LH = LBW >= 3 ? LBH : 0, LW = LBW >= 3 ? LBW : 4;
+    constexpr int HHc = (1 << LH) + 2, HWc = (1 << LW) + 2;
+    constexpr int NK = (1 << (LD + LH + LW)) / 16;
+    const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int vl = 8 * hsel + qq;  // the lane's first voxel inside a step
+    const int vrow = (vl >> LW) * HWc + (vl & ((1 << LW) - 1));  // its halo row offset
+    const char* ab0 = buf + dy_off_bf16(vl, g * 16 + pp * 4);
+    const char* ab1 = buf + dy_off_bf16(vl, 32 + g * 16 + pp * 4);
+    const bool four = wave < 3;
+    const char* bb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tap = wave + 8 * j;
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      bb[j] = buf + DYBYTES + (vrow + (kd * HHc + kh) * HWc + kw) * Tr::XROW + (g * 16 + pp * 4) * 2;
+    }
+    auto cat = [](s16x4_t lo, s16x4_t hi) __attribute__((always_inline)) {
+      return (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    auto hro = [](int s) __attribute__((always_inline)) {  // the step's first halo row (w = 0)
+      const int v0 = 16 * s, rd = v0 >> (LH + LW), rh = (v0 >> LW) & ((1 << LH) - 1);
+      return (rd * HHc + rh) * HWc * Tr::XROW;
+    };
+    s16x8_t fa[2][2], fb[2][3], f3[2];
+    auto load = [&](int s, int set) __attribute__((always_inline)) {
+      fa[set][0] = cat(tr_read(ab0, s * 2048), tr_read(ab0, s * 2048 + 512));
+      fa[set][1] = cat(tr_read(ab1, s * 2048), tr_read(ab1, s * 2048 + 512));
+#pragma unroll
+      for (int j = 0; j < 3; ++j) fb[set][j] = cat(tr_read(bb[j], hro(s)), tr_read(bb[j], hro(s) + 4 * Tr::XROW));
+    };
+    auto load3 = [&](int s, int set) __attribute__((always_inline)) {
+      f3[set] = cat(tr_read(bb[3], hro(s)), tr_read(bb[3], hro(s) + 4 * Tr::XROW));
+    };
+    load(0, 0);
+    if (four) load3(0, 0);
+    static_for<NK>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value, cs = s & 1, ns = cs ^ 1;
+      if constexpr (s + 1 < NK) load(s + 1, ns);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        acc[j] = mfma(fa[cs][0], fb[cs][j], acc[j]);
+        acc[4 + j] = mfma(fa[cs][1], fb[cs][j], acc[4 + j]);
+      }
+      if (four) {
+        if constexpr (s + 1 < NK) load3(s + 1, ns);
+        acc[3] = mfma(fa[cs][0], f3[cs], acc[3]);
+        acc[7] = mfma(fa[cs][1], f3[cs], acc[7]);
+      }
+    });
+  };
+  auto compute_box = [&](const char* buf) __attribute__((always_inline)) {
+    if constexpr (kW2 && LBW >= 3) compute_fixed(buf);
+    else compute(buf);
+  };
+
   // bf16 hot path: both tiles arrive by buffer LDS-DMA (no register staging); the next box
   // streams in while this one computes.  The dy tile keeps dy_off_bf16's half swap (applied
   // to the source address); each wave instruction is all-dy or all-halo (2048 dy pieces);
@@ -622,7 +687,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
         if (b + 1 < b_end) stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
-        compute(wlds + cur * BUFBYTES);
+        compute_box(wlds + cur * BUFBYTES);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
@@ -635,7 +700,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
         if (b + 1 < b_end) stage_load(b + 1);
-        compute(wlds + cur * BUFBYTES);
+        compute_box(wlds + cur * BUFBYTES);
         if (b + 1 < b_end) stage_store(wlds + (cur ^ 1) * BUFBYTES);
         __syncthreads();
       }
@@ -997,13 +1062,6 @@ template <int Imm> __device__ __forceinline__ void bload16(s16x8_t& dst, i32x4_t
 template <int N> __device__ __forceinline__ void vm_wait2(s16x8_t& a, s16x8_t& b) {
   static_assert(N >= 0 && N <= 63, "vmcnt");
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
-}
-template <class F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F> __device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 // vector-memory ops issued after B(t)'s second load by the time tap t waits for it: every
 // tap s issues B(s + D) x 2 then piece(s) (s < 15, chunk-relative, every chunk alike)
@@ -1504,6 +1562,7 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
     auto kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1>;
     if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
     else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
+    else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
   } else {

@@ -2,6 +2,7 @@
 #pragma once
 #include "common.h"
 #include <algorithm>
+#include <utility>
 
 namespace {
 
@@ -86,6 +87,15 @@ __device__ __forceinline__ int dy_off_bf16(int v, int co) {  // co in 0..63 (ele
 
 __device__ __forceinline__ s16x4_t tr_read(const char* lds, int byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + byte_off));
+}
+
+// compile-time loop: f(integral_constant<int, i>) for i < N
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F> __device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 struct Box { int lbd, lbh, lbw; };
