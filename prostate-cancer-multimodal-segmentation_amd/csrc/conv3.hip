@@ -119,6 +119,47 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     };
     load_b(bset[0], 0);
     load_b(bset[1], 1);
+    if constexpr (!kF32) {
+      // bf16: the A fragments roll through one register set: right after M-tile mt's MFMAs of
+      // tap t its fragment of tap t + 1 is read (15 MFMAs of slack before its first use)
+      // instead of one read -> wait -> two MFMAs per fragment
+      s16x8_t a[2][4];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) a[ks][mt] = lds_a(lds, hb[mt], ks, hsel, (T*)nullptr);
+      for (int kdh = 0; kdh < 9; ++kdh) {
+        // row bases from an opaque copy: the fragment addresses are recomputed per kdh rather
+        // than hoisted out of the loops (and spilled)
+        int hbk[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int tap = kdh * 3 + kw;
+          // (past the last tap: harmless re-reads, so every kdh iteration is alike)
+          load_b(bset[(kw + 2) % 3], min(tap + 2, 26));
+          __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
+          const int tn = tap + 1 < 27 ? tap + 1 : 0;
+          const int offn = ((tn / 9) * HH + (tn / 3) % 3) * HW + tn % 3;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+              for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[ks][mt], bset[kw][nt][ks], acc[mt][nt]);
+              a[ks][mt] = lds_a(lds, hbk[mt] + offn, ks, hsel, (T*)nullptr);
+            }
+          // (the scheduler would otherwise sink all eight reads below the last MFMA)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+          }
+        }
+      }
+      continue;
+    }
     for (int kdh = 0; kdh < 9; ++kdh) {
       const int kd = kdh / 3, kh = kdh % 3;
 #pragma unroll
@@ -1072,14 +1113,6 @@ template <int P, int Dist> constexpr int bg_wait(int t) {
   return n;
 }
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-// an opaque copy: values derived from it are recomputed where used instead of being hoisted
-// out of the box loop (and spilled: a spill reload is a vector-memory load whose wait would
-// also drain the hidden B loads and halo DMA in flight)
-__device__ __forceinline__ int opaque(int v) {
-  int r;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
-  return r;
-}
 
 __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Params p, uint32_t x0bytes,
                                                                      uint32_t x1bytes) {

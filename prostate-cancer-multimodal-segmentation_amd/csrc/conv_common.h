@@ -89,6 +89,15 @@ __device__ __forceinline__ s16x4_t tr_read(const char* lds, int byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(lds + byte_off));
 }
 
+// an opaque copy: values derived from it are recomputed where used instead of being hoisted
+// out of a loop (and spilled: a spill reload is a vector-memory load whose wait would
+// also drain the hidden B loads and halo DMA in flight)
+__device__ __forceinline__ int opaque(int v) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
 // compile-time loop: f(integral_constant<int, i>) for i < N
 template <class F, int... I>
 __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
