@@ -21,6 +21,6 @@ rc=$?; echo "smoke_rc=$rc"; tail -1 gpurun_out/smoke_$TAG.log; stop_if_bad smoke
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench_rc=$rc"; tail -1 gpurun_out/bench_$TAG.log; stop_if_bad bench $rc
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run \
-  --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline \
+  --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --fp32-steps 0 \
   > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "prof_rc=$rc"; tail -1 gpurun_out/prof_$TAG.log
