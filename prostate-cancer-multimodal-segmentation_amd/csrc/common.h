@@ -100,8 +100,11 @@ __device__ __forceinline__ i32x4_t buffer_desc(const void* base, uint32_t num_by
 // asm so the compiler's waitcnt pass does not see it: it would otherwise wait vmcnt(0)
 // before the next LDS read of ANY buffer (killing a multi-stage ring).  The caller retires
 // these with explicit s_waitcnt vmcnt(N) + a barrier before reading the data.
+// Wait states inside the string (the compiler pads nothing in it): s_nop 4 first, for an
+// soffset / descriptor SGPR fresh from v_readfirstlane (VALU SGPR write -> VMEM read), and
+// one state between the M0 write and the LDS-DMA that reads it.
 __device__ __forceinline__ void dma16(i32x4_t rsrc, uint32_t lds_base, uint32_t voff, uint32_t soff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                :
                : "s"(lds_base), "v"(voff), "s"(rsrc), "s"(soff)
                : "memory", "m0");

@@ -13,6 +13,12 @@ namespace {
 // ------------------------------------------------------------------------------------
 constexpr int kStemSteps = 14;                    // 28 taps (27 + 1 zero) / 2
 
+// timeline instrumentation hook for tests/kexp (empty in the product library)
+#ifndef STEM_STAMP
+#define STEM_STAMP(k)
+#define STEM_STAMP_END()
+#endif
+
 // master W[64][cin_w][27] fp32 -> [14][64][16] bf16, k = h * 8 + c <-> (tap 2s + h, c);
 // the 64 output columns are ordered (nt, j) -> channel 2 j + nt so that a lane's two MFMA
 // tiles hold an adjacent channel pair (one packed bf16x2 LDS write per row)
@@ -41,7 +47,8 @@ __device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
 //    (128 contiguous bytes) with ONE buffer_store_dword (per-lane voffset, wave-uniform
 //    soffset, immediate offset: no VALU address math, no LDS round trip).
 //  * Halo: double-buffered, buffer LDS-DMA (out-of-range voffset = zero padding), the next
-//    box's halo in flight while this one computes; one barrier per box.
+//    box's halo in flight while this one computes; one raw barrier per box (the stores of
+//    a box stay in flight across it: vmcnt counts loads, stores and DMA in issue order).
 //  * Weights: in LDS (28 KiB, k-halves swapped on column bit 4: conflict-free reads).
 //  * Staggered epilogue: waves 0-3 do each box's epilogue (BN sums, bf16 packing, stores)
 //    right after its MFMAs; waves 4-7 defer theirs to the start of the NEXT box, so on every
@@ -49,7 +56,12 @@ __device__ __forceinline__ int tap_off(int tap, int HH, int HW) {
 //    two waves doing the same phase at once (MFMA and VALU pipes are separate).
 //  * BatchNorm partials: shifted sums over all boxes of the workgroup, ONE stats row per
 //    workgroup (rows >= gridDim.x are zeroed: count 0).
-constexpr int kSDHaloRows = kHaloMax;                         // 1152 rows (18 x 64)
+// halo rows in LDS are padded from 18 to kSDHW = 24 voxels (384 B = 128 B mod 256): the two
+// H-rows a 16-lane ds_read_b128 group reads land on disjoint halves of the 256-B bank row
+constexpr int kSDHW = 24;
+// 1440 halo rows ((bd+2)(bh+2) = 60), rounded up to whole 64-row DMA pieces: a wave's last
+// piece writes all 64 of its rows (the ones past the halo get zeros)
+constexpr int kSDHaloRows = (6 * 10 * kSDHW + 63) / 64 * 64;
 constexpr int kSDHaloBytes = kSDHaloRows * 16;
 constexpr int kSDW = 2 * kSDHaloBytes;                        // weights [14][64][32 B]
 constexpr int kSDRed = kSDW + kStemSteps * 64 * 32;
@@ -62,29 +74,29 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   constexpr int NWV = kSDThr / 64;
   static_assert((1 << (LBD + LBH + 4)) == NWV * 64, "box = 64 voxels per wave");
   constexpr int bd = 1 << LBD, bh = 1 << LBH, bw = 16;
-  constexpr int HH = bh + 2, HW = bw + 2, HV = (bd + 2) * HH * HW;
+  constexpr int HH = bh + 2, HW = kSDHW, HV = (bd + 2) * HH * HW;  // columns >= bw + 2: zero pad
   constexpr int NP = (HV + kSDThr - 1) / kSDThr;  // halo pieces per thread
-  static_assert(HV <= kSDHaloRows, "halo fits");
+  static_assert((HV + 63) / 64 * 64 <= kSDHaloRows, "halo (whole DMA pieces) fits");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* red = reinterpret_cast<float*>(lds + kSDRed);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR math)
-  const bool late = wave >= 4;                                  // deferred-epilogue half
   const int r_lane = lane & 31, hsel = lane >> 5;
   const int D = p.D, H = p.H, W = p.W;
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x0, 0, xbytes, 0x00020000);
+  const i32x4_t xr = buffer_desc(p.x0, xbytes);
   const auto yr = __builtin_amdgcn_make_buffer_rsrc(p.y0, 0, ybytes, 0x00020000);
 
   // weights -> LDS once (read after the first barrier): row (step, column) of 32 B, its two
-  // 16-B k-halves swapped when column bit 4 is set
+  // 16-B k-halves swapped when column bit 3 is set (a 16-lane group then reads 16 distinct
+  // 16-B slots of the bank row)
   {
     const u32x4_t* wg = reinterpret_cast<const u32x4_t*>(p.w);
     for (int i = tid; i < kStemSteps * 64 * 2; i += kSDThr) {
       const int row = i >> 1, half = i & 1, col = row & 63;
-      *reinterpret_cast<u32x4_t*>(lds + kSDW + row * 32 + ((half ^ ((col >> 4) & 1)) * 16)) = wg[i];
+      *reinterpret_cast<u32x4_t*>(lds + kSDW + row * 32 + ((half ^ ((col >> 3) & 1)) * 16)) = wg[i];
     }
   }
-  const char* wl = lds + kSDW + r_lane * 32 + ((hsel ^ ((r_lane >> 4) & 1)) * 16);
+  const char* wl = lds + kSDW + r_lane * 32 + ((hsel ^ ((r_lane >> 3) & 1)) * 16);
   float bias_l[2] = {0.f, 0.f};
   if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
   // halo rows of the two 32-row MFMA tiles (perm32 layout)
@@ -102,7 +114,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
     const int hv = tid + i * kSDThr;
     const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
     prel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
-    pco[i] = hv < HV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
+    pco[i] = (hv < HV && hw_ < bw + 2) ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
   }
   // store voffsets: rows x = perm32((e & 3) + 8 g + 4 hsel) have x & 15 = 4 g + (e & 3) and
   // x >> 4 = (g in {1, 2}) ^ hsel
@@ -135,65 +147,96 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
         if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (LDS_AS void*)(lds + buf * kSDHaloBytes + (wave * 64 + i * kSDThr) * 16),
-                                               16, voff, 0, 0, 0);
+      dma16(xr, __builtin_amdgcn_readfirstlane(lds_addr(lds) + buf * kSDHaloBytes + (wave * 64 + i * kSDThr) * 16), voff, 0);
     }
   };
 
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, K[2] = {0.f, 0.f};
   float cnt = 0.f;
-  bool first = true;
-  // epilogue of one box: packed channel-pair stores + shifted BN sums
-  auto epilogue = [&](f32x16_t (&acc)[2][2], int bb) {
+  auto is_full = [&](int bb) {
     int n, d0, h0, w0;
     origin(bb, n, d0, h0, w0);
-    const bool full = d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
-    if (first) {
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(acc[0][nt][0], r_lane, 64);
-      first = false;
-    }
+    return d0 + bd <= D && h0 + bh <= H && w0 + bw <= W;
+  };
+  // store offsets (wave-uniform) of the two 32-voxel tiles of box bb
+  auto tile_so = [&](int bb, uint32_t (&so)[2]) {
+    int n, d0, h0, w0;
+    origin(bb, n, d0, h0, w0);
     const int bv = ((n * D + d0) * H + h0) * W + w0;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      const int R0 = wave * 4 + mt * 2;          // even (rd, rh) linear index of the tile
+      const int R0 = wave * 4 + mt * 2;  // even (rd, rh) linear index of the tile
+      so[mt] = __builtin_amdgcn_readfirstlane((uint32_t)(bv + ((R0 >> LBH) * H + (R0 & (bh - 1))) * W) * 128u);
+    }
+  };
+  // item (mt, e) of a full box's epilogue: one packed channel-pair store (the 32 lanes of a
+  // half-wave write one voxel's 128 B) + the shifted BN sums
+  auto item_full = [&](f32x16_t (&acc)[2][2], int mt, int e, const uint32_t (&so)[2]) {
+    const int g = e >> 2, rw = 4 * g + (e & 3);
+    const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
+    __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 0);
+    const float e0 = v0 - K[0], e1 = v1 - K[1];
+    s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
+    s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
+  };
+  // whole epilogue of one box (boundary boxes, and the last box of the workgroup)
+  auto epilogue = [&](f32x16_t (&acc)[2][2], int bb) {
+    int n, d0, h0, w0;
+    origin(bb, n, d0, h0, w0);
+    uint32_t so[2];
+    tile_so(bb, so);
+    if (is_full(bb)) {
+#pragma unroll
+      for (int q = 0; q < 32; ++q) item_full(acc, q >> 4, q & 15, so);
+      cnt += 32.f;
+      return;
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int R0 = wave * 4 + mt * 2;
       const int rd0 = R0 >> LBH, rh0 = R0 & (bh - 1);
-      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(bv + (rd0 * H + rh0) * W) * 128u);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int g = e >> 2, rw = 4 * g + (e & 3);
         const bool gB = (g == 1 || g == 2);
         const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-        uint32_t voff = gB ? vB : vA;
-        float e0 = v0 - K[0], e1 = v1 - K[1];
-        if (!full) {  // uniform branch: boundary boxes only
-          const int xh = (gB ? 1 : 0) ^ hsel;
-          const bool valid = (d0 + rd0 < D) & (h0 + rh0 + xh < H) & (w0 + rw < W);
-          voff = valid ? voff : kOOB;
-          e0 = valid ? e0 : 0.f;
-          e1 = valid ? e1 : 0.f;
-          cnt += valid ? 1.f : 0.f;
-        }
-        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so + rw * 128, 0);
+        const int xh = (gB ? 1 : 0) ^ hsel;
+        const bool valid = (d0 + rd0 < D) & (h0 + rh0 + xh < H) & (w0 + rw < W);
+        const uint32_t voff = valid ? (gB ? vB : vA) : kOOB;
+        const float e0 = valid ? v0 - K[0] : 0.f, e1 = valid ? v1 - K[1] : 0.f;
+        cnt += valid ? 1.f : 0.f;
+        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so[mt] + rw * 128, 0);
         s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
         s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
       }
     }
-    if (full) cnt += 32.f;
   };
 
+  // Every wave defers a box's epilogue to the next box: its 32 stores and BN sums are spread
+  // over that box's 14 MFMA steps (3 items per step for steps 0-3, 2 after), so each SIMD's
+  // store stream runs under the MFMAs instead of in bursts between them.
   f32x16_t prev[2][2];
-  int pb = -1;  // box whose epilogue a late wave still owes
+  int pb = -1;  // box whose epilogue is still owed
   int b = blockIdx.x;
   if (b < nbox) stage(b, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int it = 0; b < nbox; b += gridDim.x, ++it) {
     // halo(b) has landed for this wave (vmcnt at the loop end); barrier: for all waves, and
-    // every wave is done reading the buffer the next DMA overwrites
-    __syncthreads();
+    // every wave is done reading the buffer the next DMA overwrites.  A raw s_barrier, not
+    // __syncthreads(): its fence would wait vmcnt(0), draining this wave's output stores
+    // every box instead of leaving them in flight under the next box's MFMAs.  (The halo DMA
+    // is inline asm, invisible to the compiler's wait insertion, for the same reason.)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    STEM_STAMP(0);
     const int bn = b + gridDim.x;
     if (bn < nbox) stage(bn, (it + 1) & 1);
-    if (late && pb >= 0) epilogue(prev, pb);
+    STEM_STAMP(1);
+    const bool interleave = pb >= 0 && is_full(pb);
+    if (pb >= 0 && !interleave) epilogue(prev, pb);
+    uint32_t pso[2] = {0u, 0u};
+    if (interleave) tile_so(pb, pso);
+    STEM_STAMP(2);
     const char* hl = lds + (it & 1) * kSDHaloBytes;
     f32x16_t acc[2][2];
 #pragma unroll
@@ -202,7 +245,8 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = bias_l[j];
-    {
+    auto mfma_steps = [&](auto il) {
+      constexpr bool IL = decltype(il)::value;
       int hs16 = hsel * 16;
       asm volatile("" : "+v"(hs16));
       auto load_a = [&](int st, s16x8_t (&a)[2]) {
@@ -229,25 +273,55 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
           acc[mt][0] = mfma(abuf[st & 1][mt], bbuf[st & 1][0], acc[mt][0]);
           acc[mt][1] = mfma(abuf[st & 1][mt], bbuf[st & 1][1], acc[mt][1]);
         }
+        // the next step's four fragment reads go out ahead of this step's MFMAs (left to
+        // itself the scheduler sank them below three of the MFMAs, exposing the LDS
+        // latency); the owed epilogue items go between the MFMAs
+        if (st + 1 < kStemSteps) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        if constexpr (IL) {
+          constexpr int q0[15] = {0, 3, 6, 9, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30, 32};
+          const int qa = q0[st], qb = q0[st + 1];
+#pragma unroll
+          for (int q = qa; q < qb; ++q) item_full(prev, q >> 4, q & 15, pso);
+#pragma unroll
+          for (int q = qa; q < qb; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);  // pack + BN sums
+            __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // 1 store
+          }
+          if (st < 4) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 4 - 3 items
+          else __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         // 4 - 2 items
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
-    }
-    if (late) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) prev[i][j] = acc[i][j];
-      pb = b;
+    };
+    if (interleave) {
+      mfma_steps(std::true_type{});
+      cnt += 32.f;
     } else {
-      epilogue(acc, b);
+      mfma_steps(std::false_type{});
     }
-    // the next halo's DMA was issued before this box's 32 stores (a late wave: before the
-    // previous box's 32 stores, its only stores since; none in its first iteration)
-    if (late && it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STEM_STAMP(3);
+    if (it == 0) {  // BN shift: the first box's first voxel, per channel
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) K[nt] = __shfl(acc[0][nt][0], r_lane, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) prev[i][j] = acc[i][j];
+    pb = b;
+    STEM_STAMP(4);
+    // the next halo's DMA was issued before the 32 stores of the owed epilogue (none in the
+    // first iteration)
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    STEM_STAMP(5);
   }
-  if (late && pb >= 0) epilogue(prev, pb);
+  if (pb >= 0) epilogue(prev, pb);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STEM_STAMP_END();
   if (!p.stats) return;
   // per wave (lanes r_lane and r_lane + 32 share channels and K): S = sum d + n K,
   // M2 = sum d^2 - (sum d)^2 / n; then Chan across the 8 waves
@@ -297,32 +371,33 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
 
 // Streaming stem weight gradient (the HBM-bound hot case: D % 4 == H % 4 == W % 16 == 0).
 // dW[co][c][t] = sum_v dy[v][co] x[v + t][c]: GEMM with M = 64 co, N = 224 (tap, channel)
-// columns, K = voxels.  Persistent: one 4-wave workgroup per CU walks 4x4x16 voxel boxes
+// columns, K = voxels.  Persistent: one 8-wave workgroup per CU walks 4x4x16 voxel boxes
 // b = blockIdx.x + k gridDim.x.  Each box's dy tile (256 voxels x 128 B) and x halo
 // (6x6x18 rows x 16 B) arrive by buffer LDS-DMA (inline asm, see dma16) into a 3-slot ring:
 // two boxes in flight while one computes, counted vmcnt + raw s_barrier, every source
-// offset a per-thread constant + the box base.  Wave w owns k-steps w, w + 4, w + 8, w + 12
-// of every box and ALL 14 output tiles (2 co x 7 column tiles, accumulators in AGPRs), so
-// each A / B fragment is read from LDS exactly once per box (ds_read_b64_tr_b16 transposes
-// both operands) and the next k-step's fragments are read during this one's 14 MFMAs.
+// offset a per-thread constant + the box base; the 43 DMA instructions of a box are spread
+// over the 8 waves (5-6 each).  Wave w = (ks, ct) owns co tile ct = w & 1 and k-steps ks,
+// ks + 4, ks + 8, ks + 12 (ks = w >> 1) of every box, with its 7 column tiles (112
+// accumulators): two waves per SIMD, so one wave's MFMAs run while the other waits on its
+// DMA issue or its LDS reads (ds_read_b64_tr_b16 transposes both operands; a B fragment is
+// read by the two co-tile waves of its k-step).
 // Flush: one fp32 partial row [64][cin_w][27] per workgroup (plain stores), summed into dw
 // by stem_wgrad_reduce_kernel (deterministic, no atomics).
-constexpr int kSWT = 256;                                  // 4 waves, one per SIMD
-// BD = box depth (boxes BD x 4 x 16), NS = ring slots (NS - 1 boxes in flight).  The load
-// pipeline is latency-bound (bytes in flight per CU), so the product ring uses 2-deep boxes
-// in 6 slots (115 KB in flight) rather than 4-deep boxes in 3 slots (86 KB).
-template <int BD> struct SWGeom {
+constexpr int kSWT = 512;                                  // 8 waves, two per SIMD
+constexpr int kSWW = kSWT / 64;
+// BD = box depth (boxes BD x 4 x 16), NS = ring slots (NS - 1 boxes in flight)
+template <int BD, int NT = kSWT> struct SWGeom {
   static constexpr int BV = BD * 64;                            // voxels per box
   static constexpr int HV = (BD + 2) * 6 * 18;                  // halo rows (16 B)
   static constexpr int HRows = (HV + 63) / 64 * 64;             // rows written
   static constexpr int Buf = BV * 128 + HRows * 16;             // bytes per ring slot
-  static constexpr int DYP = BV * 8 / kSWT;                     // dy DMA pieces per thread
-  static constexpr int XI = (HRows / 64 + 3) / 4;               // halo DMA rounds per wave
+  static constexpr int DYP = BV * 8 / NT;                       // dy DMA pieces per thread
+  static constexpr int XI = (HRows / 64 + NT / 64 - 1) / (NT / 64);  // halo DMA rounds per wave (max)
 };
 constexpr int kSWBD = 4;  // box depth (2-deep boxes in 6 slots measured slower)
-constexpr int kSWNS = kSWBD == 4 ? 3 : 6;
+constexpr int kSWNS = 3;
 constexpr int kSWLaneStride = 20;                        // flush: floats per lane (16 used)
-constexpr int kSWRegion = 14 * 64 * kSWLaneStride * 4;   // one wave's 14 tiles, lane-major
+constexpr int kSWRegion = 14 * 64 * kSWLaneStride * 4;   // 14 tiles (2 co x 7 columns), lane-major
 constexpr int kSWRing = kSWNS * SWGeom<kSWBD>::Buf;
 constexpr int kSWLds = kSWRing > 2 * kSWRegion ? kSWRing : 2 * kSWRegion;
 static_assert(kSWLds <= 160 * 1024, "ring / flush regions fit in LDS");
@@ -334,9 +409,11 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   typedef SWGeom<BD> Gm;
   constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
   constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
+  constexpr int XI = Gm::XI;
   extern __shared__ __attribute__((aligned(16))) char swl[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ct = wave & 1, ks = wave >> 1;
   const int hsel = lane >> 5;
   const int nbw = W / BW, nbh = H / BH, nbd = D / BD;
   const int nbox = N * nbd * nbh * nbw;
@@ -353,11 +430,11 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     const int rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
     dyrel[i] = (uint32_t)(((rd * H + rh) * W + rw) * 128 + ql * 16);
   }
-  // halo pieces of this wave: rows wave*64 + lane + 256 i < HRows (XI or XI - 1 of them)
-  const int nxp = (Gm::HRows / 64 - wave + 3) / 4;
-  int xrel[Gm::XI], xco[Gm::XI];
+  // halo pieces of this wave: rows wave*64 + lane + kSWT i < HRows (XI or XI - 1 of them)
+  const int nxp = (Gm::HRows / 64 - wave + kSWW - 1) / kSWW;
+  int xrel[XI], xco[XI];
 #pragma unroll
-  for (int i = 0; i < Gm::XI; ++i) {
+  for (int i = 0; i < XI; ++i) {
     const int hv = wave * 64 + lane + i * kSWT;
     const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
     xrel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
@@ -381,7 +458,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
     const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
 #pragma unroll
-    for (int i = 0; i < Gm::XI; ++i) {
+    for (int i = 0; i < XI; ++i) {
       if (i >= nxp) break;
       uint32_t voff = (uint32_t)(vb * 16 + xrel[i]);
       const int c = xco[i];
@@ -396,48 +473,42 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   };
 
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-  f32x16_t acc[2][7];
+  f32x16_t acc[7];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 7; ++j)
 #pragma unroll
-    for (int j = 0; j < 7; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  // lane offsets of the tr reads, with the wave's k-step offset folded in (k-step s = wave +
-  // 4 i is box row (rd = i, rh = wave): dy rows at s * 2048, halo rows at (i HH + wave) HW)
-  const int aoff0 = dy_off_bf16(8 * hsel + qq, g * 16 + pp * 4) + wave * 2048;
-  const int aoff1 = dy_off_bf16(8 * hsel + qq, 32 + g * 16 + pp * 4) + wave * 2048;
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  // lane offsets of the tr reads, with the wave's k-step offset folded in (k-step s = ks +
+  // 4 i is box row (rd = i, rh = ks): dy rows at s * 2048, halo rows at (i HH + ks) HW)
+  const int aoff = dy_off_bf16(8 * hsel + qq, ct * 32 + g * 16 + pp * 4) + ks * 2048;
   int boff[7];  // column tile j: taps 4 j + 2 g + (pp >> 1), channels 4 (pp & 1) .. + 3
 #pragma unroll
   for (int j = 0; j < 7; ++j)
-    boff[j] = kSWBV * 128 + (8 * hsel + qq + tap_off(4 * j + 2 * g + (pp >> 1), HH, HW) + wave * HW) * 16 + (pp & 1) * 8;
+    boff[j] = kSWBV * 128 + (8 * hsel + qq + tap_off(4 * j + 2 * g + (pp >> 1), HH, HW) + ks * HW) * 16 + (pp & 1) * 8;
   auto compute = [&](const char* buf) {
-    uint32_t pa0 = lds_addr(buf) + aoff0, pa1 = lds_addr(buf) + aoff1, pb[7];
+    uint32_t pa = lds_addr(buf) + aoff, pb[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j) pb[j] = lds_addr(buf) + boff[j];
-    asm volatile("" : "+v"(pa0), "+v"(pa1), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]),
-                 "+v"(pb[5]), "+v"(pb[6]));
+    asm volatile("" : "+v"(pa), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]), "+v"(pb[5]),
+                 "+v"(pb[6]));
     auto tr = [](uint32_t p, int off) {
       return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(uintptr_t)(p + off));
     };
     auto cat = [](s16x4_t lo, s16x4_t hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); };
-    auto load = [&](int i, s16x8_t (&a)[2], s16x8_t (&bq)[7]) {
+    auto load = [&](int i, s16x8_t& a, s16x8_t (&bq)[7]) {
       const int dyb = i * 4 * 2048;
       const int hrb = i * HH * HW * 16;
-      a[0] = cat(tr(pa0, dyb), tr(pa0, dyb + 512));
-      a[1] = cat(tr(pa1, dyb), tr(pa1, dyb + 512));
+      a = cat(tr(pa, dyb), tr(pa, dyb + 512));
 #pragma unroll
       for (int j = 0; j < 7; ++j) bq[j] = cat(tr(pb[j], hrb), tr(pb[j], hrb + 64));
     };
-    s16x8_t a[2][2], bq[2][7];
+    s16x8_t a[2], bq[2][7];
     load(0, a[0], bq[0]);
 #pragma unroll
     for (int i = 0; i < BD; ++i) {
       if (i + 1 < BD) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
 #pragma unroll
-      for (int j = 0; j < 7; ++j)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[ct][j] = mfma(a[i & 1][ct], bq[i & 1][j], acc[ct][j]);
+      for (int j = 0; j < 7; ++j) acc[j] = mfma(a[i & 1], bq[i & 1][j], acc[j]);
     }
   };
 
@@ -451,8 +522,8 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     // every wave's share of box b has landed and every wave is done reading the slot
     // refilled below
     if (b + (NS - 2) * G < nbox) {
-      if (nxp == Gm::XI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI)) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + Gm::XI - 1)) : "memory");
+      if (nxp == XI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + XI)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + XI - 1)) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -464,53 +535,53 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // flush, two stages: waves 0 / 1 store their 14 tiles lane-major into regions 0 / 1 (16 of
-  // every 20 floats per lane: conflict-free ds_write_b128), waves 2 / 3 add theirs into the
-  // same regions, then every thread writes region 0 + region 1 into the partial row (a
-  // fixed summation order: (w0 + w2) + (w1 + w3))
-  float* reg = reinterpret_cast<float*>(swl) + (wave & 1) * (kSWRegion / 4);
-  if (wave < 2) {
+  // flush, two stages: the waves of k-step sets 0 / 1 store their 7 tiles lane-major into
+  // regions 0 / 1 (tiles ct * 7 + j; 16 of every 20 floats per lane: conflict-free
+  // ds_write_b128), the waves of sets 2 / 3 add theirs into the same regions, then every
+  // thread writes region 0 + region 1 into the partial row (a fixed summation order:
+  // (ks0 + ks2) + (ks1 + ks3))
+  float* reg = reinterpret_cast<float*>(swl) + (ks & 1) * (kSWRegion / 4);
+  if (ks < 2) {
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
+    for (int j = 0; j < 7; ++j) {
+      float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
 #pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<f32x4_t*>(dst + 4 * q) =
-              (f32x4_t){acc[ct][j][4 * q], acc[ct][j][4 * q + 1], acc[ct][j][4 * q + 2], acc[ct][j][4 * q + 3]};
-      }
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4_t*>(dst + 4 * q) =
+            (f32x4_t){acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]};
+    }
   }
   __syncthreads();
-  if (wave >= 2) {
+  if (ks >= 2) {
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
+    for (int j = 0; j < 7; ++j) {
+      float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
 #pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f32x4_t v = *reinterpret_cast<f32x4_t*>(dst + 4 * q);
-          v += (f32x4_t){acc[ct][j][4 * q], acc[ct][j][4 * q + 1], acc[ct][j][4 * q + 2], acc[ct][j][4 * q + 3]};
-          *reinterpret_cast<f32x4_t*>(dst + 4 * q) = v;
-        }
+      for (int q = 0; q < 4; ++q) {
+        f32x4_t v = *reinterpret_cast<f32x4_t*>(dst + 4 * q);
+        v += (f32x4_t){acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]};
+        *reinterpret_cast<f32x4_t*>(dst + 4 * q) = v;
       }
+    }
   }
   __syncthreads();
   // partial row [64 co][cin_w][27]: element (co, column 8 t + c) sits in tile (co >> 5, col >> 5),
   // lane (col & 31) + 32 hs, register e, where (e & 3) + 8 (e >> 2) + 4 hs = co & 31
   const float* r0 = reinterpret_cast<const float*>(swl);
   const float* r1 = r0 + kSWRegion / 4;
-  const int per_co = cin_w * 27;
-  const int total = 64 * per_co;
-  float* prow = part + (long)blockIdx.x * total;
-  for (int i = tid; i < total; i += kSWT) {
-    const int co = i / per_co, rem = i - co * per_co;
+  const int per_co = cin_w * 27;  // <= 216: thread (half h, rem) owns column rem of co rows [32 h, 32 h + 32)
+  float* prow = part + (long)blockIdx.x * 64 * per_co;
+  const int hh = tid >> 8, rem = tid & 255;
+  if (rem < per_co) {
     const int c = rem / 27, t = rem - c * 27;
     const int col = 8 * t + c;
-    const int cr = co & 31, hs = (cr >> 2) & 1, e = (cr & 3) + 4 * (cr >> 3);
-    prow[i] = r0[(((co >> 5) * 7 + (col >> 5)) * 64 + (col & 31) + 32 * hs) * kSWLaneStride + e] +
-              r1[(((co >> 5) * 7 + (col >> 5)) * 64 + (col & 31) + 32 * hs) * kSWLaneStride + e];
+    const int cb = ((hh * 7 + (col >> 5)) * 64 + (col & 31)) * kSWLaneStride;
+#pragma unroll
+    for (int cr = 0; cr < 32; ++cr) {
+      const int hs = (cr >> 2) & 1, e = (cr & 3) + 4 * (cr >> 3);
+      const int o = cb + 32 * hs * kSWLaneStride + e;
+      prow[(hh * 32 + cr) * per_co + rem] = r0[o] + r1[o];
+    }
   }
 }
 
@@ -522,8 +593,16 @@ __global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* par
   const int o = blockIdx.x * 32 + ol;
   float s = 0.f;
   if (o < total) {
-#pragma unroll 8
-    for (int r = rg; r < rows; r += 8) s += part[(long)r * total + o];
+    // rows rg, rg + 8, ... summed in that order; loads issued 32 at a time ahead of the adds
+    int r = rg;
+    for (; r + 8 * 31 < rows; r += 8 * 32) {
+      float v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v[k] = part[(long)(r + 8 * k) * total + o];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) s += v[k];
+    }
+    for (; r < rows; r += 8) s += part[(long)r * total + o];
   }
   red[rg][ol] = s;
   __syncthreads();

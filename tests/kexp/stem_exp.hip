@@ -4,6 +4,7 @@
 #include "../../prostate-cancer-multimodal-segmentation_amd/csrc/stem.hip"
 
 namespace {
+constexpr int kSWT4 = 256;  // the 4-wave wgrad experiment kernels
 
 // ---------------------------------------------------------------------------------------
 // (1) wave-specialised stem forward: waves 0-3 compute (MFMA, one per SIMD), waves 4-7 move
@@ -267,10 +268,10 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_ws_kernel(Conv3Params p, int 
 // MODE bit 0: compute, bit 1: halo DMA, bit 2: per-box barrier (else per-wave waits only)
 // ---------------------------------------------------------------------------------------
 template <int BD, int NS, int MODE>
-__global__ void __launch_bounds__(kSWT, 1) wg_exp_kernel(const bf16_t* x, const bf16_t* dy, float* part,
+__global__ void __launch_bounds__(kSWT4, 1) wg_exp_kernel(const bf16_t* x, const bf16_t* dy, float* part,
                                                         int N, int D, int H, int W, uint32_t xbytes,
                                                         uint32_t dybytes) {
-  typedef SWGeom<BD> Gm;
+  typedef SWGeom<BD, kSWT4> Gm;
   constexpr bool COMP = MODE & 1, HALO = MODE & 2, BAR = MODE & 4;
   constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
   constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
@@ -286,7 +287,7 @@ __global__ void __launch_bounds__(kSWT, 1) wg_exp_kernel(const bf16_t* x, const 
   uint32_t dyrel[Gm::DYP];
 #pragma unroll
   for (int i = 0; i < Gm::DYP; ++i) {
-    const int pc = tid + i * kSWT;
+    const int pc = tid + i * kSWT4;
     const int r = pc >> 3, q = pc & 7;
     const int ql = q ^ (((r >> 1) & 1) << 2);
     const int rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(kSWT, 1) wg_exp_kernel(const bf16_t* x, const 
   int xrel[Gm::XI], xco[Gm::XI];
 #pragma unroll
   for (int i = 0; i < Gm::XI; ++i) {
-    const int hv = wave * 64 + lane + i * kSWT;
+    const int hv = wave * 64 + lane + i * kSWT4;
     const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
     xrel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
     xco[i] = hv < kSWHV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
@@ -316,7 +317,7 @@ __global__ void __launch_bounds__(kSWT, 1) wg_exp_kernel(const bf16_t* x, const 
     const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(swl) + slot * kSWBuf + wave * 64 * 16);
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)vb * 128u);
 #pragma unroll
-    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
+    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT4 * 16, dyrel[i], so);
     const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
@@ -329,7 +330,7 @@ __global__ void __launch_bounds__(kSWT, 1) wg_exp_kernel(const bf16_t* x, const 
         const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
         if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
       }
-      dma16(xr, lb + kSWBV * 128 + i * kSWT * 16, voff, 0);
+      dma16(xr, lb + kSWBV * 128 + i * kSWT4 * 16, voff, 0);
     }
   };
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
@@ -719,10 +720,10 @@ constexpr int kW2Region = 14 * 64 * kW2LaneStride * 4;   // 71,680 B
 constexpr int kW2Lds = kSWRing > 2 * kW2Region ? kSWRing : 2 * kW2Region;
 
 template <int BD, int NS>
-__global__ void __launch_bounds__(kSWT, 1) stem_wgrad_v2_kernel(const bf16_t* x, const bf16_t* dy, float* part,
+__global__ void __launch_bounds__(kSWT4, 1) stem_wgrad_v2_kernel(const bf16_t* x, const bf16_t* dy, float* part,
                                                                int N, int D, int H, int W, int cin_w,
                                                                uint32_t xbytes, uint32_t dybytes) {
-  typedef SWGeom<BD> Gm;
+  typedef SWGeom<BD, kSWT4> Gm;
   constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
   constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
   extern __shared__ __attribute__((aligned(16))) char swl[];
@@ -736,7 +737,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_v2_kernel(const bf16_t* x,
   uint32_t dyrel[Gm::DYP];
 #pragma unroll
   for (int i = 0; i < Gm::DYP; ++i) {
-    const int pc = tid + i * kSWT;
+    const int pc = tid + i * kSWT4;
     const int r = pc >> 3, q = pc & 7;
     const int ql = q ^ (((r >> 1) & 1) << 2);
     const int rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
@@ -746,7 +747,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_v2_kernel(const bf16_t* x,
   int xrel[Gm::XI], xco[Gm::XI];
 #pragma unroll
   for (int i = 0; i < Gm::XI; ++i) {
-    const int hv = wave * 64 + lane + i * kSWT;
+    const int hv = wave * 64 + lane + i * kSWT4;
     const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
     xrel[i] = (((hd_ - 1) * H + (hh_ - 1)) * W + (hw_ - 1)) * 16;
     xco[i] = hv < kSWHV ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
@@ -766,7 +767,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_v2_kernel(const bf16_t* x,
     const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(swl) + slot * kSWBuf + wave * 64 * 16);
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)vb * 128u);
 #pragma unroll
-    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
+    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT4 * 16, dyrel[i], so);
     const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
 #pragma unroll
     for (int i = 0; i < Gm::XI; ++i) {
@@ -779,7 +780,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_v2_kernel(const bf16_t* x,
         const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
         if ((unsigned)gd >= (unsigned)D || (unsigned)gh >= (unsigned)H || (unsigned)gw >= (unsigned)W) voff = kOOB;
       }
-      dma16(xr, lb + kSWBV * 128 + i * kSWT * 16, voff, 0);
+      dma16(xr, lb + kSWBV * 128 + i * kSWT4 * 16, voff, 0);
     }
   };
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
@@ -882,7 +883,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_v2_kernel(const bf16_t* x,
   const int per_co = cin_w * 27;
   const int total = 64 * per_co;
   float* prow = part + (long)blockIdx.x * total;
-  for (int i = tid; i < total; i += kSWT) {
+  for (int i = tid; i < total; i += kSWT4) {
     const int co = i / per_co, rem = i - co * per_co;
     const int c = rem / 27, t = rem - c * 27;
     const int col = 8 * t + c;
@@ -929,7 +930,7 @@ int exp_wg(int mode, int ns, const void* x, const void* dy, float* part, int N, 
   if (mode == M && ns == NSV) {                                                                                 \
     auto k = wg_exp_kernel<4, NSV, M>;                                                                          \
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, NSV * SWGeom<4>::Buf); \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kSWT), NSV * SWGeom<4>::Buf, s, (const bf16_t*)x, (const bf16_t*)dy,   \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kSWT4), NSV * SWGeom<4>::Buf, s, (const bf16_t*)x, (const bf16_t*)dy,   \
                        part, N, D, H, W, xb, yb);                                                               \
     return (int)hipGetLastError();                                                                              \
   }
@@ -980,7 +981,7 @@ int exp_stem_wgrad_v2(const void* x, const void* dy, float* dw, float* ws, int c
   const long xbytes = (long)N * D * H * W * 16, dybytes = (long)N * D * H * W * 128;
   auto kern = stem_wgrad_v2_kernel<kSWBD, kSWNS>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kW2Lds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT), kW2Lds, s, (const bf16_t*)x, (const bf16_t*)dy, ws, N, D, H, W,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT4), kW2Lds, s, (const bf16_t*)x, (const bf16_t*)dy, ws, N, D, H, W,
                      cin_w, (uint32_t)xbytes, (uint32_t)dybytes);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
