@@ -109,6 +109,13 @@ __device__ __forceinline__ void dma16(i32x4_t rsrc, uint32_t lds_base, uint32_t 
                : "s"(lds_base), "v"(voff), "s"(rsrc), "s"(soff)
                : "memory", "m0");
 }
+// the same with the non-temporal policy (data read once: streamed past the caches)
+__device__ __forceinline__ void dma16_nt(i32x4_t rsrc, uint32_t lds_base, uint32_t voff, uint32_t soff) {
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen nt lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rsrc), "s"(soff)
+               : "memory", "m0");
+}
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }

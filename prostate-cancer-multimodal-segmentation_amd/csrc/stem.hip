@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   auto item_full = [&](f32x16_t (&acc)[2][2], int mt, int e, const uint32_t (&so)[2]) {
     const int g = e >> 2, rw = 4 * g + (e & 3);
     const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-    __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 2);
     const float e0 = v0 - K[0], e1 = v1 - K[1];
     s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
     s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         const uint32_t voff = valid ? (gB ? vB : vA) : kOOB;
         const float e0 = valid ? v0 - K[0] : 0.f, e1 = valid ? v1 - K[1] : 0.f;
         cnt += valid ? 1.f : 0.f;
-        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so[mt] + rw * 128, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so[mt] + rw * 128, 2);
         s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
         s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
       }
@@ -455,7 +455,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(swl) + slot * kSWBuf + wave * 64 * 16);
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)vb * 128u);
 #pragma unroll
-    for (int i = 0; i < Gm::DYP; ++i) dma16(dr, lb + i * kSWT * 16, dyrel[i], so);
+    for (int i = 0; i < Gm::DYP; ++i) dma16_nt(dr, lb + i * kSWT * 16, dyrel[i], so);
     const bool inner = d0 >= 1 && d0 + BD < D && h0 >= 1 && h0 + BH < H && w0 >= 1 && w0 + BW < W;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
