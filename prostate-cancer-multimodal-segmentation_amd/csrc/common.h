@@ -76,6 +76,41 @@ template <> __device__ __forceinline__ void store16<bf16_t>(bf16_t* p, const flo
   *reinterpret_cast<u32x4_t*>(p) = v;
 }
 
+// non-temporal forms (streams far larger than the 256 MB Infinity Cache: nothing to keep)
+template <typename T> __device__ __forceinline__ void load16_nt(const T* p, float* out);
+template <> __device__ __forceinline__ void load16_nt<float>(const float* p, float* out) {
+  f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p));
+  out[0] = v[0]; out[1] = v[1]; out[2] = v[2]; out[3] = v[3];
+}
+template <> __device__ __forceinline__ void load16_nt<bf16_t>(const bf16_t* p, float* out) {
+  u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    out[2 * i] = __uint_as_float(v[i] << 16);
+    out[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+template <typename T> __device__ __forceinline__ void store16_nt(T* p, const float* in);
+template <> __device__ __forceinline__ void store16_nt<float>(float* p, const float* in) {
+  f32x4_t v = {in[0], in[1], in[2], in[3]};
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4_t*>(p));
+}
+template <> __device__ __forceinline__ void store16_nt<bf16_t>(bf16_t* p, const float* in) {
+  u32x4_t v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = (uint32_t)f2bf(in[2 * i]) | ((uint32_t)f2bf(in[2 * i + 1]) << 16);
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+}
+template <bool NT, typename T> __device__ __forceinline__ void ld16(const T* p, float* out) {
+  if constexpr (NT) load16_nt<T>(p, out); else load16<T>(p, out);
+}
+template <bool NT, typename T> __device__ __forceinline__ void st16(T* p, const float* in) {
+  if constexpr (NT) store16_nt<T>(p, in); else store16<T>(p, in);
+}
+// streams this large bypass the caches (non-temporal loads / stores)
+constexpr long kNtBytes = 128L << 20;
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -144,7 +144,8 @@ constexpr int kCDPieces = kCDStage / 16 / 512;                    // 6 per threa
 
 __device__ __forceinline__ int cd_slot(int row, int slot) { return row * 128 + ((slot ^ (row & 7)) << 4); }
 
-template <bool FWD>
+// NT (forward): non-temporal output stores, for outputs far larger than the Infinity Cache
+template <bool FWD, bool NT = false>
 __global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, const bf16_t* wpk, const float* bias,
                                                            bf16_t* out, UpGeom g, int Cin, int Cout) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -243,9 +244,12 @@ __global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, 
       if (m >= M) continue;
       bf16_t* crow = out + child_base(g, m) * Cout;
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
-        *reinterpret_cast<uint32_t*>(crow + dq[pr] + cq[pr]) =
-            pack_bf16x2(acc[2 * pr][e] + b0[pr], acc[2 * pr + 1][e] + b1[pr]);
+      for (int pr = 0; pr < 2; ++pr) {
+        const uint32_t v = pack_bf16x2(acc[2 * pr][e] + b0[pr], acc[2 * pr + 1][e] + b1[pr]);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(crow + dq[pr] + cq[pr]);
+        if constexpr (NT) __builtin_nontemporal_store(v, dst);
+        else *dst = v;
+      }
     }
   } else {
 #pragma unroll
@@ -517,9 +521,10 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
   }
   const long M = (long)N * Din * Hin * Win;
   if (dtype == PCMS_BF16 && Cin % 64 == 0 && (8 * Cout) % kCDN == 0) {
-    (void)hipFuncSetAttribute((const void*)convt_lds_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * kCDStage);
-    hipLaunchKernelGGL(convt_lds_kernel<true>, dim3(cdiv(M, kCDM), 8 * Cout / kCDN), dim3(512), 2 * kCDStage, s,
+    const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;
+    auto kern = nt ? convt_lds_kernel<true, true> : convt_lds_kernel<true, false>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kCDStage);
+    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), 8 * Cout / kCDN), dim3(512), 2 * kCDStage, s,
                        (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
     PCMS_CHECK_LAUNCH();
   }

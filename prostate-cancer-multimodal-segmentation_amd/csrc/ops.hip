@@ -108,7 +108,10 @@ __global__ void bn_eval_coeffs_kernel(const float* gamma, const float* beta, con
 
 // a = relu(y * scale[c] + shift[c]); 16-byte vectors.  Block = (256 / CG) voxel lanes x
 // CG channel groups, so every thread keeps its VEC channels' coefficients in registers.
-template <typename T>
+// NT: non-temporal loads and stores for tensors far larger than the Infinity Cache
+// (measured: level-0 bn_relu 90 -> 87 us; walking the voxels in reverse to catch the
+// producer's cached tail bought nothing)
+template <typename T, bool NT>
 __global__ void __launch_bounds__(TPB) bn_relu_kernel(const T* y, T* a, const float* scale, const float* shift,
                                                       int C, long nvox) {
   constexpr int VEC = Elem<T>::kVec;
@@ -120,16 +123,16 @@ __global__ void __launch_bounds__(TPB) bn_relu_kernel(const T* y, T* a, const fl
   for (int j = 0; j < VEC; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
   for (long v = (long)blockIdx.x * VL + vl; v < nvox; v += (long)gridDim.x * VL) {
     float x[VEC];
-    load16<T>(y + v * C + c0, x);
+    ld16<NT>(y + v * C + c0, x);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) x[j] = fmaxf(x[j] * sc[j] + sh[j], 0.f);
-    store16<T>(a + v * C + c0, x);
+    st16<NT>(a + v * C + c0, x);
   }
 }
 
 // BN+ReLU backward, pass 1: per-block partial sums of g and g*xhat, g = da * [a > 0].
 // Block: 256 threads = (256 / C8) voxel lanes x C8 channel groups of VEC channels.
-template <typename T>
+template <typename T, bool NT>
 __global__ void __launch_bounds__(TPB) bn_relu_bwd_reduce_kernel(
     const T* da, const T* y, const float* scale, const float* shift, const float* mean,
     const float* invstd, float* part, int C, long nvox) {
@@ -160,8 +163,8 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_reduce_kernel(
     float dv[4][VEC], yv[4][VEC];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      load16<T>(da + (v + u * stride) * C + c0, dv[u]);
-      load16<T>(y + (v + u * stride) * C + c0, yv[u]);
+      ld16<NT>(da + (v + u * stride) * C + c0, dv[u]);
+      ld16<NT>(y + (v + u * stride) * C + c0, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc1(dv[u], yv[u]);
@@ -202,7 +205,8 @@ __global__ void bn_bwd_finalize_kernel(const double* ws, int C, double count, co
   coef[c * 3 + 2] = (float)(-k1 * s1 / count);
 }
 
-template <typename T>
+// NT: as bn_relu_kernel (level-0 apply: 805 MB in 118 us = 6.8 TB/s)
+template <typename T, bool NT>
 __global__ void __launch_bounds__(TPB) bn_relu_bwd_apply_kernel(
     const T* da, const T* y, const float* scale, const float* shift, const float* mean, const float* invstd,
     const float* coef, T* dy, int C, long nvox) {
@@ -219,14 +223,14 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_apply_kernel(
   }
   for (long v = (long)blockIdx.x * VL + vl; v < nvox; v += (long)gridDim.x * VL) {
     float dv[VEC], yv[VEC], o[VEC];
-    load16<T>(da + v * C + c0, dv);
-    load16<T>(y + v * C + c0, yv);
+    ld16<NT>(da + v * C + c0, dv);
+    ld16<NT>(y + v * C + c0, yv);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float g = (yv[j] * sc[j] + sh[j] > 0.f) ? dv[j] : 0.f;
       o[j] = k1[j] * g + k2[j] * ((yv[j] - mu[j]) * is[j]) + k3[j];
     }
-    store16<T>(dy + v * C + c0, o);
+    st16<NT>(dy + v * C + c0, o);
   }
 }
 
@@ -737,8 +741,13 @@ int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const fl
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || TPB % (C / VEC)) return -1;
   const int grid = ew_grid(dtype, C, nvox);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(bn_relu_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, (bf16_t*)a, scale, shift, C, nvox);
-  else hipLaunchKernelGGL(bn_relu_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)y, (float*)a, scale, shift, C, nvox);
+  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((nt ? bn_relu_kernel<bf16_t, true> : bn_relu_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0, s,
+                       (const bf16_t*)y, (bf16_t*)a, scale, shift, C, nvox);
+  else
+    hipLaunchKernelGGL((nt ? bn_relu_kernel<float, true> : bn_relu_kernel<float, false>), dim3(grid), dim3(TPB), 0, s,
+                       (const float*)y, (float*)a, scale, shift, C, nvox);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -755,10 +764,13 @@ int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scal
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || (TPB % (C / VEC)) != 0) return -1;
   const int rows = pcms_bn_bwd_rows(dtype, C, nvox);
+  // the reduce keeps the default cache policy: what it leaves in the Infinity Cache the apply
+  // pass below re-reads (measured: nt here 99 us but the apply 118 -> 135 us at level 0)
+  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<bf16_t>, dim3(rows), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, part, C, nvox);
+    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<bf16_t, false>, dim3(rows), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, part, C, nvox);
   else
-    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<float>, dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
+    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<float, false>, dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C,
@@ -771,9 +783,9 @@ int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scal
   if (e != hipSuccess) return (int)e;
   const int grid = ew_grid(dtype, C, nvox);
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, (const float*)coef, (bf16_t*)dy, C, nvox);
+    hipLaunchKernelGGL((nt ? bn_relu_bwd_apply_kernel<bf16_t, true> : bn_relu_bwd_apply_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, (const float*)coef, (bf16_t*)dy, C, nvox);
   else
-    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, (const float*)coef, (float*)dy, C, nvox);
+    hipLaunchKernelGGL((nt ? bn_relu_bwd_apply_kernel<float, true> : bn_relu_bwd_apply_kernel<float, false>), dim3(grid), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, (const float*)coef, (float*)dy, C, nvox);
   PCMS_CHECK_LAUNCH();
 }
 
