@@ -768,9 +768,9 @@ int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scal
   // pass below re-reads (measured: nt here 99 us but the apply 118 -> 135 us at level 0)
   const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<bf16_t, false>, dim3(rows), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, part, C, nvox);
+    hipLaunchKernelGGL((bn_relu_bwd_reduce_kernel<bf16_t, false>), dim3(rows), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, part, C, nvox);
   else
-    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<float, false>, dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
+    hipLaunchKernelGGL((bn_relu_bwd_reduce_kernel<float, false>), dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C,
