@@ -1074,18 +1074,22 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
 // of the next box's first taps count them).  BatchNorm partials: per wave a running Chan
 // merge over its boxes (count, mean, M2 per channel); one stats row per slot at the end.
 // ------------------------------------------------------------------------------------
-constexpr int kBgThreads = 256;
+constexpr int kBgThreads = 512;  // 8 waves = 4 M-groups x 2 N-tiles, two waves per SIMD
 constexpr int kBgHH = 10, kBgHW = 18;
 constexpr int kBgBD = 8;                                                  // box depth
 constexpr int kBgMT = 8;                                                  // M-tiles per wave
 constexpr int kBgHalo = (kBgBD + 2) * kBgHH * kBgHW;                      // rows x 32 B
-constexpr int kBgPieces = (2 * kBgHalo + kBgThreads - 1) / kBgThreads;    // DMA pieces / thread
-constexpr int kBgBuf = kBgPieces * kBgThreads * 16;                       // (tail pad)
+constexpr int kBgPieces = (2 * kBgHalo + kBgThreads - 1) / kBgThreads;    // DMA pieces / thread (8)
+// pieces pc = tid + 512 j; the last round (j = 7) holds real rows only for wave 0: the other
+// waves aim it at a 1 KiB dummy slot (out-of-range source: no memory traffic) so every wave
+// issues the same count; a buffer holds rows up to wave 0's last piece
+constexpr int kBgBuf = ((kBgPieces - 1) * kBgThreads + 64) * 16;
+constexpr int kBgDummy = 1024;
 constexpr int kBgStage = 64 * 128;                                        // per-wave store slice
 constexpr int kBgRed = 4 * 64 * 3 * 4;                                    // BN moments
-constexpr int kBgLds = 2 * kBgBuf + 4 * kBgStage + kBgRed + 64 * 4;       // + bias
+constexpr int kBgLds = 2 * kBgBuf + kBgDummy + 4 * kBgStage + kBgRed + 64 * 4;  // + bias
 constexpr int kBgDist = 8;                 // B prefetch distance (taps); (Dist + 1) | 27
-constexpr int kBgEpiStores = kBgMT * 4;    // 16-B stores per wave and box
+constexpr int kBgEpiStores = kBgMT * 2;    // 16-B stores per wave and box
 static_assert(27 % (kBgDist + 1) == 0, "B ring index must continue across chunks");
 static_assert(kBgLds <= 160 * 1024, "LDS");
 
@@ -1100,16 +1104,16 @@ template <int Imm> __device__ __forceinline__ void bload16(s16x8_t& dst, i32x4_t
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3" : "=v"(dst) : "v"(voff), "s"(rsrc), "n"(Imm)
                : "memory");
 }
-template <int N> __device__ __forceinline__ void vm_wait2(s16x8_t& a, s16x8_t& b) {
+template <int N> __device__ __forceinline__ void vm_wait1(s16x8_t& a) {
   static_assert(N >= 0 && N <= 63, "vmcnt");
-  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
 }
-// vector-memory ops issued after B(t)'s second load by the time tap t waits for it: every
-// tap s issues B(s + D) x 2 then piece(s) (s < 15, chunk-relative, every chunk alike)
+// vector-memory ops issued after B(t)'s load by the time tap t waits for it: every tap s
+// issues B(s + D) then piece(s) (s < P, chunk-relative, every chunk alike)
 template <int P> constexpr int bg_piece(int s) { return ((s % 27) + 27) % 27 < P ? 1 : 0; }
 template <int P, int Dist> constexpr int bg_wait(int t) {
   int n = bg_piece<P>(t - Dist);
-  for (int s = t - Dist + 1; s <= t; ++s) n += 2 + bg_piece<P>(s);
+  for (int s = t - Dist + 1; s <= t; ++s) n += 1 + bg_piece<P>(s);
   return n;
 }
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -1121,6 +1125,8 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r_lane = lane & 31, hsel = lane >> 5;
+  // wave = (M-group mg: box voxel rows 256 mg ..; N-tile nt: the output channels of parity nt)
+  const int mg = wave & 3, nt = wave >> 2;
   const int Cout = p.Cout, ncob = Cout >> 6;
   // logical workgroup id: consecutive ids on one XCD (dispatch is round-robin over 8), output
   // channel block fastest, so the workgroups sharing a halo (and neighbouring boxes) share L2
@@ -1159,8 +1165,10 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
         (unsigned)gw < (unsigned)p.W)
       voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs +
               (uint32_t)((pc & 1) ^ ((hw_ >> 3) & 1)) * 8u) * 2u;
-    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
-    dma16(first ? xr0 : xr1, lb, voff, 0);
+    const bool dummy = j == kBgPieces - 1 && wave > 0;  // wave-uniform
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(
+        dummy ? lds0 + 2 * kBgBuf : lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
+    dma16(first ? xr0 : xr1, lb, dummy ? kOOB : voff, 0);
   };
 
   // A fragment byte offsets in a halo buffer: MFMA row r = 256 wave + 32 mt + perm32(lane)
@@ -1178,16 +1186,15 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   const int nchunk = p.Cin >> 4;
   const uint32_t tap_bytes = (uint32_t)Cout * 64u;
   const i32x4_t wr = buffer_desc(p.w, (uint32_t)(p.Cin >> 5) * 27u * tap_bytes);
-  auto load_b = [&](s16x8_t (&dst)[2], int chunk, int tap, uint32_t boff) {
+  auto load_b = [&](s16x8_t& dst, int chunk, int tap, uint32_t boff) {
     const uint32_t off = boff + (uint32_t)((chunk >> 1) * 27 + tap) * tap_bytes + (uint32_t)(chunk & 1) * 32u;
-    bload16<0>(dst[0], wr, off);
-    bload16<64>(dst[1], wr, off);
+    bload16<0>(dst, wr, off);
   };
 
   // epilogue constants: output columns are channel pairs (column j of N-tile nt = channel
   // 2 j + nt); two-pointer output split at cy0 (workgroup-uniform)
   // (bias and the running BatchNorm moments live in LDS between boxes, not in registers)
-  float* red = reinterpret_cast<float*>(lds + 2 * kBgBuf + 4 * kBgStage);  // [wave][64][3]
+  float* red = reinterpret_cast<float*>(lds + 2 * kBgBuf + kBgDummy + 4 * kBgStage);  // [mg][64][3]
   float* bls = red + 4 * 64 * 3;                                           // [64]
   if (tid < 64) bls[tid] = p.bias ? p.bias[co_base + tid] : 0.f;
   const bool to0 = co_base < p.cy0;
@@ -1197,11 +1204,11 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   // every byte offset fits 31 bits)
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
       to0 ? p.y0 : p.y1, (short)0, (int)(p.nvox * ys * 2), 0x00020000);
-  char* stg = lds + 2 * kBgBuf + wave * kBgStage;
+  char* stg = lds + 2 * kBgBuf + kBgDummy + mg * kBgStage;  // shared by the M-group's two waves
   int nbdone = 0;  // boxes merged into the running moments (uniform: kept in an SGPR)
 
-  f32x16_t acc[MT][2];
-  s16x8_t bset[kBgDist + 1][2];
+  f32x16_t acc[MT];
+  s16x8_t bset[kBgDist + 1];
   int box = slot;
   int n, d0, h0, w0;
   origin(box, n, d0, h0, w0);
@@ -1214,7 +1221,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 #pragma unroll
   for (int j = 0; j < kBgPieces; ++j) stage_piece(n, d0, h0, w0, 0, 0, j, true);
 #pragma unroll
-  for (int t = 0; t < kBgDist; ++t) load_b(bset[t], 0, t, (uint32_t)((co_base + 2 * r_lane) * 64 + hsel * 16));
+  for (int t = 0; t < kBgDist; ++t) load_b(bset[t], 0, t, (uint32_t)((co_base + 2 * r_lane + nt) * 64 + hsel * 16));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int buf = 0;
@@ -1222,9 +1229,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
     const int nbx = box + nslot;
     const bool has_next = nbx < nbox;
     int nn = n, nd0 = d0, nh0 = h0, nw0 = w0;
@@ -1241,11 +1246,11 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
       const char* hl = lds + buf * kBgBuf;
       const int lo = opaque(lane);
       const int prow = perm32(lo & 31), hs = lo >> 5;
-      const int hbase = ((2 * wave * kBgHH + (prow >> 4)) * kBgHW + (prow & 15)) * 32;
+      const int hbase = ((2 * mg * kBgHH + (prow >> 4)) * kBgHW + (prow & 15)) * 32;
       int swk[3];
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) swk[kw] = hbase + kw * 32 + ((hs ^ ((((prow & 15) + kw) >> 3) & 1)) << 4);
-      const uint32_t boff = (uint32_t)((co_base + 2 * (lo & 31)) * 64 + hs * 16);
+      const uint32_t boff = (uint32_t)((co_base + 2 * (lo & 31) + nt) * 64 + hs * 16);
       auto read_a1 = [&](int tap, int mt) {
         const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
         return *reinterpret_cast<const s16x8_t*>(hl + swk[kw] + (kd * kBgHH + kh) * kBgHW * 32 +
@@ -1264,13 +1269,12 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
         if constexpr (tn < 27) load_b(bset[tn % (kBgDist + 1)], chunk, tn, boff);
         else load_b(bset[tn % (kBgDist + 1)], schunk, tn - 27, boff);
         if constexpr (tap < kBgPieces) stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, tap, live);
-        s16x8_t(&b)[2] = bset[tap % (kBgDist + 1)];
+        s16x8_t& b = bset[tap % (kBgDist + 1)];
         constexpr int extra = (Slack && tap < kBgDist) ? kBgEpiStores : 0;
-        vm_wait2<bg_wait<kBgPieces, kBgDist>(tap) + extra>(b[0], b[1]);
+        vm_wait1<bg_wait<kBgPieces, kBgDist>(tap) + extra>(b);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          acc[mt][0] = mfma(a[mt], b[0], acc[mt][0]);
-          acc[mt][1] = mfma(a[mt], b[1], acc[mt][1]);
+          acc[mt] = mfma(a[mt], b, acc[mt]);
           if constexpr (tap + 1 < 27) a[mt] = read_a1(tap + 1, mt);
         }
       });
@@ -1279,7 +1283,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
       // everything: the epilogue needs registers, and the compiler may move (or, after the
       // workgroup's last box, reuse) the destinations of the next box's B loads -- they
       // must hold landed data by then (costs one L2 round trip per box).
-      if (!last) vm_wait<2 * (27 - kBgPieces)>();
+      if (!last) vm_wait<27 - kBgPieces>();
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       buf ^= 1;
@@ -1287,23 +1291,24 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     run_chunk(0, std::true_type{});
     for (int chunk = 1; chunk < nchunk; ++chunk) run_chunk(chunk, std::false_type{});
 
-    // ---- epilogue of this box, two M-tiles at a time: + bias, bf16 pairs into the wave's
-    // LDS slice (row = 32 mm + C row, 128 B of 32 channel pairs), read back as 8 x 16 B per
-    // lane = whole 128-B channel rows, 16-B stores.  BatchNorm moments in the same pass,
-    // shifted by K (the running mean; the bias before the first box): box mean K + S1 / n,
-    // M2 = S2 - S1^2 / n, Chan-merged into the running moments.
+    // ---- epilogue of this box, two M-tiles at a time: + bias, bf16 channels into the
+    // M-group's LDS slice (row = 32 mm + C row, 128 B of 64 channels; the two waves of the
+    // group write the even / odd channels), read back as 4 x 16 B per lane and wave = whole
+    // 128-B channel rows, 16-B stores.  BatchNorm moments in the same pass, shifted by K
+    // (the running mean; the bias before the first box): box mean K + S1 / n, M2 = S2 -
+    // S1^2 / n, Chan-merged into the running moments.
     // (lane-dependent offsets from an opaque lane copy: box-invariant, the compiler would
     // hoist them out of the box loop and spill them)
     const int lane_o = opaque(lane);
     const long plane = (long)p.H * p.W;
     const long vbase = (((long)n * p.D + d0) * p.H + h0) * p.W + w0;
-    char* wst = stg + (lane_o & 31) * 4 + (lane_o >> 5) * 512;
-    float* rme = red + (wave * 64 + 2 * (lane_o & 31)) * 3;  // [ch][mean, M2, n] x 2 channels
-    const float bias0 = bls[2 * (lane_o & 31)], bias1 = bls[2 * (lane_o & 31) + 1];
+    char* wst = stg + (lane_o & 31) * 4 + nt * 2 + (lane_o >> 5) * 512;
+    float* rme = red + (mg * 64 + 2 * (lane_o & 31) + nt) * 3;  // [ch][mean, M2, n] of this wave's channel
+    const float bias0 = bls[2 * (lane_o & 31) + nt];
     const float rn = (float)nbdone * (32.f * MT);
-    const float K0 = nbdone ? rme[0] : bias0, K1 = nbdone ? rme[3] : bias1;
-    const float c0s = bias0 - K0, c1s = bias1 - K1;  // d = acc + bias - K
-    float S1[2] = {0.f, 0.f}, S2[2] = {0.f, 0.f};
+    const float K0 = nbdone ? rme[0] : bias0;
+    const float c0s = bias0 - K0;  // d = acc + bias - K
+    float S1 = 0.f, S2 = 0.f;
 #pragma unroll
     for (int pass = 0; pass < MT / 2; ++pass) {
 #pragma unroll
@@ -1311,43 +1316,42 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int row = mm * 32 + (e & 3) + 8 * (e >> 2);
-          const float v0 = acc[2 * pass + mm][0][e], v1 = acc[2 * pass + mm][1][e];
-          *reinterpret_cast<uint32_t*>(wst + row * 128) = pack_bf16x2(v0 + bias0, v1 + bias1);
-          const float e0 = v0 + c0s, e1 = v1 + c1s;
-          S1[0] += e0;
-          S1[1] += e1;
-          S2[0] = fmaf(e0, e0, S2[0]);
-          S2[1] = fmaf(e1, e1, S2[1]);
+          const float v0 = acc[2 * pass + mm][e];
+          *reinterpret_cast<bf16_t*>(wst + row * 128) = f2bf(v0 + bias0);
+          const float e0 = v0 + c0s;
+          S1 += e0;
+          S2 = fmaf(e0, e0, S2);
         }
-      asm volatile("" ::: "memory");
+      // both waves of the M-group have written their channels of the slice (raw barrier:
+      // __syncthreads() would also drain this wave's stores of the previous pass)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int row = k * 8 + (lane_o >> 3), c16 = lane_o & 7;
+      for (int k = 0; k < 4; ++k) {
+        const int row = (4 * nt + k) * 8 + (lane_o >> 3), c16 = lane_o & 7;
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(stg + row * 128 + c16 * 16);
         const int mt = 2 * pass + (row >> 5), pr = perm32(row & 31);
-        const int rd = 2 * wave + (mt >> 2), rh = 2 * (mt & 3) + (pr >> 4), rw = pr & 15;
+        const int rd = 2 * mg + (mt >> 2), rh = 2 * (mt & 3) + (pr >> 4), rw = pr & 15;
         const long vox = vbase + (long)rd * plane + (long)rh * p.W + rw;
         __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0, 0);
       }
-      asm volatile("" ::: "memory");
+      // both waves are done reading the slice before the next pass rewrites it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
     {
       constexpr float nb = 32.f * MT;  // voxels per wave and box
       const float nnew = rn + nb;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const float s1 = S1[nt] + __shfl_xor(S1[nt], 32, 64);
-        const float s2 = S2[nt] + __shfl_xor(S2[nt], 32, 64);
-        const float K = nt ? K1 : K0;
-        const float mbox = K + s1 / nb;
-        const float m2b = fmaxf(s2 - s1 * s1 / nb, 0.f);
-        const float rmean = nbdone ? rme[3 * nt] : 0.f, rm2 = nbdone ? rme[3 * nt + 1] : 0.f;
-        const float delta = mbox - rmean;
-        if ((lane_o >> 5) == 0) {
-          rme[3 * nt] = rmean + delta * (nb / nnew);
-          rme[3 * nt + 1] = rm2 + m2b + delta * delta * (rn * nb / nnew);
-          rme[3 * nt + 2] = nnew;
-        }
+      const float s1 = S1 + __shfl_xor(S1, 32, 64);
+      const float s2 = S2 + __shfl_xor(S2, 32, 64);
+      const float mbox = K0 + s1 / nb;
+      const float m2b = fmaxf(s2 - s1 * s1 / nb, 0.f);
+      const float rmean = nbdone ? rme[0] : 0.f, rm2 = nbdone ? rme[1] : 0.f;
+      const float delta = mbox - rmean;
+      if ((lane_o >> 5) == 0) {
+        rme[0] = rmean + delta * (nb / nnew);
+        rme[1] = rm2 + m2b + delta * delta * (rn * nb / nnew);
+        rme[2] = nnew;
       }
       ++nbdone;
     }
