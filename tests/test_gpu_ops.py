@@ -502,13 +502,14 @@ def test_pack_input(dt, code):
 
 @pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (1, (9, 10, 11)), (2, (8, 8, 4)), (1, (6, 20, 33)),
                                  (1, (8, 12, 48)), (3, (4, 4, 16)), (1, (32, 32, 32)), (1, (48, 64, 64)),
-                                 (2, (32, 64, 64))])
+                                 (2, (32, 64, 64)), (1, (12, 16, 16)), (4, (8, 64, 128))])
 def test_stem_fwd_wgrad_bf16(N, S):
     """Dedicated stem kernels (tap-pair packed K) vs torch conv3d on the bf16-rounded input,
     on the shapes they support (pcms_stem_supported; others refuse and the engine takes the
     general kernels)."""
     L = _lib()
     sup = L.query("pcms_stem_supported", N, *S)
+    # (4, (8, 64, 128)): 4096 boxes, 16 per persistent workgroup of each kernel
     hot = S[0] % 4 == 0 and S[1] % 4 == 0 and S[2] % 16 == 0
     if hot:
         assert sup == 3, (S, sup)
