@@ -380,6 +380,92 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad_kernel(const T* x, const T
     }
 }
 
+// bf16, Cin % 128 == 0: the same product with all 128 input channels of a tile in one
+// workgroup, so each dout child row is staged once per 128 ci instead of once per 64 (at
+// level 0, Cin = 128: dout -- 268 MB -- read once, not twice).  x tile [VB][128] as two
+// [VB][64] halves; 8 waves = (ci quarter cq, co half), each all 8 taps (8 accumulators):
+// per 16 voxels one x fragment and 8 dout fragments feed 8 MFMAs.
+__global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout, float* ws,
+                                                               UpGeom g, int Cin, int Cout, int vox_per_split) {
+  constexpr int VB = 64, ROW = 128, PPR = 8;
+  constexpr int XP = VB * 2 * PPR;               // x pieces (two 64-ci halves)
+  constexpr int NP = XP + 8 * VB * PPR;          // + 8 taps
+  constexpr int PT = NP / 512;                   // 10 per thread
+  static_assert(NP % 512 == 0, "whole pieces per thread");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* P = lds;                                 // x tiles [2][VB][64]
+  char* Q = lds + 2 * VB * ROW;                  // dout tiles [8][VB][64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int cq = wave & 3, wq = wave >> 2;       // ci quarter, co half
+  const int p0 = blockIdx.z * 128;               // ci tile
+  const int co0 = blockIdx.y * 64;               // co tile
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  const long vbeg = (long)blockIdx.x * vox_per_split;
+  const long vend = std::min<long>(M, vbeg + vox_per_split);
+  f32x16_t acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  const int gg = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int ca = (cq & 1) * 32 + gg * 16 + pp * 4, cb = wq * 32 + gg * 16 + pp * 4;
+  const char* Pq = P + (cq >> 1) * VB * ROW;
+  for (long vb = vbeg; vb < vend; vb += VB) {
+    u32x4_t stg[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int pc = tid + i * 512;
+      const bf16_t* src;
+      int v;
+      if (pc < XP) {                             // x: (half, voxel, piece)
+        const int hf = pc / (VB * PPR), rem = pc % (VB * PPR);
+        v = rem / PPR;
+        const long m = std::min<long>(vb + v, vend - 1);
+        src = x + m * Cin + p0 + hf * 64 + (rem % PPR) * 8;
+      } else {                                   // dout tap t
+        const int t = (pc - XP) / (VB * PPR), rem = (pc - XP) % (VB * PPR);
+        v = rem / PPR;
+        const long m = std::min<long>(vb + v, vend - 1);
+        src = dout + child_vox(g, m, t) * Cout + co0 + (rem % PPR) * 8;
+      }
+      stg[i] = *reinterpret_cast<const u32x4_t*>(src);
+      if (vb + v >= vend) stg[i] = (u32x4_t){0u, 0u, 0u, 0u};
+    }
+    __syncthreads();  // every wave is done with the previous block's tiles
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int pc = tid + i * 512;
+      const int tile = pc / (VB * PPR), rem = pc % (VB * PPR);  // tiles 0-1: x halves, 2-9: taps
+      const int v = rem / PPR, q = rem % PPR;
+      *reinterpret_cast<u32x4_t*>(lds + tile * VB * ROW + half_swz(v, q * 8)) = stg[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k0 = 0; k0 < VB; k0 += 16) {
+      const int v = k0 + 8 * h + qq;
+      s16x4_t a0 = tr_read(Pq, half_swz(v, ca)), a1 = tr_read(Pq, half_swz(v + 4, ca));
+      s16x8_t a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const char* Qt = Q + t * VB * ROW;
+        s16x4_t b0 = tr_read(Qt, half_swz(v, cb)), b1 = tr_read(Qt, half_swz(v + 4, cb));
+        s16x8_t b = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        acc[t] = mfma(a, b, acc[t]);
+      }
+    }
+  }
+  // C[row = ci][col = co] per tap -> this split's partial row ws[split][Cin][8][Cout]
+  float* prow = ws + (long)blockIdx.x * 8 * Cin * Cout;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int ci = p0 + cq * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int co = co0 + wq * 32 + (lane & 31);
+      prow[((long)ci * 8 + t) * Cout + co] = acc[t][e];
+    }
+}
+
 // split reduction, fixed order.  Stage 1 (S > 16): rows r*16 .. r*16+15 summed in place into
 // row r*16 (E floats per row).
 __global__ void __launch_bounds__(256) convt_group_sum(float* ws, int S, long E) {
@@ -557,6 +643,8 @@ int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
   PCMS_CHECK_LAUNCH();
 }
 
+// (the 128-ci bf16 kernel keeps the 64-ci split count: half the workgroups, the same
+// partial rows -- doubling the splits doubled the partial-row traffic: slower at levels 1-3)
 static int convt_wgrad_splits(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs, int* vps) {
   const long M = (long)N * Din * Hin * Win;
   const int tiles = (Cout / 64) * (Cin / 64);
@@ -582,9 +670,15 @@ int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, floa
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
   if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
   int vps;
+  const bool ci128 = dtype == PCMS_BF16 && Cin % 128 == 0;
   const int splits = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps);
-  dim3 grid(splits, Cout / 64, Cin / 64);
-  if (dtype == PCMS_BF16) {
+  dim3 grid(splits, Cout / 64, Cin / (ci128 ? 128 : 64));
+  if (ci128) {
+    constexpr int lds = 10 * 64 * 128;
+    (void)hipFuncSetAttribute((const void*)convt_wgrad128_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(convt_wgrad128_kernel, grid, dim3(512), lds, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g,
+                       Cin, Cout, vps);
+  } else if (dtype == PCMS_BF16) {
     constexpr int lds = 9 * CW<bf16_t>::VB * 128;
     (void)hipFuncSetAttribute((const void*)convt_wgrad_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(convt_wgrad_kernel<bf16_t>, grid, dim3(512), lds, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g,
