@@ -363,20 +363,16 @@ __global__ void __launch_bounds__(256) rows_sum_kernel(const float* part, int ro
 // 8 lanes per voxel, 8 channels each (Cin = 64).  act 0: logits; 1: sigmoid(logits)
 // (UNet3D.predict, models/unet3d.py:298-318); 2: (sigmoid(logits) > thr) as 0 / 1
 // (UNet3D.inference, :320-344) -- the eval outputs leave the head kernel finished.
-template <typename T>
+template <typename T, bool NT>
 __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, float* logits,
                                 long nvox_per_n, int N, int ncls, int act, float thr) {
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7;
-  for (long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3; v < total;
-       v += ((long)gridDim.x * blockDim.x) >> 3) {
-    float x[8];
-    if constexpr (sizeof(T) == 2) {
-      load16<T>(a + v * 64 + sub * 8, x);
-    } else {
-      load16<T>(a + v * 64 + sub * 8, x);
-      load16<T>(a + v * 64 + sub * 8 + 4, x + 4);
-    }
+  auto load = [&](long v, float (&x)[8]) {
+    ld16<NT>(a + v * 64 + sub * 8, x);
+    if constexpr (sizeof(T) == 4) ld16<NT>(a + v * 64 + sub * 8 + 4, x + 4);
+  };
+  auto one = [&](long v, const float (&x)[8]) {
     const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
     for (int k = 0; k < ncls; ++k) {
       float s = 0.f;
@@ -394,12 +390,29 @@ __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, floa
         logits[(n * ncls + k) * nvox_per_n + vv] = o;
       }
     }
+  };
+  // two voxels per trip, both loads in flight
+  const long stride = ((long)gridDim.x * blockDim.x) >> 3;
+  long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
+  for (; v + stride < total; v += 2 * stride) {
+    float x0[8], x1[8];
+    load(v, x0);
+    load(v + stride, x1);
+    one(v, x0);
+    one(v + stride, x1);
+  }
+  for (; v < total; v += stride) {
+    float x0[8];
+    load(v, x0);
+    one(v, x0);
   }
 }
 
 // da[v, c] = sum_k dl[k, v] w[k, c]  (written);  per-block partials of dw[k, c] = sum_v dl a,
 // db[k] = sum_v dl
-template <typename T>
+// NT: non-temporal a / da streams (level-0 sized).  Two voxels per trip with both loads in
+// flight (accumulated in the same voxel order as one at a time: identical sums).
+template <typename T, bool NT>
 __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* dlogits, const float* w,
                                                        T* da, float* part, long nvox_per_n, int N, int ncls) {
   __shared__ float red[TPB / 64][4][65];
@@ -407,11 +420,12 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
   const int sub = threadIdx.x & 7, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float accw[4][8], accb[4];
   for (int k = 0; k < 4; ++k) { accb[k] = 0.f; for (int j = 0; j < 8; ++j) accw[k][j] = 0.f; }
-  for (long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3; v < total;
-       v += ((long)gridDim.x * blockDim.x) >> 3) {
-    float x[8], o[8];
-    load16<T>(a + v * 64 + sub * 8, x);
-    if constexpr (sizeof(T) == 4) load16<T>(a + v * 64 + sub * 8 + 4, x + 4);
+  auto load = [&](long v, float (&x)[8]) {
+    ld16<NT>(a + v * 64 + sub * 8, x);
+    if constexpr (sizeof(T) == 4) ld16<NT>(a + v * 64 + sub * 8 + 4, x + 4);
+  };
+  auto one = [&](long v, const float (&x)[8]) {
+    float o[8];
     const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = 0.f;
@@ -424,8 +438,22 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
       }
       if (sub == 0) accb[k] += g;
     }
-    store16<T>(da + v * 64 + sub * 8, o);
-    if constexpr (sizeof(T) == 4) store16<T>(da + v * 64 + sub * 8 + 4, o + 4);
+    st16<NT>(da + v * 64 + sub * 8, o);
+    if constexpr (sizeof(T) == 4) st16<NT>(da + v * 64 + sub * 8 + 4, o + 4);
+  };
+  const long stride = ((long)gridDim.x * blockDim.x) >> 3;
+  long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
+  for (; v + stride < total; v += 2 * stride) {
+    float x0[8], x1[8];
+    load(v, x0);
+    load(v + stride, x1);
+    one(v, x0);
+    one(v + stride, x1);
+  }
+  for (; v < total; v += stride) {
+    float x0[8];
+    load(v, x0);
+    one(v, x0);
   }
   // reduce accw over the 8 voxel-lanes of each wave that share `sub`
   for (int k = 0; k < ncls && k < 4; ++k) {
@@ -839,8 +867,13 @@ int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, floa
   if ((long)N * nvox_per_n >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   if (act < 0 || act > 2) return -1;
   const int grid = grid_for((long)N * nvox_per_n * 8, TPB);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
-  else hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
+  const bool nt = (long)N * nvox_per_n * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((nt ? head_fwd_kernel<bf16_t, true> : head_fwd_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0,
+                       s, (const bf16_t*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
+  else
+    hipLaunchKernelGGL((nt ? head_fwd_kernel<float, true> : head_fwd_kernel<float, false>), dim3(grid), dim3(TPB), 0, s,
+                       (const float*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -856,8 +889,13 @@ int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w
   if (ncls > 4 || ncls < 1) return -1;
   if (ws == nullptr) return -2;
   const int grid = head_bwd_rows((long)N * nvox_per_n);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, ws, nvox_per_n, N, ncls);
-  else hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)a, dlogits, w, (float*)da, ws, nvox_per_n, N, ncls);
+  const bool nt = (long)N * nvox_per_n * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((nt ? head_bwd_kernel<bf16_t, true> : head_bwd_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0,
+                       s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, ws, nvox_per_n, N, ncls);
+  else
+    hipLaunchKernelGGL((nt ? head_bwd_kernel<float, true> : head_bwd_kernel<float, false>), dim3(grid), dim3(TPB), 0, s,
+                       (const float*)a, dlogits, w, (float*)da, ws, nvox_per_n, N, ncls);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   float* sums = ws + (long)grid * ncls * 65;
