@@ -47,17 +47,28 @@ __global__ void __launch_bounds__(256) colsum2_kernel(const float* part, int row
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
-  if (c < C)
-    for (int r = blockIdx.y * 4 + rl; r < rows; r += kRB * 4) {
-      const float2 v = *reinterpret_cast<const float2*>(part + ((long)r * C + c) * 2);
-      s1 += (double)v.x;
-      if (cnt) {
-        const double n = (double)cnt[r];
-        s2 += (double)v.y + (n > 0.0 ? (double)v.x * (double)v.x / n : 0.0);
-      } else {
-        s2 += (double)v.y;
-      }
+  auto add = [&](const float2 v, int r) {
+    s1 += (double)v.x;
+    if (cnt) {
+      const double n = (double)cnt[r];
+      s2 += (double)v.y + (n > 0.0 ? (double)v.x * (double)v.x / n : 0.0);
+    } else {
+      s2 += (double)v.y;
     }
+  };
+  if (c < C) {
+    // rows r, r + 256, ... added in that order, four rows' loads in flight per trip
+    constexpr int RS = kRB * 4;
+    int r = blockIdx.y * 4 + rl;
+    for (; r + 3 * RS < rows; r += 4 * RS) {
+      float2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float2*>(part + ((long)(r + u * RS) * C + c) * 2);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u], r + u * RS);
+    }
+    for (; r < rows; r += RS) add(*reinterpret_cast<const float2*>(part + ((long)r * C + c) * 2), r);
+  }
   red[rl][cl][0] = s1;
   red[rl][cl][1] = s2;
   __syncthreads();
@@ -68,9 +79,19 @@ __global__ void __launch_bounds__(256) colsum2_kernel(const float* part, int row
   }
 }
 
+// the kRB row sums of channel c, added in row order; 16 rows' loads in flight at a time (one
+// thread per channel: a dependent load -> add chain made each finalize launch ~8 us)
 __device__ __forceinline__ void colsum_final(const double* ws, int C, int c, double& s1, double& s2) {
   s1 = 0.0; s2 = 0.0;
-  for (int r = 0; r < kRB; ++r) { s1 += ws[((long)r * C + c) * 2]; s2 += ws[((long)r * C + c) * 2 + 1]; }
+  const double2* p = reinterpret_cast<const double2*>(ws) + c;
+#pragma unroll
+  for (int r0 = 0; r0 < kRB; r0 += 16) {
+    double2 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = p[(long)(r0 + i) * C];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { s1 += v[i].x; s2 += v[i].y; }
+  }
 }
 
 // Stage 2: -> mean/invstd/scale/shift (+ running stats when training)
