@@ -1088,7 +1088,7 @@ constexpr int kBgDummy = 1024;
 constexpr int kBgStage = 64 * 128;                                        // per-wave store slice
 constexpr int kBgRed = 4 * 64 * 3 * 4;                                    // BN moments
 constexpr int kBgLds = 2 * kBgBuf + kBgDummy + 4 * kBgStage + kBgRed + 64 * 4;  // + bias
-constexpr int kBgDist = 8;                 // B prefetch distance (taps); (Dist + 1) | 27
+constexpr int kBgDist = 2;                 // B prefetch distance (taps); (Dist + 1) | 27
 constexpr int kBgEpiStores = kBgMT * 2;    // 16-B stores per wave and box
 static_assert(27 % (kBgDist + 1) == 0, "B ring index must continue across chunks");
 static_assert(kBgLds <= 160 * 1024, "LDS");
