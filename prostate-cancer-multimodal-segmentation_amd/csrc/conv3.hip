@@ -1058,21 +1058,24 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
 
 // ------------------------------------------------------------------------------------
 // Big-box forward / dgrad (bf16; the level-0/1 hot case: D % 8 == H % 8 == 0, W % 16 == 0,
-// input channels in 16-channel chunks), PERSISTENT: one 4-wave workgroup per CU, one grid of
+// input channels in 16-channel chunks), PERSISTENT: one 8-wave workgroup per CU, one grid of
 // at most #CU workgroups; workgroup (slot, cob) computes 8 x 8 x 16 = 1024-voxel boxes
-// slot, slot + nslot, ... for its 64 output channels.  Wave w owns voxel rows
-// [256 w, 256 w + 256) = 8 M-tiles, so every B fragment (weights, L2-resident) feeds 8 MFMAs.
+// slot, slot + nslot, ... for its 64 output channels.  Wave w = (M-group mg = w & 3, N-tile
+// nt = w >> 2) owns voxel rows [256 mg, 256 mg + 256) = 8 M-tiles and the output channels of
+// parity nt, so every B fragment (weights, L2-resident) feeds 8 MFMAs and the two waves of a
+// SIMD overlap one's operand waits with the other's MFMAs.
 // The 10 x 10 x 18 halo of a chunk (32-B rows; the two 16-B halves swapped on odd row octets,
 // so 16 consecutive rows hit 16 distinct bank groups) is double-buffered: the next chunk's
 // halo -- the NEXT BOX's first chunk during a box's last chunk -- streams in by buffer
-// LDS-DMA, one piece per thread and tap over the first 15 taps, and A fragments of tap t + 1
-// are read while tap t's 16 MFMAs run; B loads run Dist taps ahead across chunk and box
+// LDS-DMA, one piece per thread and tap over the first 8 taps, and A fragments of tap t + 1
+// are read while tap t's 8 MFMAs run; B loads run Dist taps ahead across chunk and box
 // boundaries.  So only the first box of a workgroup waits for its operands; every later box
-// starts on a landed halo.  Epilogue per box: + bias, bf16 pairs staged through a wave-private
-// 8 KiB LDS slice (two M-tiles at a time) and written back as 16-B stores of whole 128-B
-// channel rows (32 store instructions per wave and box, issued without waiting: the B waits
-// of the next box's first taps count them).  BatchNorm partials: per wave a running Chan
-// merge over its boxes (count, mean, M2 per channel); one stats row per slot at the end.
+// starts on a landed halo.  Epilogue per box: + bias, bf16 channels staged through the
+// M-group's 8 KiB LDS slice (two M-tiles at a time, the pair's even / odd channels) and
+// written back as 16-B stores of whole 128-B channel rows (16 store instructions per wave and
+// box, issued without waiting: the B waits of the next box's first taps count them).
+// BatchNorm partials: per (M-group, channel) a running Chan merge over the boxes (count,
+// mean, M2); one stats row per slot at the end.
 // ------------------------------------------------------------------------------------
 constexpr int kBgThreads = 512;  // 8 waves = 4 M-groups x 2 N-tiles, two waves per SIMD
 constexpr int kBgHH = 10, kBgHW = 18;
@@ -1085,7 +1088,7 @@ constexpr int kBgPieces = (2 * kBgHalo + kBgThreads - 1) / kBgThreads;    // DMA
 // issues the same count; a buffer holds rows up to wave 0's last piece
 constexpr int kBgBuf = ((kBgPieces - 1) * kBgThreads + 64) * 16;
 constexpr int kBgDummy = 1024;
-constexpr int kBgStage = 64 * 128;                                        // per-wave store slice
+constexpr int kBgStage = 64 * 128;                                        // per-M-group store slice
 constexpr int kBgRed = 4 * 64 * 3 * 4;                                    // BN moments
 constexpr int kBgLds = 2 * kBgBuf + kBgDummy + 4 * kBgStage + kBgRed + 64 * 4;  // + bias
 constexpr int kBgDist = 2;                 // B prefetch distance (taps); (Dist + 1) | 27
