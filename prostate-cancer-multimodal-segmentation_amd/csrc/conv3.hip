@@ -122,41 +122,50 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     if constexpr (!kF32) {
       // bf16: the A fragments roll through one register set: right after M-tile mt's MFMAs of
       // tap t its fragment of tap t + 1 is read (15 MFMAs of slack before its first use)
-      // instead of one read -> wait -> two MFMAs per fragment
+      // instead of one read -> wait -> two MFMAs per fragment.  B: two register sets, tap t + 1
+      // loaded while tap t computes (a third set, two taps ahead, pushed the kernel past 256
+      // VGPRs into spills with a reload inside this loop); taps walked two (kd, kh) rows per
+      // trip so every set index is a compile-time constant.
       s16x8_t a[2][4];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) a[ks][mt] = lds_a(lds, hb[mt], ks, hsel, (T*)nullptr);
-      for (int kdh = 0; kdh < 9; ++kdh) {
-        // row bases from an opaque copy: the fragment addresses are recomputed per kdh rather
+      auto tap_step = [&](int tap, int set, const int (&hbk)[4]) {
+        load_b(bset[set ^ 1], min(tap + 1, 26));
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
+        const int tn = tap + 1 < 27 ? tap + 1 : 0;
+        const int offn = ((tn / 9) * HH + (tn / 3) % 3) * HW + tn % 3;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[ks][mt], bset[set][nt][ks], acc[mt][nt]);
+            a[ks][mt] = lds_a(lds, hbk[mt] + offn, ks, hsel, (T*)nullptr);
+          }
+        // (the scheduler would otherwise sink all eight reads below the last MFMA)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+      };
+      for (int kdh = 0; kdh < 8; kdh += 2) {
+        // row bases from an opaque copy: the fragment addresses are recomputed per trip rather
         // than hoisted out of the loops (and spilled)
         int hbk[4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int tap = kdh * 3 + kw;
-          // (past the last tap: harmless re-reads, so every kdh iteration is alike)
-          load_b(bset[(kw + 2) % 3], min(tap + 2, 26));
-          __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
-          const int tn = tap + 1 < 27 ? tap + 1 : 0;
-          const int offn = ((tn / 9) * HH + (tn / 3) % 3) * HW + tn % 3;
+        for (int j = 0; j < 6; ++j) tap_step(kdh * 3 + j, j & 1, hbk);
+      }
+      {
+        int hbk[4];
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
+        for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-              for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[ks][mt], bset[kw][nt][ks], acc[mt][nt]);
-              a[ks][mt] = lds_a(lds, hbk[mt] + offn, ks, hsel, (T*)nullptr);
-            }
-          // (the scheduler would otherwise sink all eight reads below the last MFMA)
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-          }
-        }
+        for (int j = 0; j < 3; ++j) tap_step(24 + j, j & 1, hbk);
       }
       continue;
     }
