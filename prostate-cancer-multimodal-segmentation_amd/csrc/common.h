@@ -137,19 +137,24 @@ __device__ __forceinline__ i32x4_t buffer_desc(const void* base, uint32_t num_by
 // these with explicit s_waitcnt vmcnt(N) + a barrier before reading the data.
 // Wait states inside the string (the compiler pads nothing in it): s_nop 4 first, for an
 // soffset / descriptor SGPR fresh from v_readfirstlane (VALU SGPR write -> VMEM read), and
-// one state between the M0 write and the LDS-DMA that reads it.
+// one state between the M0 write and the LDS-DMA that reads it.  M0 is compiler-reserved
+// and not preserved around an asm statement, so the statement saves and restores it.
 __device__ __forceinline__ void dma16(i32x4_t rsrc, uint32_t lds_base, uint32_t voff, uint32_t soff) {
-  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               :
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
                : "s"(lds_base), "v"(voff), "s"(rsrc), "s"(soff)
-               : "memory", "m0");
+               : "memory");
 }
 // the same with the non-temporal policy (data read once: streamed past the caches)
 __device__ __forceinline__ void dma16_nt(i32x4_t rsrc, uint32_t lds_base, uint32_t voff, uint32_t soff) {
-  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen nt lds"
-               :
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
                : "s"(lds_base), "v"(voff), "s"(rsrc), "s"(soff)
-               : "memory", "m0");
+               : "memory");
 }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
