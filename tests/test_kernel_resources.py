@@ -1,0 +1,48 @@
+"""Register / scratch resources of the hand-pipelined kernels (CPU: device assembly only).
+
+The big-box conv, the stem kernels and the bf16 general conv count their vector-memory
+operations by hand (LDS-DMA from inline asm + counted ``s_waitcnt vmcnt``); a register spill
+inside such a loop adds scratch loads whose compiler-inserted waits drain the pipeline.  The
+kernels must therefore fit their VGPR budget with no scratch (private segment 0)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "prostate-cancer-multimodal-segmentation_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+KERNELS = {
+    "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E"],
+    "stem.hip": ["stem_fwd_direct_kernelILi2ELi3E", "stem_fwd_direct_kernelILi3ELi2E", "stem_wgrad_stream_kernel"],
+}
+
+
+def _meta(src, tmp):
+    out = os.path.join(tmp, os.path.basename(src) + ".s")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{REPO}/include", "-Wno-unused-function",
+                    "-Wno-inline-asm", "--cuda-device-only", "-S", "-o", out, src], check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    s = open(out).read()
+    meta = {}
+    for m in re.finditer(r"\.name:\s+(\S+)", s):
+        blk = s[m.start():m.start() + 2000]
+        priv = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+        vgpr = re.search(r"\.vgpr_count:\s+(\d+)", blk)
+        meta[m.group(1)] = (int(priv.group(1)), int(vgpr.group(1)))
+    return meta
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) or shutil.which("bash") is None, reason="hipcc not available")
+@pytest.mark.parametrize("src", sorted(KERNELS))
+def test_pipelined_kernels_do_not_spill(src, tmp_path):
+    meta = _meta(os.path.join(CSRC, src), str(tmp_path))
+    for key in KERNELS[src]:
+        hits = [(n, v) for n, v in meta.items() if key in n]
+        assert hits, f"{key} not found in {src}"
+        for name, (priv, vgpr) in hits:
+            assert priv == 0, f"{name}: {priv} B of scratch (spills) at {vgpr} VGPRs"
+            assert vgpr <= 256, f"{name}: {vgpr} VGPRs (two waves per SIMD need <= 256)"
