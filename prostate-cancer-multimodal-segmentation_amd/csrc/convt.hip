@@ -144,7 +144,8 @@ constexpr int kCDPieces = kCDStage / 16 / 512;                    // 6 per threa
 
 __device__ __forceinline__ int cd_slot(int row, int slot) { return row * 128 + ((slot ^ (row & 7)) << 4); }
 
-// NT (forward): non-temporal output stores, for outputs far larger than the Infinity Cache
+// NT: non-temporal streams for tensors far larger than the Infinity Cache (forward: the
+// output stores; dgrad: the dout loads)
 template <bool FWD, bool NT = false>
 __global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, const bf16_t* wpk, const float* bias,
                                                            bf16_t* out, UpGeom g, int Cin, int Cout) {
@@ -189,8 +190,11 @@ __global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, 
       const int t = st % 8, kc = st / 8;
       const long dt = tap_delta(g, t);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        stg[j] = *reinterpret_cast<const u32x4_t*>(a_src + (arow[j] + dt) * Ka + kc * 64 + aslot[j] * 8);
+      for (int j = 0; j < 4; ++j) {
+        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(a_src + (arow[j] + dt) * Ka + kc * 64 + aslot[j] * 8);
+        if constexpr (NT) stg[j] = __builtin_nontemporal_load(src);
+        else stg[j] = *src;
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         stg[4 + j] = *reinterpret_cast<const u32x4_t*>(wpk + (long)brow[j] * K + t * Cout + kc * 64 + bslot[j] * 8);
@@ -629,9 +633,10 @@ int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
   if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
   const long M = (long)N * Din * Hin * Win;
   if (dtype == PCMS_BF16 && Cin % kCDN == 0 && Cout % 64 == 0) {
-    (void)hipFuncSetAttribute((const void*)convt_lds_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * kCDStage);
-    hipLaunchKernelGGL(convt_lds_kernel<false>, dim3(cdiv(M, kCDM), Cin / kCDN), dim3(512), 2 * kCDStage, s,
+    const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;  // dout
+    auto kern = nt ? convt_lds_kernel<false, true> : convt_lds_kernel<false, false>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kCDStage);
+    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), Cin / kCDN), dim3(512), 2 * kCDStage, s,
                        (const bf16_t*)dout, (const bf16_t*)wpack_d, nullptr, (bf16_t*)dx, g, Cin, Cout);
     PCMS_CHECK_LAUNCH();
   }
