@@ -389,6 +389,8 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad_kernel(const T* x, const T
 // level 0, Cin = 128: dout -- 268 MB -- read once, not twice).  x tile [VB][128] as two
 // [VB][64] halves; 8 waves = (ci quarter cq, co half), each all 8 taps (8 accumulators):
 // per 16 voxels one x fragment and 8 dout fragments feed 8 MFMAs.
+// NT: non-temporal loads (dout far larger than the Infinity Cache)
+template <bool NT>
 __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout, float* ws,
                                                                UpGeom g, int Cin, int Cout, int vox_per_split) {
   constexpr int VB = 64, ROW = 128, PPR = 8;
@@ -432,7 +434,8 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
         const long m = std::min<long>(vb + v, vend - 1);
         src = dout + child_vox(g, m, t) * Cout + co0 + (rem % PPR) * 8;
       }
-      stg[i] = *reinterpret_cast<const u32x4_t*>(src);
+      stg[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src))
+                  : *reinterpret_cast<const u32x4_t*>(src);
       if (vb + v >= vend) stg[i] = (u32x4_t){0u, 0u, 0u, 0u};
     }
     __syncthreads();  // every wave is done with the previous block's tiles
@@ -680,8 +683,10 @@ int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, floa
   dim3 grid(splits, Cout / 64, Cin / (ci128 ? 128 : 64));
   if (ci128) {
     constexpr int lds = 10 * 64 * 128;
-    (void)hipFuncSetAttribute((const void*)convt_wgrad128_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(convt_wgrad128_kernel, grid, dim3(512), lds, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g,
+    const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;
+    auto kern = nt ? convt_wgrad128_kernel<true> : convt_wgrad128_kernel<false>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, grid, dim3(512), lds, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g,
                        Cin, Cout, vps);
   } else if (dtype == PCMS_BF16) {
     constexpr int lds = 9 * CW<bf16_t>::VB * 128;
