@@ -1029,18 +1029,21 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
   for (int i = 0; i < 27; ++i) {
     const int q4 = threadIdx.x + i * 256, run = q4 / 216, q = q4 % 216;
     const long idx = off + ((long)(j0 + run) * Cin + chunk * 32) * 27 + 4 * q;
-    f32x4_t pv = *reinterpret_cast<const f32x4_t*>(P + idx), gv = *reinterpret_cast<const f32x4_t*>(Gr + idx);
-    f32x4_t mv = *reinterpret_cast<const f32x4_t*>(Mo + idx), vv = *reinterpret_cast<const f32x4_t*>(Vo + idx);
+    // the fp32 master / gradient / moment streams (1.4 GB per step) bypass the caches
+    f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(P + idx));
+    f32x4_t gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Gr + idx));
+    f32x4_t mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Mo + idx));
+    f32x4_t vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Vo + idx));
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float pk = pv[k], gk = gv[k], mk = mv[k], vk = vv[k];
       adam_update(pk, gk, mk, vk, c, s);
       pv[k] = pk; gv[k] = gk; mv[k] = mk; vv[k] = vk;
     }
-    *reinterpret_cast<f32x4_t*>(P + idx) = pv;
-    *reinterpret_cast<f32x4_t*>(Mo + idx) = mv;
-    *reinterpret_cast<f32x4_t*>(Vo + idx) = vv;
-    if (s != 1.f) *reinterpret_cast<f32x4_t*>(Gr + idx) = gv;
+    __builtin_nontemporal_store(pv, reinterpret_cast<f32x4_t*>(P + idx));
+    __builtin_nontemporal_store(mv, reinterpret_cast<f32x4_t*>(Mo + idx));
+    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4_t*>(Vo + idx));
+    if (s != 1.f) __builtin_nontemporal_store(gv, reinterpret_cast<f32x4_t*>(Gr + idx));
     uint2 o;
     o.x = pack_bf16x2(pv[0], pv[1]);
     o.y = pack_bf16x2(pv[2], pv[3]);
