@@ -135,7 +135,10 @@ __global__ void __launch_bounds__(256) convt_dgrad_kernel(const T* dout, const T
 // GEMM columns; per stage (a 64-channel chunk of K) it stages the 256 A rows (full 128-B
 // rows, 8 lanes per row) and the 128 x 64 weight tile into LDS (16-B slots XOR-swizzled by
 // row & 7), register-prefetching the next stage while 8 waves (32 voxels x 128 columns, 4
-// N-tiles) run their MFMAs.  Columns are channel pairs (packed bf16x2 stores).
+// N-tiles) run their MFMAs.  Columns are channel pairs (packed bf16x2 stores).  One 48-KiB
+// stage buffer and <= 128 VGPRs: two workgroups per CU hide each other's staging and
+// epilogue (vs a double buffer at one workgroup per CU: level-0 forward 164 -> 125 us,
+// convT dgrad 0.238 -> 0.222 ms/step).
 //   FWD:   A = x[m][Cin],                 K = Cin,      columns q = (t, co), out[child(m,t)][co] + b
 //   dgrad: A = dout[child(m, t)][Cout],   K = 8 Cout,   columns = ci,        dx[m][ci]
 constexpr int kCDM = 256, kCDN = 128;
@@ -147,7 +150,7 @@ __device__ __forceinline__ int cd_slot(int row, int slot) { return row * 128 + (
 // NT: non-temporal streams for tensors far larger than the Infinity Cache (forward: the
 // output stores; dgrad: the dout loads)
 template <bool FWD, bool NT = false>
-__global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, const bf16_t* wpk, const float* bias,
+__global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, const bf16_t* wpk, const float* bias,
                                                            bf16_t* out, UpGeom g, int Cin, int Cout) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r_lane = lane & 31, hsel = lane >> 5;
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, 
   store(lds);
   __syncthreads();
   for (int st = 0; st < nst; ++st) {
-    const char* buf = lds + (st & 1) * kCDStage;
+    const char* buf = lds;
     if (st + 1 < nst) load(st + 1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -227,7 +230,10 @@ __global__ void __launch_bounds__(512, 1) convt_lds_kernel(const bf16_t* a_src, 
         acc[nt] = mfma(a, b, acc[nt]);
       }
     }
-    if (st + 1 < nst) store(lds + ((st + 1) & 1) * kCDStage);
+    if (st + 1 < nst) {
+      __syncthreads();
+      store(lds);
+    }
     __syncthreads();
   }
   if constexpr (FWD) {
@@ -616,8 +622,8 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
   if (dtype == PCMS_BF16 && Cin % 64 == 0 && (8 * Cout) % kCDN == 0) {
     const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;
     auto kern = nt ? convt_lds_kernel<true, true> : convt_lds_kernel<true, false>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kCDStage);
-    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), 8 * Cout / kCDN), dim3(512), 2 * kCDStage, s,
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);
+    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), 8 * Cout / kCDN), dim3(512), kCDStage, s,
                        (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
     PCMS_CHECK_LAUNCH();
   }
@@ -638,8 +644,8 @@ int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
   if (dtype == PCMS_BF16 && Cin % kCDN == 0 && Cout % 64 == 0) {
     const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;  // dout
     auto kern = nt ? convt_lds_kernel<false, true> : convt_lds_kernel<false, false>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kCDStage);
-    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), Cin / kCDN), dim3(512), 2 * kCDStage, s,
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);
+    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), Cin / kCDN), dim3(512), kCDStage, s,
                        (const bf16_t*)dout, (const bf16_t*)wpack_d, nullptr, (bf16_t*)dx, g, Cin, Cout);
     PCMS_CHECK_LAUNCH();
   }

@@ -3,7 +3,8 @@
 The big-box conv, the stem kernels and the bf16 general conv count their vector-memory
 operations by hand (LDS-DMA from inline asm + counted ``s_waitcnt vmcnt``); a register spill
 inside such a loop adds scratch loads whose compiler-inserted waits drain the pipeline.  The
-kernels must therefore fit their VGPR budget with no scratch (private segment 0)."""
+kernels must therefore fit their VGPR budget with no scratch (private segment 0).  The
+ConvTranspose LDS kernel relies on two 512-thread workgroups per CU: <= 128 VGPRs."""
 import os
 import re
 import shutil
@@ -18,7 +19,9 @@ HIPCC = "/opt/rocm/bin/hipcc"
 KERNELS = {
     "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E"],
     "stem.hip": ["stem_fwd_direct_kernelILi2ELi3E", "stem_fwd_direct_kernelILi3ELi2E", "stem_wgrad_stream_kernel"],
+    "convt.hip": ["convt_lds_kernel"],
 }
+VGPR_BUDGET = {"convt_lds_kernel": 128}
 
 
 def _meta(src, tmp):
@@ -45,4 +48,5 @@ def test_pipelined_kernels_do_not_spill(src, tmp_path):
         assert hits, f"{key} not found in {src}"
         for name, (priv, vgpr) in hits:
             assert priv == 0, f"{name}: {priv} B of scratch (spills) at {vgpr} VGPRs"
-            assert vgpr <= 256, f"{name}: {vgpr} VGPRs (two waves per SIMD need <= 256)"
+            budget = VGPR_BUDGET.get(key, 256)
+            assert vgpr <= budget, f"{name}: {vgpr} VGPRs (budget {budget}: its waves per SIMD)"
