@@ -119,6 +119,12 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
                    int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
 int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
+/* the same with an fp32 workspace of pcms_convt_dgrad_ws_floats(...) floats (0: none needed):
+ * small grids (the deepest levels) split the 8 Cout reduction into K slabs summed in a fixed
+ * order; ws may be NULL (no split)                                                        */
+int pcms_convt_dgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout);
+int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* dx, float* ws,
+                        int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
 /* dw += ConvTranspose3d weight gradient; ws: pcms_convt_wgrad_ws_floats(...) fp32 (one
  * [Cin][8][Cout] partial row per voxel split, summed in a fixed order)                   */
 int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs);

@@ -48,6 +48,8 @@ SIGNATURES = {
     "pcms_convt_pack": "ippiiis",
     "pcms_convt_fwd": "ippppiiiiiiiiis",
     "pcms_convt_dgrad": "ipppiiiiiiiiis",
+    "pcms_convt_dgrad_ws_floats": "iiiiii",
+    "pcms_convt_dgrad_ws": "ippppiiiiiiiiis",
     "pcms_convt_wgrad_ws_floats": "iiiiiii",
     "pcms_convt_wgrad": "ippppiiiiiiiiiis",
     "pcms_box_channel_sum_ws_floats": "iiiiii",

@@ -149,16 +149,18 @@ __device__ __forceinline__ int cd_slot(int row, int slot) { return row * 128 + (
 
 // NT: non-temporal streams for tensors far larger than the Infinity Cache (forward: the
 // output stores; dgrad: the dout loads)
-template <bool FWD, bool NT = false>
+// SPLIT (dgrad with few workgroups): blockIdx.z takes an equal share of the K stages and
+// writes fp32 partials ws[z][m][ci], summed in z order by convt_dgrad_reduce.
+template <bool FWD, bool NT = false, bool SPLIT = false>
 __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, const bf16_t* wpk, const float* bias,
-                                                           bf16_t* out, UpGeom g, int Cin, int Cout) {
+                                                           bf16_t* out, UpGeom g, int Cin, int Cout, float* ws) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r_lane = lane & 31, hsel = lane >> 5;
   const long M = (long)g.N * g.Din * g.Hin * g.Win;
   const long m0 = (long)blockIdx.x * kCDM;
   const int q0 = blockIdx.y * kCDN;
   const int K = FWD ? Cin : 8 * Cout, Ka = FWD ? Cin : Cout;  // K, A row pitch
-  const int nst = K / 64;
+  const int nst = K / 64 / (SPLIT ? (int)gridDim.z : 1), st0 = SPLIT ? (int)blockIdx.z * nst : 0;
   // staging pieces of this thread: j < 4: A rows (256 x 8 slots), j >= 4: weight rows (128 x 8)
   long arow[4];  // FWD: input voxel; dgrad: its tap-0 child voxel
   int aslot[4], aoff[4];
@@ -215,12 +217,12 @@ __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, 
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
   const int arw = wave * 32 + r_lane;
-  load(0);
+  load(st0);
   store(lds);
   __syncthreads();
-  for (int st = 0; st < nst; ++st) {
+  for (int st = st0; st < st0 + nst; ++st) {
     const char* buf = lds;
-    if (st + 1 < nst) load(st + 1);
+    if (st + 1 < st0 + nst) load(st + 1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const s16x8_t a = *reinterpret_cast<const s16x8_t*>(buf + cd_slot(arw, ks * 2 + hsel));
@@ -230,7 +232,7 @@ __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, 
         acc[nt] = mfma(a, b, acc[nt]);
       }
     }
-    if (st + 1 < nst) {
+    if (st + 1 < st0 + nst) {
       __syncthreads();
       store(lds);
     }
@@ -261,6 +263,15 @@ __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, 
         else *dst = v;
       }
     }
+  } else if constexpr (SPLIT) {
+    float* part = ws + (long)blockIdx.z * M * Cin + q0 + 2 * r_lane;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const long m = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+      if (m >= M) continue;
+      *reinterpret_cast<f32x2_t*>(part + m * Cin) = f32x2_t{acc[0][e], acc[1][e]};
+      *reinterpret_cast<f32x2_t*>(part + m * Cin + 64) = f32x2_t{acc[2][e], acc[3][e]};
+    }
   } else {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -271,6 +282,26 @@ __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, 
       *reinterpret_cast<uint32_t*>(row + 64) = pack_bf16x2(acc[2][e], acc[3][e]);
     }
   }
+}
+
+// dx[m][ci] = bf16(sum over z = 0..S-1 of ws[z][m][ci]), z in order; 4 elements per thread
+__global__ void __launch_bounds__(256) convt_dgrad_reduce(const float* ws, int S, long E, bf16_t* dx) {
+  const long i = (blockIdx.x * 256L + threadIdx.x) * 4;
+  if (i >= E) return;
+  f32x4_t v[16];
+  f32x4_t a = *reinterpret_cast<const f32x4_t*>(ws + i);
+  for (int z0 = 1; z0 < S; z0 += 16) {
+    const int nz = std::min(16, S - z0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < nz) v[j] = *reinterpret_cast<const f32x4_t*>(ws + (z0 + j) * E + i);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < nz) a += v[j];
+  }
+  uint32_t* d = reinterpret_cast<uint32_t*>(dx + i);
+  d[0] = pack_bf16x2(a[0], a[1]);
+  d[1] = pack_bf16x2(a[2], a[3]);
 }
 
 // ---- weight gradient: C[p = ci][q = (t, co)] over K = input voxels ----
@@ -624,7 +655,7 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
     auto kern = nt ? convt_lds_kernel<true, true> : convt_lds_kernel<true, false>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);
     hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), 8 * Cout / kCDN), dim3(512), kCDStage, s,
-                       (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
+                       (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout, nullptr);
     PCMS_CHECK_LAUNCH();
   }
   dim3 grid(cdiv(M, 128), 8 * Cout / 64);
@@ -635,18 +666,51 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
   PCMS_CHECK_LAUNCH();
 }
 
+// K splits of the bf16 LDS dgrad: doubled while the grid is under 256 workgroups (level 4:
+// 16 workgroups x 64 stages -> 256 x 4), each a power of two dividing the 8 Cout / 64 stages
+static int convt_dgrad_splits(long M, int Cin, int Cout) {
+  if (Cin % kCDN || Cout % 64) return 1;
+  const long wgs = cdiv(M, kCDM) * (Cin / kCDN);
+  const int nst = 8 * Cout / 64;
+  int S = 1;
+  while (wgs * S < 256 && S < 16 && nst % (2 * S) == 0) S *= 2;
+  return S;
+}
+
+int pcms_convt_dgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout) {
+  const long M = (long)N * Din * Hin * Win, S = convt_dgrad_splits(M, Cin, Cout);
+  const long f = S > 1 ? S * M * Cin : 0;
+  return f >= (1L << 31) ? -7 : (int)f;
+}
+
 int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
+  return pcms_convt_dgrad_ws(dtype, dout, wpack_d, dx, nullptr, N, Din, Hin, Win, Cin, Cout, Do, Ho, Wo, s);
+}
+
+int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* dx, float* ws,
+                        int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
   if (Cin % 64 || Cout % 16) return -1;
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
   if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
   const long M = (long)N * Din * Hin * Win;
   if (dtype == PCMS_BF16 && Cin % kCDN == 0 && Cout % 64 == 0) {
     const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;  // dout
+    const int S = ws ? convt_dgrad_splits(M, Cin, Cout) : 1;
+    if (S > 1) {
+      auto kern = convt_lds_kernel<false, false, true>;
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);
+      hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), Cin / kCDN, S), dim3(512), kCDStage, s,
+                         (const bf16_t*)dout, (const bf16_t*)wpack_d, nullptr, (bf16_t*)dx, g, Cin, Cout, ws);
+      const long E = M * Cin;
+      hipLaunchKernelGGL(convt_dgrad_reduce, dim3((unsigned)cdiv(E / 4, 256)), dim3(256), 0, s, (const float*)ws, S,
+                         E, (bf16_t*)dx);
+      PCMS_CHECK_LAUNCH();
+    }
     auto kern = nt ? convt_lds_kernel<false, true> : convt_lds_kernel<false, false>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);
     hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), Cin / kCDN), dim3(512), kCDStage, s,
-                       (const bf16_t*)dout, (const bf16_t*)wpack_d, nullptr, (bf16_t*)dx, g, Cin, Cout);
+                       (const bf16_t*)dout, (const bf16_t*)wpack_d, nullptr, (bf16_t*)dx, g, Cin, Cout, nullptr);
     PCMS_CHECK_LAUNCH();
   }
   dim3 grid(cdiv(M, 128), Cin / 64);

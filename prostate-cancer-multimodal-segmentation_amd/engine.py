@@ -417,6 +417,9 @@ class UNetEngine:
         self.stem_sup = query("pcms_stem_supported", N, D, H, W) if self.stem_fast else 0
         ctws = [query("pcms_convt_wgrad_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels, 512)
                 for i, up in enumerate(self.ups)]
+        # the ConvT dgrad's K slabs share it (the weight gradient has reduced it by then)
+        ctws += [query("pcms_convt_dgrad_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels)
+                 for i, up in enumerate(self.ups)]
         b["ctws"] = torch.empty(max(ctws), dtype=torch.float32, device=dev)
         self.bufs = b
         self.buf_key = key
@@ -615,8 +618,8 @@ class UNetEngine:
                  2 * S[l + 1][0], 2 * S[l + 1][1], 2 * S[l + 1][2])
             self._grads_done(f"up{i + 1}")
             gnext = b["gx4"] if i == 0 else b[f"gA{l + 1}"]
-            call("pcms_convt_dgrad", self.code, gu, dpack, gnext, N, *S[l + 1], up.in_channels, up.out_channels,
-                 *S[l])
+            call("pcms_convt_dgrad_ws", self.code, gu, dpack, gnext, b["ctws"], N, *S[l + 1], up.in_channels,
+                 up.out_channels, *S[l])
             g = gnext
         # encoder, deepest first; gx{l} holds the skip gradient already (l < 4)
         for l in reversed(range(5)):

@@ -360,7 +360,8 @@ def test_maxpool_fwd_bwd(dt, code, tol):
 
 @pytest.mark.parametrize("dt,code,tol", DTS)
 @pytest.mark.parametrize("Sin,Sout,cin,cout", [((4, 4, 2), (8, 8, 4), 128, 64), ((2, 2, 3), (5, 4, 7), 128, 64),
-                                               ((8, 8, 6), (16, 16, 12), 256, 128)])  # > 1 tile, 2 co chunks
+                                               ((8, 8, 6), (16, 16, 12), 256, 128),  # > 1 tile, 2 co chunks
+                                               ((8, 8, 4), (16, 16, 8), 1024, 512)])  # level 4 (split dgrad)
 def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     L = _lib()
     g = torch.Generator().manual_seed(9)
@@ -386,6 +387,12 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     god = ndhwc(gout).to(DEV)
     dx = torch.empty(N, *Sin, cin, dtype=dt, device=DEV)
     L.call("pcms_convt_dgrad", code, god, dp, dx, N, *Sin, cin, cout, *Sout)
+    # K-split dgrad (fp32 slabs in ws, summed in a fixed order) where the grid is small
+    nws = L.query("pcms_convt_dgrad_ws_floats", N, *Sin, cin, cout)
+    assert nws > 0 or cin % 128, "small grids split the dgrad"
+    dxs = torch.full_like(dx, float("nan"))
+    dws = torch.full((max(nws, 1),), float("nan"), device=DEV)
+    L.call("pcms_convt_dgrad_ws", code, god, dp, dxs, dws, N, *Sin, cin, cout, *Sout)
     dw = torch.zeros(cin, cout, 2, 2, 2, device=DEV)
     ws = torch.empty(L.query("pcms_convt_wgrad_ws_floats", N, *Sin, cin, cout, 64), device=DEV)
     L.call("pcms_convt_wgrad", code, ndhwc(x).to(DEV), god, dw, ws, N, *Sin, cin, cout, *Sout, 64)
@@ -397,6 +404,7 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     torch.cuda.synchronize()
     close(ncdhw(out.cpu()), up.detach(), tol, "convT fwd (+pad)")
     close(ncdhw(dx.cpu()), xr.grad, tol, "convT dgrad")
+    close(ncdhw(dxs.cpu()), xr.grad, tol, "convT dgrad (K-split)")
     close(dw.cpu(), wr.grad, 1e-4 if code else 2e-5, "convT wgrad")
     close(db.cpu(), br.grad, 1e-4 if code else 1e-5, "convT bias grad")
 

@@ -23,7 +23,7 @@ def flops(name, a):
         return 2 * 27 * 5 * 64 * a[5] * a[6] * a[7] * a[8]
     if name == "pcms_stem_wgrad":
         return 2 * 27 * 5 * 64 * a[5] * a[6] * a[7] * a[8]
-    if name in ("pcms_convt_fwd", "pcms_convt_wgrad"):
+    if name in ("pcms_convt_fwd", "pcms_convt_wgrad", "pcms_convt_dgrad_ws"):
         return 2 * 8 * a[9] * a[10] * a[5] * a[6] * a[7] * a[8]
     if name == "pcms_convt_dgrad":
         return 2 * 8 * a[8] * a[9] * a[4] * a[5] * a[6] * a[7]
@@ -37,7 +37,7 @@ def desc(name, a):
         return f"{a[2]}+{a[4]}->{a[12]} {a[9]}x{a[10]}x{a[11]}"
     if name == "pcms_convt_dgrad":
         return f"{a[8]}->{a[9]} {a[5]}x{a[6]}x{a[7]}"
-    if name in ("pcms_convt_fwd", "pcms_convt_wgrad"):
+    if name in ("pcms_convt_fwd", "pcms_convt_wgrad", "pcms_convt_dgrad_ws"):
         return f"{a[9]}->{a[10]} {a[6]}x{a[7]}x{a[8]}"
     return ""
 
