@@ -157,8 +157,21 @@ __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, 
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r_lane = lane & 31, hsel = lane >> 5;
   const long M = (long)g.N * g.Din * g.Hin * g.Win;
-  const long m0 = (long)blockIdx.x * kCDM;
-  const int q0 = blockIdx.y * kCDN;
+  // forward on a 1-D grid: the column blocks of one voxel tile run back to back on one XCD
+  // (workgroups are dealt to the 8 XCDs round-robin), so its A rows are re-read from that L2
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (FWD && gridDim.y == 1) {
+    const int ny = 8 * Cout / kCDN, b = blockIdx.x;
+    if ((gridDim.x / ny) % 8 == 0) {
+      by = (b >> 3) % ny;
+      bx = (b >> 3) / ny * 8 + (b & 7);
+    } else {
+      by = b % ny;
+      bx = b / ny;
+    }
+  }
+  const long m0 = (long)bx * kCDM;
+  const int q0 = by * kCDN;
   const int K = FWD ? Cin : 8 * Cout, Ka = FWD ? Cin : Cout;  // K, A row pitch
   const int nst = K / 64 / (SPLIT ? (int)gridDim.z : 1), st0 = SPLIT ? (int)blockIdx.z * nst : 0;
   // staging pieces of this thread: j < 4: A rows (256 x 8 slots), j >= 4: weight rows (128 x 8)
@@ -654,7 +667,8 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
     const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;
     auto kern = nt ? convt_lds_kernel<true, true> : convt_lds_kernel<true, false>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);
-    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), 8 * Cout / kCDN), dim3(512), kCDStage, s,
+    // 1-D grid, XCD-aware tile order (level-0 forward 125 -> 117 us vs the 2-D grid)
+    hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM) * (8 * Cout / kCDN)), dim3(512), kCDStage, s,
                        (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout, nullptr);
     PCMS_CHECK_LAUNCH();
   }
