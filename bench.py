@@ -47,7 +47,44 @@ def parse():
     ap.add_argument("--zero-fill", action="store_true", help="config 4: 1-2 modalities zeroed")
     ap.add_argument("--ckpt-decoder", action="store_true", help="config 5: decoder activation checkpointing")
     ap.add_argument("--fp32-steps", type=int, default=5, help="timed steps of the fp32 parity build (0: skip)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="launcher check only (CPU, gloo): every rank joins the group, rank 0 prints the "
+                         "world size it saw; no GPU work, no measurement")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(a) -> int:
+    """``--gpus N`` (N > 1) run as a plain ``python bench.py``: relaunch this script as N
+    ranks (one process per GPU, LOCAL_RANK = GPU index) through torch.distributed.run on
+    127.0.0.1, wait for them and return their exit status.  Called before this process
+    touches the GPU (the children initialise HIP; the parent never does)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def plumbing(a, world, rank):
+    """The launcher path without a GPU: each rank joins a gloo group and contributes 1 to
+    an all-reduce; rank 0 prints the rank count it saw."""
+    dist.init_process_group("gloo")
+    seen = torch.ones(1)
+    dist.all_reduce(seen)
+    if rank == 0:
+        print(json.dumps({"plumbing": True, "n_gpus": world, "ranks_seen": int(seen.item()),
+                          "requested": a.gpus, "backend": dist.get_backend()}), flush=True)
+    dist.destroy_process_group()
 
 
 def stem_roofline(tr, N, spatial, reps, in_step=None):
@@ -207,12 +244,22 @@ def timed_steps(tr, host_batches, warmup, steps, world):
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if a.plumbing:
+        return plumbing(a, world, rank)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != a.gpus:
+            print(f"bench.py: RCCL group has {dist.get_world_size()} ranks, --gpus {a.gpus}", file=sys.stderr)
+            sys.exit(2)
     import pcms_amd  # noqa: F401
     from pcms_amd.utils.trainer import Trainer
 

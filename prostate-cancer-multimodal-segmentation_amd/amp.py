@@ -45,24 +45,34 @@ class GradScaler:
             self._mul = torch.empty(1, device=dev)
         return self._ws, self._norm, self._mul
 
-    def unscale_(self, optimizer, max_norm: float = 0.0):
-        """Fold 1/scale (and the optimizer's pending data-parallel grad_scale, and a clip to
-        ``max_norm`` if > 0) into the optimizer's device-side gradient multiplier; the norm
-        of the unscaled gradient tells whether any element is inf/NaN."""
+    def unscale_(self, optimizer):
+        """torch.amp.GradScaler.unscale_: divide the gradients by the scale (and apply the
+        optimizer's pending data-parallel ``grad_scale``) IN PLACE, so ``param.grad`` holds
+        the unscaled values afterwards and a following ``clip_grad_norm_`` measures and clips
+        them (torch's documented unscale_ -> clip -> step sequence).  The norm of the unscaled
+        gradient, taken in the same pass, tells ``step`` whether any element is inf/NaN."""
+        self._unscale(optimizer, 0.0, in_place=True)
+
+    def _unscale(self, optimizer, max_norm: float = 0.0, in_place: bool = False):
+        """``in_place=False`` (Trainer's own step, and ``step`` without a prior unscale_):
+        1/scale, the data-parallel grad_scale and a clip to ``max_norm`` (> 0) are folded into
+        the optimizer's device-side gradient multiplier -- one norm pass, no scale pass; the
+        Adam kernel writes the unscaled (clipped) gradient back into ``param.grad``."""
         if not self.enabled or self._unscaled:
             return
         eng = optimizer.model.engine()
         ws, norm, mul = self._buffers(eng.flat_g.device)
         gscale = float(optimizer.grad_scale) / self._scale
-        call("pcms_grad_clip", eng.flat_g, eng.flat_g.numel(), gscale, float(max_norm), 0, ws, norm, mul)
-        optimizer.grad_mul = mul
+        call("pcms_grad_clip", eng.flat_g, eng.flat_g.numel(), gscale, float(max_norm), 1 if in_place else 0, ws,
+             norm, mul)
+        optimizer.grad_mul = None if in_place else mul
         optimizer.grad_scale = 1.0
         self._unscaled = True
 
     def step(self, optimizer, *args, **kwargs):
         if not self.enabled:
             return optimizer.step(*args, **kwargs)
-        self.unscale_(optimizer)
+        self._unscale(optimizer)
         self._found_inf = not math.isfinite(float(self._norm))  # host sync, as torch's scaler
         if self._found_inf:
             optimizer.grad_mul = None

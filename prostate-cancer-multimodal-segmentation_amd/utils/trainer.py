@@ -160,7 +160,7 @@ class BaseTrainer:
         # sum over ranks -> mean: folded into the Adam pass (which writes the mean back)
         self.optimizer.grad_scale = sync.finish() if self.distributed else 1.0
         if self.scaler is not None:
-            self.scaler.unscale_(self.optimizer, max_norm=self.max_grad_norm or 0.0)
+            self.scaler._unscale(self.optimizer, max_norm=self.max_grad_norm or 0.0)
             self.last_grad_norm = self.scaler._norm
             self.scaler.step(self.optimizer)
             self.scaler.update()

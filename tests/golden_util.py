@@ -56,3 +56,50 @@ def batch(name: str, step: int = 0):
     if ncls != 1:
         y = y.repeat(1, ncls, 1, 1, 1)
     return x, y
+
+
+PRE_BN_BIAS = ("conv.0.bias", "conv.3.bias")  # exact gradient 0
+
+
+def check_step_against_oracle(m, grads, r, lr=1e-4, grad_rl2=5e-3, report=None, min_confident=0.5):
+    """Gradients, post-Adam parameters and BatchNorm buffers of the GPU step ``m`` (after
+    opt.step; ``grads`` {name: cpu tensor}) vs an oracle step ``r`` with keys ``grads``,
+    ``p0`` (initial parameters) and ``post`` (state dict after the step).  Bars: gradient
+    relative L2 <= ``grad_rl2`` (pre-BN conv biases: |g| < 1e-4); parameters within 2.01 lr
+    everywhere (Adam's first step is ~lr sign(g)) and within 1e-5 relative where the
+    oracle's |g + wd p| exceeds 8x the tensor's largest gradient discrepancy (the update's
+    sign and size are then fixed), those "confident" elements being at least
+    ``min_confident`` of all weights; BatchNorm running stats within 1e-4 relative."""
+    nconf = ntot = 0
+    worst = (0.0, "")
+    for k, p in m.named_parameters():
+        got, exp = grads[k].double(), r["grads"][k].double()
+        if k.endswith(PRE_BN_BIAS):
+            assert got.abs().max() < 1e-4, k
+        else:
+            nrm = float(exp.norm())
+            rl = float((got - exp).norm()) / max(nrm, 1e-30)
+            worst = max(worst, (rl, k))
+            assert rl <= grad_rl2, (k, rl)
+        e = float((got - exp).abs().max())
+        pk = p.detach().cpu().double()
+        pe = r["post"][k].double()
+        d = (pk - pe).abs()
+        assert float(d.max()) <= 2.01 * lr + 1e-6, (k, float(d.max()))
+        if k.endswith(PRE_BN_BIAS):
+            continue
+        conf = (exp + 1e-5 * r["p0"][k].double()).abs() > max(8 * e, 1e-6)
+        nconf += int(conf.sum())
+        ntot += conf.numel()
+        if conf.any():
+            assert bool(torch.all(d[conf] <= 1e-5 * pe[conf].abs() + 2e-6)), (k, float(d[conf].max()))
+    sd = m.state_dict()
+    for k in sd:
+        if k.endswith(("running_mean", "running_var")):
+            torch.testing.assert_close(sd[k].cpu(), r["post"][k], rtol=1e-4, atol=1e-5, msg=k)
+        elif k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == int(r["post"][k]), k
+    if report is not None:
+        report.update(worst_grad_rl2=worst, confident=nconf / max(ntot, 1))
+    # most weights must actually be held to the tight bar
+    assert nconf >= min_confident * ntot, (nconf, ntot)

@@ -84,10 +84,29 @@ def test_dp_trainer_step_two_ranks(tmp_path, clip):
         rl = float((got - exp).norm() / exp.norm().clamp_min(1e-30))
         assert rl <= 5e-2, (k, rl)
     # Adam's first step moves each weight by ~lr * sign(g): within 2 lr of the simulation
+    # everywhere, and within 1e-5 relative where the simulated |g + wd p| exceeds 8x the
+    # tensor's largest gradient discrepancy (sign and size of the update fixed)
+    p0 = {k: sd[k].detach().clone() for k in keys}
     _, _ = ref.dp_step_simulated(sd, shards, lr=1e-4, loss="bce_dice") if clip == 0 else (None, None)
     if clip == 0:
-        pv = torch.cat([sd[k].detach().reshape(-1) for k in keys])
-        assert float((r["params"] - pv).abs().max()) <= 2.01e-4
+        off, nconf, ntot = 0, 0, 0
+        for k in keys:
+            n = sd[k].numel()
+            got, exp = r["params"][off:off + n].double(), sd[k].detach().reshape(-1).double()
+            gd = r["grad"][off:off + n].double()
+            ge = mean_g[off:off + n].double()
+            off += n
+            d = (got - exp).abs()
+            assert float(d.max()) <= 2.01e-4, (k, float(d.max()))
+            if k.endswith(PRE_BN_BIAS):
+                continue
+            e = float((gd - ge).abs().max())
+            conf = (ge + 1e-5 * p0[k].reshape(-1).double()).abs() > max(8 * e, 1e-6)
+            nconf += int(conf.sum())
+            ntot += n
+            if conf.any():
+                assert bool(torch.all(d[conf] <= 1e-5 * exp[conf].abs() + 2e-6)), (k, float(d[conf].max()))
+        assert nconf >= 0.2 * ntot, (nconf, ntot)
         bn = torch.cat([sd[k].reshape(-1) for k in sd if k.endswith(("running_mean", "running_var"))])
         np.testing.assert_allclose(r["bn"].numpy(), bn.numpy(), rtol=1e-4, atol=1e-5)
 
@@ -120,3 +139,18 @@ def test_dp_trainer_train_loop_two_ranks(tmp_path):
     assert ranks[0] == ranks[1]
     assert np.isfinite(ranks[0]["best"])
     assert (save / "latest_checkpoint.pth").exists()
+
+
+def test_rccl_backend_gradsync():
+    """The "nccl" (RCCL) backend that bench.py / Trainer use under data parallelism, at the
+    world size one GPU allows (1): group init through torch.distributed.run on 127.0.0.1, the
+    bucketed GradSync all-reduce and the BatchNorm broadcast on the device."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr=127.0.0.1", f"--master-port={_port()}",
+                        os.path.join(HERE, "tools", "rccl_worker.py")], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "rccl ok: world 1" in r.stdout

@@ -7,8 +7,9 @@ fp32 build (precision="fp32"): the north-star bar —
   * loss (1e-5), every gradient (relative L2 vs the reference's fp64 run, bar set by the
     reference fp32 path's own error), the post-Adam parameters and BatchNorm buffers, eval
     logits, and the second step's loss.
-bf16 build: a stated looser bound (bf16 storage cannot meet 1e-3: SURVEY F4/H3) —
-  loss within 1e-2 absolute, >= 99 % identical masks, logits within 0.1 * max|logit|.
+bf16 build: a stated looser bound (bf16 storage cannot meet 1e-3: SURVEY F4/H3) set by the
+  oracle's own bf16-autocast run on the same init and input — max |dlogit| <= 2x its error,
+  mask agreement >= its agreement - 0.5 %, loss within 2x its loss error (floor 1e-3).
 """
 import numpy as np
 import pytest
@@ -147,11 +148,28 @@ def test_bf16_parity_step(name, ckpt):
     loss = crit(logits, y.cuda())
     loss.backward()
     opt.step()
-    lg = logits.detach().cpu().numpy()
-    ref = g["logits_train"]
-    assert abs(float(loss) - float(g["loss0"])) < 1e-2
-    assert np.abs(lg - ref).max() <= 0.1 * np.abs(ref).max()
-    assert np.mean((lg > 0) == (ref > 0)) >= 0.99
+    lg = logits.detach().cpu()
+    # bar set by the oracle's own bf16 run (torch CPU autocast bf16 of the restatement, same
+    # init and input), as at the full-size configs (tests/test_gpu_configs.py)
+    from oracle import unet3d_cpu as ref_mod
+    torch.manual_seed(0)
+    sd = ref_mod.init_params(5, gu.CASES[name][0])
+    with torch.no_grad():
+        ref = ref_mod.forward({k: v.clone() for k, v in sd.items()}, x, training=True)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            auto = ref_mod.forward({k: v.clone() for k, v in sd.items()}, x, training=True).float()
+    lf = ref_mod.bce_dice_loss if gu.CASES[name][4] == "bce_dice" else ref_mod.dice_loss
+    l32, lbf = float(lf(ref, y)), float(lf(auto, y))
+    assert np.abs(ref.numpy() - g["logits_train"]).max() <= 1e-3  # the oracle is the reference's
+    e_auto = (auto - ref).abs().max().item()
+    agree_auto = ((auto > 0) == (ref > 0)).float().mean().item()
+    e = (lg - ref).abs().max().item()
+    agree = ((lg > 0) == (ref > 0)).float().mean().item()
+    print(f"\n[{name} bf16] max|dlogit| {e:.4f} (autocast {e_auto:.4f}), masks {agree:.5f} (autocast "
+          f"{agree_auto:.5f}), loss {float(loss):.6f} vs {l32:.6f} (autocast {lbf:.6f})")
+    assert e <= 2 * e_auto, (e, e_auto)
+    assert agree >= agree_auto - 0.005, (agree, agree_auto)
+    assert abs(float(loss) - l32) <= max(2 * abs(lbf - l32), 1e-3), (float(loss), l32, lbf)
     for k, p in m.named_parameters():
         assert torch.isfinite(p.grad).all(), k
 

@@ -193,3 +193,82 @@ def test_fused_adam_packs_match_flat_adam(gscale):
     torch.cuda.synchronize()
     for a, b in zip(packs, fresh):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+
+
+def _oracle_amp_clip_step(x, y, max_norm, init_scale=2.0 ** 16):
+    """The reference's mixed-precision step with the clip of its other trainers, on the CPU
+    oracle with torch's own GradScaler (train_bph_optimized.py:296-298 + train_bph.py:166):
+    scaler.scale(loss).backward(); scaler.unscale_(opt); clip_grad_norm_(params, max_norm);
+    scaler.step(opt); scaler.update()."""
+    from oracle import unet3d_cpu as ref
+    torch.manual_seed(0)
+    sd = ref.init_params(5, 1)
+    keys = ref.param_keys(sd)
+    p0 = {k: sd[k].detach().clone() for k in keys}
+    for k in keys:
+        sd[k].requires_grad_(True)
+    params = [sd[k] for k in keys]
+    opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-5)
+    scaler = torch.amp.GradScaler("cpu", init_scale=init_scale)
+    loss = ref.bce_dice_loss(ref.forward(sd, x, training=True), y)
+    scaler.scale(loss).backward()
+    scaler.unscale_(opt)
+    norm = float(torch.nn.utils.clip_grad_norm_(params, max_norm))
+    grads = {k: sd[k].grad.detach().clone() for k in keys}
+    scaler.step(opt)
+    scaler.update()
+    return {"loss": float(loss), "norm": norm, "grads": grads, "p0": p0,
+            "post": {k: v.detach().clone() for k, v in sd.items()}, "scale": scaler.get_scale()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["user_sequence", "trainer"])
+def test_amp_clip_step_matches_oracle_torch_gradscaler(path):
+    """AMP + clip against the oracle driven by torch.amp.GradScaler (not against our own
+    engine): ``user_sequence`` is torch's documented unscale_ -> clip_grad_norm_ -> step
+    pattern on our GradScaler / clip (unscale_ must leave unscaled gradients in
+    param.grad); ``trainer`` is Trainer(use_amp, max_grad_norm).step with unscale and clip
+    folded into the Adam pass.  Same loss, same total norm, gradients (left in param.grad:
+    unscaled and clipped) within the 16^3 golden bar, post-step parameters with the
+    confident-element bar (tests/golden_util.check_step_against_oracle)."""
+    from pcms_amd.amp import GradScaler, clip_grad_norm_
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    from pcms_amd.utils.trainer import Trainer
+    from tests import golden_util as gu
+    gen = torch.Generator().manual_seed(9)
+    x = torch.rand(2, 5, 16, 16, 16, generator=gen)
+    y = (torch.rand(2, 1, 16, 16, 16, generator=gen) < 0.5).float()
+    r = _oracle_amp_clip_step(x, y, 1.0)
+    torch.manual_seed(0)
+    if path == "user_sequence":
+        m = UNet3D(n_modalities=5, n_classes=1, precision="fp32").cuda()
+        opt = FlatAdam(m, lr=1e-4, weight_decay=1e-5)
+        sc = GradScaler()
+        opt.zero_grad()
+        loss = BCEDiceLoss()(m(x.cuda()), y.cuda())
+        sc.scale(loss).backward()
+        sc.unscale_(opt)
+        # param.grad now holds the unscaled gradient (torch semantics)
+        g_unscaled = torch.cat([p.grad.detach().reshape(-1) for p in m.parameters()]).double()
+        norm = float(clip_grad_norm_(m, 1.0, opt))
+        assert abs(float(g_unscaled.norm()) - norm) <= 1e-6 * norm
+        sc.step(opt)
+        sc.update()
+        loss = float(loss)
+        scale = sc.get_scale()
+    else:
+        tr = Trainer({"device": "cuda", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1,
+                      "loss": "bce_dice", "precision": "fp32", "use_amp": True, "max_grad_norm": 1.0})
+        m = tr.model
+        loss = tr.step({"image": x, "label": y})
+        norm = float(tr.last_grad_norm)
+        scale = tr.scaler.get_scale()
+    torch.cuda.synchronize()
+    assert abs(loss - r["loss"]) <= 1e-5, (loss, r["loss"])
+    assert abs(norm - r["norm"]) <= 1e-3 * r["norm"], (norm, r["norm"])
+    assert norm > 1.0  # the clip engaged
+    assert scale == r["scale"]
+    grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
+    gu.check_step_against_oracle(m, grads, r, grad_rl2=5e-2, min_confident=0.2)
