@@ -266,11 +266,37 @@ def get_dataloader(data_dir: str, batch_size: int = 2, shuffle: bool = True, mod
     if indices is not None:
         ds = torch.utils.data.Subset(ds, indices)
     sampler = None
+    if world_size > 1 and not is_training:
+        # evaluation: whole batches of the single-process order, batch b on rank b % W (no
+        # padding, no duplicates: the (sum, count) of per-batch losses over ranks is the
+        # single-process mean)
+        return DataLoader(ds, batch_sampler=BatchShard(len(ds), batch_size, rank, world_size),
+                          num_workers=num_workers, pin_memory=torch.cuda.is_available())
     if world_size > 1:
         sampler = torch.utils.data.distributed.DistributedSampler(ds, num_replicas=world_size, rank=rank,
                                                                   shuffle=shuffle)
     return DataLoader(ds, batch_size=batch_size, shuffle=shuffle and sampler is None, sampler=sampler,
                       num_workers=num_workers, pin_memory=torch.cuda.is_available())
+
+
+class BatchShard(torch.utils.data.Sampler):
+    """Batches ``b = 0, 1, ...`` of ``range(n)`` in order (``batch_size`` each, the last one
+    short), keeping those with ``b % world_size == rank``."""
+
+    def __init__(self, n: int, batch_size: int, rank: int, world_size: int):
+        self.n, self.bs, self.rank, self.world = n, batch_size, rank, world_size
+
+    def __iter__(self):
+        for b, lo in enumerate(range(0, self.n, self.bs)):
+            if b % self.world == self.rank:
+                yield list(range(lo, min(self.n, lo + self.bs)))
+
+    def __len__(self):
+        nb = -(-self.n // self.bs)
+        return max(0, -(-(nb - self.rank) // self.world))
+
+    def set_epoch(self, epoch: int) -> None:  # the evaluation order does not change
+        pass
 
 
 def kfold_indices(n_cases: int, n_splits: int = 5, seed: int = 42):

@@ -252,10 +252,14 @@ class UNetEngine:
             return (t.data_ptr() - base) // 4
 
         fused = []
+        skipped = 0  # layers (besides the stem) whose packs the Adam kernels do not write
         conv_rows, tiles = [], 0
         for i, cs in enumerate(self.convs):
             w = cs.mod.weight
-            if i == 0 or cs.cin % 32 or cs.cout % 32 or offset(w) % 4:
+            if i == 0:
+                continue
+            if cs.cin % 32 or cs.cout % 32 or offset(w) % 4:
+                skipped += 1
                 continue
             conv_rows.append([offset(w), cs.cout, cs.cin, cs.fwd.data_ptr(), cs.dgrad.data_ptr(), tiles, 0, 0])
             tiles += (cs.cout // 32) * (cs.cin // 32)
@@ -265,6 +269,7 @@ class UNetEngine:
             w = up.weight
             cin, cout = up.in_channels, up.out_channels
             if cin % 32 or cout % 32 or offset(w) % 4:
+                skipped += 1
                 continue
             f, d = self.convt_packs[i]
             ct_rows.append([offset(w), cin, cout, f.data_ptr(), d.data_ptr(), ct_tiles, 0, 0])
@@ -286,6 +291,9 @@ class UNetEngine:
             "convt": tab(ct_rows), "nconvt": len(ct_rows), "convt_tiles": ct_tiles,
             "ranges": torch.tensor(ranges if ranges else [[0, 0]], dtype=torch.int64, device=dev),
             "nranges": len(ranges), "max_len": max([e - b for b, e in ranges], default=0),
+            # every conv / ConvT pack but the stem's comes out of the Adam pass (else the step
+            # must not mark the packs fresh: a skipped layer would train on stale packs)
+            "complete": skipped == 0,
         }
         return self._adam_plan
 

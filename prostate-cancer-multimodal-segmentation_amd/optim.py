@@ -71,7 +71,7 @@ class FlatAdam(torch.optim.Optimizer):
         # back into param.grad)
         self.grad_scale = 1.0
         self.grad_mul = None
-        eng.mark_dirty(packs_fresh=plan is not None)
+        eng.mark_dirty(packs_fresh=plan is not None and plan["complete"])
         return loss
 
     def zero_grad(self, set_to_none: bool = True):

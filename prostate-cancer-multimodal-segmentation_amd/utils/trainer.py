@@ -212,9 +212,7 @@ class BaseTrainer:
             n += 1
         return total / max(n, 1)
 
-    def validate_epoch(self):
-        if self.val_loader is None:
-            return None
+    def _validate_sums(self):
         self.model.eval()
         total, n = 0.0, 0
         with torch.no_grad():
@@ -222,6 +220,21 @@ class BaseTrainer:
                 out = self.model(batch["image"].to(self.device))
                 total += self.criterion(out, batch["label"].to(self.device)).item()
                 n += 1
+        return total, n
+
+    def validate_epoch(self):
+        """utils/trainer.py:201-234: the mean of the per-batch losses.  Under data
+        parallelism each rank evaluates whole batches of the single-process batching
+        (data.get_dataloader, ``is_training=False``: batches r, r + W, ...; no padding) and
+        the (sum, count) pair is summed over ranks, so every rank gets the full-set value the
+        single-process reference computes."""
+        if self.val_loader is None:
+            return None
+        total, n = self._validate_sums()
+        if self.distributed:
+            t = torch.tensor([total, float(n)], dtype=torch.float64, device=self.model.engine().flat_p.device)
+            dist.all_reduce(t)
+            total, n = float(t[0]), int(t[1])
         return total / max(n, 1)
 
     def save_checkpoint(self, epoch, loss, is_best=False, best_loss=None, patience=None):
@@ -284,7 +297,7 @@ class BaseTrainer:
             train_loss = self._mean_over_ranks(self.train_epoch())
             if self.distributed:  # validate with rank 0's running statistics everywhere
                 dist.broadcast(self.model.engine().flat_bn, src=0)
-            val_loss = self._mean_over_ranks(self.validate_epoch())
+            val_loss = self.validate_epoch()  # already the full-set value on every rank
             cur = val_loss if val_loss is not None else train_loss
             self.scheduler.step(cur)
             if cur < best:
@@ -293,6 +306,10 @@ class BaseTrainer:
                     self.save_checkpoint(epoch + 1, cur, is_best=True, best_loss=best, patience=patience)
             else:
                 patience += 1
+                if self.config.get("save_dir"):
+                    # latest_checkpoint.pth every epoch (the reference writes it on improvement
+                    # only): a resumed train() continues from this epoch with this patience
+                    self.save_checkpoint(epoch + 1, cur, best_loss=best, patience=patience)
             if patience >= 20:
                 break
         self._resume = (best, patience)

@@ -61,11 +61,29 @@ def batch(name: str, step: int = 0):
 PRE_BN_BIAS = ("conv.0.bias", "conv.3.bias")  # exact gradient 0
 
 
+def oracle_grads64(sd, x, y, loss: str = "bce_dice"):
+    """The oracle's gradients of one training forward/backward in fp64 (the truth the fp32
+    runs are measured against: both are fp32 approximations with different summation
+    orders, so their distance alone says little at large sizes)."""
+    from oracle import unet3d_cpu as ref
+    sd64 = {k: v.detach().double().clone() for k, v in sd.items()}
+    keys = ref.param_keys(sd64)
+    for k in keys:
+        sd64[k].requires_grad_(True)
+    fn = ref.bce_dice_loss if loss == "bce_dice" else ref.dice_loss
+    out = ref.forward(sd64, x.double(), training=True)
+    fn(out, y.double()).backward()
+    return {k: sd64[k].grad.detach().clone() for k in keys}
+
+
 def check_step_against_oracle(m, grads, r, lr=1e-4, grad_rl2=5e-3, report=None, min_confident=0.5):
     """Gradients, post-Adam parameters and BatchNorm buffers of the GPU step ``m`` (after
     opt.step; ``grads`` {name: cpu tensor}) vs an oracle step ``r`` with keys ``grads``,
-    ``p0`` (initial parameters) and ``post`` (state dict after the step).  Bars: gradient
-    relative L2 <= ``grad_rl2`` (pre-BN conv biases: |g| < 1e-4); parameters within 2.01 lr
+    ``p0`` (initial parameters) and ``post`` (state dict after the step), optionally
+    ``grads64`` (the oracle's fp64 gradients, ``oracle_grads64``).  Bars: gradient
+    relative L2 <= ``grad_rl2`` -- with ``grads64``: the distance to the fp64 truth within
+    max(``grad_rl2``, 10x the fp32 oracle's own distance to it), the bar of the golden
+    tests (test_gpu_parity.py) -- (pre-BN conv biases: |g| < 1e-4); parameters within 2.01 lr
     everywhere (Adam's first step is ~lr sign(g)) and within 1e-5 relative where the
     oracle's |g + wd p| exceeds 8x the tensor's largest gradient discrepancy (the update's
     sign and size are then fixed), those "confident" elements being at least
@@ -76,6 +94,13 @@ def check_step_against_oracle(m, grads, r, lr=1e-4, grad_rl2=5e-3, report=None, 
         got, exp = grads[k].double(), r["grads"][k].double()
         if k.endswith(PRE_BN_BIAS):
             assert got.abs().max() < 1e-4, k
+        elif "grads64" in r:
+            t = r["grads64"][k].double()
+            nrm = max(float(t.norm()), 1e-30)
+            rl = float((got - t).norm()) / nrm
+            rl_ref = float((exp - t).norm()) / nrm
+            worst = max(worst, (rl, k))
+            assert rl <= max(grad_rl2, 10 * rl_ref), (k, rl, rl_ref)
         else:
             nrm = float(exp.norm())
             rl = float((got - exp).norm()) / max(nrm, 1e-30)

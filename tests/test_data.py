@@ -102,3 +102,19 @@ def test_dataset_strategies(tmp_path):
     dl = d.get_dataloader(str(tmp_path), batch_size=2, shuffle=False, target_size=(8, 8, 8))
     b = next(iter(dl))
     assert b["image"].shape == (2, 5, 8, 8, 8) and b["case_id"] == ["full", "noDWI"]
+
+
+@pytest.mark.parametrize("n,bs,world", [(5, 2, 2), (7, 3, 4), (4, 2, 2), (1, 2, 2)])
+def test_eval_batches_shard_without_padding(n, bs, world):
+    """Data-parallel evaluation: the ranks' batches are exactly the single-process batches
+    (whole, in order, none duplicated), so (sum, count) of per-batch losses over ranks gives
+    the reference's validate_epoch mean (DistributedSampler padded the set)."""
+    d = _data()
+    single = [list(range(lo, min(n, lo + bs))) for lo in range(0, n, bs)]
+    got = []
+    for r in range(world):
+        s = d.BatchShard(n, bs, r, world)
+        b = list(s)
+        assert len(b) == len(s)
+        got += b
+    assert sorted(got) == sorted(single)

@@ -8,9 +8,11 @@
 Bars, against the CPU oracle (tests/test_oracle_golden.py pins it to the
 reference) run on the GPU box's host cores:
 * fp32 build, configs 2 and 4, a whole training step: train-mode logits within 1e-3,
-  identical ``logit > 0`` masks where |ref| >= 1e-3, loss within 1e-5; every gradient
-  within 5e-3 relative L2 of the oracle's fp32 gradient (the config-1 golden bar; the 18
-  pre-BN conv biases, whose exact gradient is 0, within 1e-4 absolute); the
+  identical ``logit > 0`` masks where |ref| >= 1e-3, loss within 1e-5; every gradient's
+  relative L2 distance to the oracle's fp64 gradient within max(5e-3, 10x the fp32
+  oracle's own distance to it) (the golden tests' bar: at this size two fp32 summation
+  orders alone differ by ~5e-3 on some BatchNorm parameters; the 18 pre-BN conv biases,
+  whose exact gradient is 0, within 1e-4 absolute); the
   post-Adam parameters within 2.01 lr everywhere and within 1e-5 relative on "confident"
   elements (|g + wd p| of the oracle above 8x the tensor's largest gradient discrepancy,
   so the Adam update's sign and size are fixed); BatchNorm running statistics within
@@ -73,6 +75,7 @@ def oracle_run(request):
     torch.manual_seed(0)
     sd = ref.init_params(5, 1)
     out = _oracle_forward_pair(sd, x, y)
+    out["grads64"] = gu.oracle_grads64(sd, x, y)
     step = ref.RefStep(sd, lr=1e-4, loss="bce_dice")
     p0 = {k: sd[k].detach().clone() for k in step.keys}
     loss, logits = step.forward_backward(x, y)
