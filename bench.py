@@ -8,7 +8,8 @@ loss + backward + (all-reduce) + Adam.  The K timed steps run back to back betwe
 device synchronize on both sides; per-step times are HIP events recorded on the compute
 stream at every step boundary, max over ranks, and ``value`` uses their MEDIAN (the wall time
 of the K steps is reported beside it).  Prints ONE JSON line (rank 0) with the roofline of the stem conv
-(forward + weight-gradient kernels, HBM-bound, 578.9 MB algorithmic at N=2), their launch
+(forward + weight-gradient kernels with the stem's BatchNorm-backward apply fused into the
+latter, HBM-bound, 847.3 MB algorithmic at N=2), their launch
 durations measured with HIP events on the launch stream inside the timed steps, the fp32
 parity build's rate, and the CPU oracle timed on the host cores
 (rank 0, N=1 only: 1 warm-up + 3 timed steps at the config batch, median).
@@ -118,14 +119,18 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
 
     def fwd(s):
         if sup & 1:
-            L.call("pcms_stem_fwd", s[0], eng.stem_pack, cs.mod.bias, s[1], stats, N, D, H, W)
+            L.call("pcms_stem_fwd", s[0], eng.stem_pack, cs.mod.bias, s[1], stats, N, D, H, W, 0)
         else:
             L.call("pcms_conv3_fwd", code, s[0], eng.cp, None, 0, cs.fwd, cs.mod.bias, s[1], None, 64, None,
                    stats, 0, N, D, H, W, 64, 1)
 
+    bn = eng.enc[0].b0
+    coef = torch.zeros(3 * 64, device="cuda")
+
     def wgrad(s):
-        if sup & 2:
-            L.call("pcms_stem_wgrad", s[0], s[2], dw, dwt, 5, N, D, H, W)
+        if sup & 2:  # the product path: the stem's BN0 backward apply fused in (y = s[1])
+            L.call("pcms_stem_wgrad_bn", s[0], s[2], s[1], bn.scale, bn.shift, bn.mean, bn.invstd, coef, dw, dwt, 5,
+                   N, D, H, W)
         else:
             L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
 
@@ -147,26 +152,32 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
             trials.append(ev0.elapsed_time(ev1) / reps * 1e-3)  # s per launch
         res[name] = statistics.median(trials)
     es = 2 if code == 1 else 4
-    # algorithmic bytes: X (5 ch) + W + Y  /  X + dY + dW
+    # algorithmic bytes: X (5 ch) + W + Y  /  X + dY + dW; with the stem's
+    # BatchNorm + ReLU backward apply fused into its weight gradient (pcms_stem_wgrad_bn) the
+    # backward reads dA (the ReLU output's gradient) and Y (pre-BN) instead of dY
     xb = nvox * 5 * es
     yb = nvox * 64 * es
+    fused = bool(sup & 2)
     fwd_bytes = xb + 64 * 5 * 27 * es + yb
-    wg_bytes = xb + yb + 64 * 5 * 27 * 4
+    wg_bytes = xb + (2 if fused else 1) * yb + 64 * 5 * 27 * 4
     t = res["fwd"] + res["wgrad"]
     achieved = (fwd_bytes + wg_bytes) / t
     # HBM bytes per fwd+wgrad pair from the PMC counters (FETCH_SIZE / WRITE_SIZE in separate
     # rocprofv3 passes, gfx950 FETCH correction: tests/kexp/pmc_stem_traffic.sh), committed
     # for the shape they were measured on; null for any other shape
     traffic = None
-    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2_stem_traffic.json")
+    kernel = ("stem conv3d 5->64 fwd + wgrad with the BN0 backward apply fused in (stem_fwd_direct_kernel + "
+              "stem_wgrad_stream_kernel<BN>)" if fused else
+              "stem conv3d 5->64 fwd + wgrad (stem_fwd_direct_kernel + stem_wgrad_stream_kernel)")
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3_stem_traffic.json")
     if os.path.exists(tf):
         with open(tf) as f:
             rec = json.load(f)
-        if rec.get("shape") == [N, D, H, W] and code == 1:
+        if rec.get("shape") == [N, D, H, W] and code == 1 and rec.get("kernel") == kernel:
             traffic = rec["traffic_bytes_per_pair"]
     return {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
-            "kernel": "stem conv3d 5->64 fwd + wgrad (stem_fwd_direct_kernel + stem_wgrad_stream_kernel)",
+            "kernel": kernel,
             "algorithmic_bytes": fwd_bytes + wg_bytes, "t_fwd_us": round(res["fwd"] * 1e6, 1),
             "t_wgrad_us": round(res["wgrad"] * 1e6, 1),
             "timing": "HIP events around each launch inside the timed steps" if in_step else

@@ -23,6 +23,12 @@
 extern "C" {
 #endif
 
+/* conv epilogue flags (pcms_conv3_fwd, pcms_split_epilogue, pcms_stem_fwd): ACCUMULATE
+ * adds into y; RELU stores relu(conv + bias) -- eval mode with the BatchNorm folded into the
+ * weights and bias (pcms_bn_fold), no statistics                                          */
+#define PCMS_CONV_ACCUMULATE 1
+#define PCMS_CONV_RELU 2
+
 /* ---- layout ---------------------------------------------------------------------- */
 /* batch['image'] (N, Cin, D, H, W) fp32 NCDHW -> NDHWC, channels zero-padded to Cp.
  * Replaces the implicit layout of images.to(device) (utils/trainer.py:179).          */
@@ -56,7 +62,7 @@ int pcms_conv3_pack2(int dtype, const float* w, void* fwd, void* dgrad, int Cout
 int pcms_conv3_splits(int dtype, int Cin, int splits);  /* slabs a split-K launch uses   */
 int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
-                   float* yacc, float* stats, int accumulate,
+                   float* yacc, float* stats, int flags,
                    int N, int D, int H, int W, int Cout, int splits, hipStream_t s);
 /* dw [Cout][cin_w][27] fp32 += sum_v dy[v, co] * x[v + tap, ci] (ci < cin_w <= c0 + c1);
  * dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (one partial row per voxel split,
@@ -76,17 +82,25 @@ int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
  * with rows = pcms_stem_fwd_rows(N, D, H, W) (one row per workgroup on the hot shapes)   */
 int pcms_stem_fwd_rows(int N, int D, int H, int W);
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
-                  int N, int D, int H, int W, hipStream_t s);
+                  int N, int D, int H, int W, int flags, hipStream_t s);
 /* dw [64][cin_w][27] += stem weight gradient (streaming kernel: one partial row per
  * workgroup in ws, then a fixed-order sum), ws = pcms_stem_wgrad_ws_floats(...) floats.   */
 int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w);
 int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H,
                     int W, hipStream_t s);
+/* Block fusion of the stem's BatchNorm + ReLU backward (models/unet3d.py:29-33) into its
+ * weight gradient: da = gradient of the block's first ReLU output, y = the stem's pre-BN
+ * output, scale / shift / mean / invstd = the forward's BN coefficients, coef = the apply
+ * coefficients pcms_bn_relu_bwd(..., dy = NULL, ...) left; the stem's dy is formed in LDS
+ * per box and never stored (the stem input needs no gradient).                          */
+int pcms_stem_wgrad_bn(const void* x, const void* da, const void* y, const float* scale, const float* shift,
+                       const float* mean, const float* invstd, const float* coef, float* dw, float* ws, int cin_w,
+                       int N, int D, int H, int W, hipStream_t s);
 /* y = sum of the `splits` slabs of acc (in split order) + bias -> storage type; stats
  * layout as pcms_conv3_fwd with rows = pcms_split_epilogue_rows(nvox)                    */
 int pcms_split_epilogue_rows(long nvox);
 int pcms_split_epilogue(int dtype, const float* acc, int splits, const float* bias, void* y0, void* y1,
-                        int cy0, float* stats, int C, long nvox, hipStream_t s);
+                        int cy0, float* stats, int C, long nvox, int flags, hipStream_t s);
 
 /* ---- BatchNorm3d (train / eval) + ReLU(inplace): models/unet3d.py:31-39 ----------- */
 /* part: the [rows][C][2] (sum, M2) partials + [rows] counts written by the conv / stem /
@@ -97,21 +111,47 @@ int pcms_bn_finalize(const float* part, int rows, int C, double count, const flo
                      const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
                      float eps, float* scale, float* shift, float* mean, float* invstd, double* ws,
                      hipStream_t s);
+/* Eval-mode BatchNorm folded into the conv before it (UNet3D.predict / .inference,
+ * models/unet3d.py:298-344): wo = w * sc[co], bo = b * sc + sh (sc = gamma / sqrt(rvar +
+ * eps), sh = beta - rmean * sc, in fp64); w [Cout][K] fp32 (K = Cin * 27), b may be NULL.
+ * The folded conv with PCMS_CONV_RELU is conv -> BN -> ReLU in one pass.                  */
+int pcms_bn_fold(const float* w, const float* b, const float* gamma, const float* beta, const float* rmean,
+                 const float* rvar, float eps, int Cout, long K, float* wo, float* bo, hipStream_t s);
 int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                         float eps, int C, float* scale, float* shift, hipStream_t s);
 int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const float* shift, int C,
                  long nvox, hipStream_t s);
 int pcms_bn_bwd_rows(int dtype, int C, long nvox);
-/* dy = BN+ReLU backward(da); dgamma/dbeta += ; part: rows*C*2 fp32; coef: 3*C fp32   */
+/* dy = BN+ReLU backward(da); dgamma/dbeta += ; part: rows*C*2 fp32; coef: 3*C fp32 (the
+ * apply coefficients k1, k2, k3 per channel: dy = k1 g + k2 xhat + k3).  dy == NULL: no
+ * apply pass (a fused consumer applies from coef: pcms_stem_wgrad_bn)                    */
 int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scale, const float* shift,
                      const float* mean, const float* invstd, const float* gamma, float* part, float* coef,
                      float* dgamma, float* dbeta, void* dy, int C, long nvox, double* ws, hipStream_t s);
+/* the same without the reduction pass: ``part`` holds ``rows`` partial rows [rows][C][2] of
+ * (sum g, sum g xhat) written by a fused producer (pcms_maxpool_bwd_bn)                  */
+int pcms_bn_relu_bwd_finish(int dtype, const void* da, const void* y, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, const float* gamma, const float* part,
+                            int rows, float* coef, float* dgamma, float* dbeta, void* dy, int C, long nvox,
+                            double* ws, hipStream_t s);
 
 /* ---- MaxPool3d(2): models/unet3d.py:80 ------------------------------------------- */
 int pcms_maxpool_fwd(int dtype, const void* a, void* p, int N, int D, int H, int W, int C, hipStream_t s);
 /* da[argmax] += dp (first max in d,h,w scan order wins, as PyTorch)                  */
 int pcms_maxpool_bwd(int dtype, const void* a, const void* dp, void* da, int N, int D, int H, int W,
                      int C, hipStream_t s);
+/* Block fusion at the encoder's Down3D boundary (a DoubleConv's second BatchNorm3d + ReLU,
+ * models/unet3d.py:37-39, and the next MaxPool3d, :80).  Forward: a = relu(y scale + shift)
+ * is stored (the block output, also the skip input) and pooled into p in the same pass.
+ * Backward: da (the block output's gradient, holding the skip part) += dp at the argmax of a,
+ * which is recomputed from y; the pass also writes the BatchNorm-backward partial rows
+ * [rows][C][2] for pcms_bn_relu_bwd_finish (rows = pcms_maxpool_bwd_bn_rows(...)).       */
+int pcms_bn_relu_pool(int dtype, const void* y, void* a, void* p, const float* scale, const float* shift,
+                      int N, int D, int H, int W, int C, hipStream_t s);
+int pcms_maxpool_bwd_bn_rows(int dtype, int N, int D, int H, int W, int C);
+int pcms_maxpool_bwd_bn(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                        const float* invstd, const void* dp, void* da, float* part, int N, int D, int H, int W,
+                        int C, hipStream_t s);
 
 /* ---- ConvTranspose3d(k=2, s=2) + F.pad: models/unet3d.py:120,139-151 --------------- */
 int pcms_convt_pack(int dtype, const float* w, void* out, int Cin, int Cout, int dgrad, hipStream_t s);
@@ -147,6 +187,22 @@ int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, floa
 int pcms_head_bwd_ws_floats(long nvox_per_n, int N, int ncls);
 int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w, void* da, float* dw,
                   float* db, float* ws, long nvox_per_n, int N, int ncls, hipStream_t s);
+/* Block fusion of the decoder's last BatchNorm3d + ReLU (models/unet3d.py:37-39, up4's
+ * DoubleConv) with the head (:222, :295).  Forward: the head reads that block's pre-BN conv
+ * output y and applies BN + ReLU itself (scale / shift from pcms_bn_finalize or
+ * pcms_bn_eval_coeffs); the ReLU output is never stored.  Backward: dw / db += the head's
+ * gradients, dgamma / dbeta += the BatchNorm's, and dy = the gradient of y -- the head's input
+ * gradient is recomputed per voxel from dlogits instead of being stored and read twice.
+ * ws: pcms_head_bwd_ws_floats; bnpart: pcms_head_bn_bwd_rows(...) * 64 * 2 fp32; coef: 3*64
+ * fp32; bnws: pcms_bn_ws_doubles(64) fp64.  C = 64 input channels.                      */
+int pcms_head_bn_fwd(int dtype, const void* y, const float* scale, const float* shift, const float* w,
+                     const float* b, float* out, long nvox_per_n, int N, int ncls, int act, float thr,
+                     hipStream_t s);
+int pcms_head_bn_bwd_rows(long nvox_per_n, int N);
+int pcms_head_bn_bwd(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                     const float* invstd, const float* gamma, const float* dlogits, const float* w, float* dw,
+                     float* db, float* ws, float* bnpart, float* coef, float* dgamma, float* dbeta, void* dy,
+                     long nvox_per_n, int N, int ncls, double* bnws, hipStream_t s);
 
 /* ---- DiceLoss / BCEDiceLoss: utils/losses.py:44-92, 124-152 ------------------------ */
 int pcms_loss_rows(long M);

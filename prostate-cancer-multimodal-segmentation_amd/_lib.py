@@ -32,19 +32,25 @@ SIGNATURES = {
     "pcms_stem_pack": "ppis",
     "pcms_stem_supported": "iiii",
     "pcms_stem_fwd_rows": "iiii",
-    "pcms_stem_fwd": "pppppiiiis",
+    "pcms_stem_fwd": "pppppiiiiis",
     "pcms_stem_wgrad_ws_floats": "iiiii",
     "pcms_stem_wgrad": "ppppiiiiis",
+    "pcms_stem_wgrad_bn": "ppppppppppiiiiis",
     "pcms_split_epilogue_rows": "l",
-    "pcms_split_epilogue": "ipipppipils",
+    "pcms_split_epilogue": "ipipppipilis",
     "pcms_bn_ws_doubles": "i",
     "pcms_bn_finalize": "piidpppppffppppps",
     "pcms_bn_eval_coeffs": "ppppfipps",
+    "pcms_bn_fold": "ppppppfilpps",
     "pcms_bn_relu": "ippppils",
     "pcms_bn_bwd_rows": "iil",
     "pcms_bn_relu_bwd": "i" + "p" * 12 + "ilps",
     "pcms_maxpool_fwd": "ippiiiiis",
     "pcms_maxpool_bwd": "ipppiiiiis",
+    "pcms_bn_relu_pool": "ipppppiiiiis",
+    "pcms_maxpool_bwd_bn_rows": "iiiiii",
+    "pcms_maxpool_bwd_bn": "ippppppppiiiiis",
+    "pcms_bn_relu_bwd_finish": "i" + "p" * 8 + "ippppilps",
     "pcms_convt_pack": "ippiiis",
     "pcms_convt_fwd": "ippppiiiiiiiiis",
     "pcms_convt_dgrad": "ipppiiiiiiiiis",
@@ -57,6 +63,9 @@ SIGNATURES = {
     "pcms_head_fwd": "ippppliiifs",
     "pcms_head_bwd_ws_floats": "lii",
     "pcms_head_bwd": "ipppppppliis",
+    "pcms_head_bn_fwd": "ippppppliiifs",
+    "pcms_head_bn_bwd_rows": "li",
+    "pcms_head_bn_bwd": "i" + "p" * 16 + "liips",
     "pcms_loss_rows": "l",
     "pcms_loss_fwd": "pplfffppps",
     "pcms_loss_bwd": "pplpfffpps",

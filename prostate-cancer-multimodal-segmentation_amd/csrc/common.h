@@ -19,6 +19,8 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 #define LDS_AS __attribute__((address_space(3)))
 
 enum { PCMS_F32 = 0, PCMS_BF16 = 1 };
+// conv epilogue flags (pcms_conv3_fwd, pcms_split_epilogue, pcms_stem_fwd)
+enum { PCMS_CONV_ACCUMULATE = 1, PCMS_CONV_RELU = 2 };
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) {
@@ -108,6 +110,21 @@ template <bool NT, typename T> __device__ __forceinline__ void ld16(const T* p, 
 template <bool NT, typename T> __device__ __forceinline__ void st16(T* p, const float* in) {
   if constexpr (NT) store16_nt<T>(p, in); else store16<T>(p, in);
 }
+// BatchNorm (train or eval coefficients) + ReLU of one element: the one expression every
+// kernel that applies it uses (bn_relu pass and the fused consumers), so a recomputed
+// activation equals the stored one bit for bit
+__device__ __forceinline__ float bn_relu1(float y, float sc, float sh) { return fmaxf(__builtin_fmaf(y, sc, sh), 0.f); }
+// ReLU of 8 packed bf16 values: negative ones (sign bit set) -> +0
+__device__ __forceinline__ u32x4_t relu_bf16x8(u32x4_t v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] &= ~(((v[i] >> 15) & 0x00010001u) * 0xffffu);
+  return v;
+}
+// a value as it reads back after a store in T (bf16: rounded to nearest even)
+template <typename T> __device__ __forceinline__ float round_st(float v) {
+  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v)); else return v;
+}
+
 // streams this large bypass the caches (non-temporal loads / stores)
 constexpr long kNtBytes = 128L << 20;
 

@@ -250,7 +250,9 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
       }
   }
   constexpr int kRedOff = 512 * 64 * 2;  // bf16 C tile [512][64] occupies the first 64 KiB
-  if (!kF32 && !p.yacc && !p.accumulate) {
+  // (PCMS_CONV_RELU, eval with the BatchNorm folded into w / b: tested where used, from the
+  // kernel argument -- a flag held across the epilogue cost a spill)
+  if (!kF32 && !p.yacc && !(p.accumulate & PCMS_CONV_ACCUMULATE)) {
     // bf16 fast path: + bias, stats from the fp32 values, C tile -> LDS (box order), then
     // 16-byte coalesced stores (one box row = a contiguous w-run of voxels).
     __syncthreads();  // every wave is done reading the halo
@@ -281,7 +283,9 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
       const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
       const int co = co_base + q * 8;
       T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
-      *reinterpret_cast<u32x4_t*>(dst) = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
+      u32x4_t o = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
+      if (p.accumulate & PCMS_CONV_RELU) o = relu_bf16x8(o);
+      *reinterpret_cast<u32x4_t*>(dst) = o;
     }
   } else if (wave_active) {
 #pragma unroll
@@ -305,7 +309,8 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
           v += bias_l[nt];
           T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co
                                 : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
-          if (p.accumulate) v += Elem<T>::ld(dst);  // (stats are refused with accumulate)
+          if (p.accumulate & PCMS_CONV_ACCUMULATE) v += Elem<T>::ld(dst);  // (stats are refused with accumulate)
+          if (p.accumulate & PCMS_CONV_RELU) v = fmaxf(v, 0.f);
           Elem<T>::st(dst, v);
           s1[nt] += v;
         }
@@ -1320,6 +1325,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     char* wst = stg + (lane_o & 31) * 4 + nt * 2 + (lane_o >> 5) * 512;
     float* rme = red + (mg * 64 + 2 * (lane_o & 31) + nt) * 3;  // [ch][mean, M2, n] of this wave's channel
     const float bias0 = bls[2 * (lane_o & 31) + nt];
+    const bool relu = p.accumulate & PCMS_CONV_RELU;  // eval: BatchNorm folded (no stats then)
     const float rn = (float)nbdone * (32.f * MT);
     const float K0 = nbdone ? rme[0] : bias0;
     const float c0s = bias0 - K0;  // d = acc + bias - K
@@ -1332,7 +1338,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
         for (int e = 0; e < 16; ++e) {
           const int row = mm * 32 + (e & 3) + 8 * (e >> 2);
           const float v0 = acc[2 * pass + mm][e];
-          *reinterpret_cast<bf16_t*>(wst + row * 128) = f2bf(v0 + bias0);
+          *reinterpret_cast<bf16_t*>(wst + row * 128) = f2bf(relu ? fmaxf(v0 + bias0, 0.f) : v0 + bias0);
           const float e0 = v0 + c0s;
           S1 += e0;
           S2 = fmaf(e0, e0, S2);
@@ -1505,13 +1511,15 @@ int pcms_conv3_splits(int dtype, int Cin, int splits) {
 // bias, converts, and forms the BN statistics.
 int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
-                   float* yacc, float* stats, int accumulate,
+                   float* yacc, float* stats, int flags,
                    int N, int D, int H, int W, int Cout, int splits, hipStream_t s) {
+  const int accumulate = flags & PCMS_CONV_ACCUMULATE;
   const int Cin = c0 + c1;
   const int CK = pcms_conv3_chunk(dtype);
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0 || (c1 > 0 && x1 == nullptr)) return -1;
-  if (stats && accumulate) return -6;  // BN statistics describe a fresh output only
+  if (stats && flags) return -6;  // BN statistics describe a fresh, pre-activation output only
+  if (flags & ~(PCMS_CONV_ACCUMULATE | PCMS_CONV_RELU)) return -8;
   if (y1 == nullptr) cy0 = Cout;
   if (cy0 % 64 != 0 && cy0 != Cout) return -2;
   Box b = fwd_box(D, H, W);
@@ -1519,7 +1527,7 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1;
   p.w = wpack; p.bias = bias; p.y0 = y0; p.y1 = y1; p.cy0 = cy0;
   p.yacc = splits > 1 ? yacc : nullptr;
-  p.stats = stats; p.accumulate = accumulate;
+  p.stats = stats; p.accumulate = flags;
   p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
   p.nvox = (long)N * D * H * W;
   p.nchunk = cdiv(Cin, CK);

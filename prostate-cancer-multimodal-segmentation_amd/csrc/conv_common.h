@@ -72,7 +72,7 @@ struct Conv3Params {
   const void* w; const float* bias;
   void* y0; void* y1; int cy0;
   float* yacc; float* stats;
-  int accumulate;
+  int accumulate;        // PCMS_CONV_ACCUMULATE: y += conv; PCMS_CONV_RELU: y = relu(conv + b)
   int N, D, H, W, Cin, Cout;
   int nchunk, chunks_per_split;
   long nvox;             // N * D * H * W (split-K slab stride, in voxels)

@@ -118,6 +118,25 @@ __global__ void bn_finalize_kernel(const double* ws, int C, double count, const 
   }
 }
 
+// Eval-mode BatchNorm folded into the conv before it (UNet3D.predict / inference,
+// models/unet3d.py:298-344: BN over the running statistics is an affine map per output
+// channel): w' = w sc, b' = b sc + sh, sc / sh in fp64 as bn_eval_coeffs_kernel forms them.
+// w: [Cout][K] fp32 (torch layout, K = Cin x 27).
+__global__ void bn_fold_kernel(const float* w, const float* b, const float* gamma, const float* beta,
+                               const float* rmean, const float* rvar, float eps, int Cout, long K, float* wo,
+                               float* bo) {
+  const int co = blockIdx.y;
+  const double inv = 1.0 / sqrt((double)rvar[co] + (double)eps);
+  const double sc = (double)gamma[co] * inv;
+  const float scf = (float)sc;
+  for (long k = blockIdx.x * (long)blockDim.x + threadIdx.x; k < K; k += (long)gridDim.x * blockDim.x)
+    wo[(long)co * K + k] = w[(long)co * K + k] * scf;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const double sh = (double)beta[co] - (double)rmean[co] * sc;
+    bo[co] = (float)((b ? (double)b[co] : 0.0) * sc + sh);
+  }
+}
+
 __global__ void bn_eval_coeffs_kernel(const float* gamma, const float* beta, const float* rmean,
                                       const float* rvar, float eps, int C, float* scale, float* shift) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -146,7 +165,7 @@ __global__ void __launch_bounds__(TPB) bn_relu_kernel(const T* y, T* a, const fl
     float x[VEC];
     ld16<NT>(y + v * C + c0, x);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) x[j] = fmaxf(x[j] * sc[j] + sh[j], 0.f);
+    for (int j = 0; j < VEC; ++j) x[j] = bn_relu1(x[j], sc[j], sh[j]);
     st16<NT>(a + v * C + c0, x);
   }
 }
@@ -320,6 +339,146 @@ __global__ void maxpool_bwd_kernel(const T* a, const T* dp, T* da, int N, int D,
   }
 }
 
+// ---------------- encoder block output: BN + ReLU fused with the MaxPool3d of Down3D --------
+// (models/unet3d.py:37-39 of a DoubleConv, then :80 of the next Down3D.)  One thread per
+// (2x2x2 cell of the ceil-sized grid, VEC channels): a = round_T(relu(y sc + sh)) for the cell's
+// children is stored (the block output, read by the skip connection), and for whole cells the
+// max of those stored values (maxpool_fwd_kernel's scan order and NaN rule) -- the output is
+// pooled while it is in registers instead of being read back by a separate pass.
+template <typename T, bool NT>
+__global__ void __launch_bounds__(TPB) bn_relu_pool_kernel(const T* y, T* a, T* p, const float* scale,
+                                                           const float* shift, int N, int D, int H, int W,
+                                                           int C) {
+  constexpr int VEC = Elem<T>::kVec;
+  const int Dc = (D + 1) / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2, CV = C / VEC;
+  const int Do = D / 2, Ho = H / 2, Wo = W / 2;
+  const long total = (long)N * Dc * Hc * Wc * CV;
+  const long stride = (long)gridDim.x * blockDim.x;  // multiple of CV (host): cv is per thread
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int cv = (int)(i % CV);
+  float sc[VEC], sh[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) { sc[j] = scale[cv * VEC + j]; sh[j] = shift[cv * VEC + j]; }
+  for (; i < total; i += stride) {
+    uint32_t r = (uint32_t)(i / CV);  // 32-bit decomposition (host: cells < 2^31)
+    const int wc = r % Wc; r /= Wc;
+    const int hc = r % Hc; r /= Hc;
+    const int dc = r % Dc; const long n = r / Dc;
+    float m[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) m[j] = -INFINITY;
+    float v[8][VEC];
+    long vin[8];
+    bool in[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int d = 2 * dc + (k >> 2), h = 2 * hc + ((k >> 1) & 1), w = 2 * wc + (k & 1);
+      in[k] = d < D && h < H && w < W;
+      vin[k] = ((n * D + d) * H + h) * W + w;
+      if (in[k]) ld16<NT>(y + vin[k] * C + cv * VEC, v[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (!in[k]) continue;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) v[k][j] = round_st<T>(bn_relu1(v[k][j], sc[j], sh[j]));
+      st16<NT>(a + vin[k] * C + cv * VEC, v[k]);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (v[k][j] > m[j] || v[k][j] != v[k][j]) m[j] = v[k][j];
+    }
+    if (dc < Do && hc < Ho && wc < Wo) store16<T>(p + (((n * Do + dc) * Ho + hc) * Wo + wc) * C + cv * VEC, m);
+  }
+}
+
+// MaxPool3d backward fused with the BatchNorm + ReLU backward reduction of the block whose
+// output was pooled: da (the block output's gradient, already holding the skip-path part) +=
+// dp at the argmax of a = round_T(relu(y sc + sh)) -- a recomputed from y exactly as
+// bn_relu_pool_kernel stored it, maxpool_bwd_kernel's first-max / NaN rule -- and, over every
+// voxel (the floor-mode leftovers too), the partial sums of g = da [y sc + sh > 0] and g xhat
+// per channel: one [C][2] row per block (bn_relu_bwd_reduce_kernel's quantities), so the
+// BatchNorm backward needs no reduction pass over da and y of its own.
+template <typename T>
+__global__ void __launch_bounds__(TPB) maxpool_bwd_bn_kernel(const T* y, const float* scale, const float* shift,
+                                                             const float* mean, const float* invstd, const T* dp,
+                                                             T* da, float* part, int N, int D, int H, int W,
+                                                             int C) {
+  constexpr int VEC = Elem<T>::kVec;
+  __shared__ float red[TPB][VEC][2];
+  const int Dc = (D + 1) / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2, CV = C / VEC;
+  const int Do = D / 2, Ho = H / 2, Wo = W / 2;
+  const long total = (long)N * Dc * Hc * Wc * CV;
+  const long stride = (long)gridDim.x * blockDim.x;  // multiple of CV (host)
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int cv = (int)(i % CV);
+  float sc[VEC], sh[VEC], mu[VEC], is[VEC], sg[VEC], sgx[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    const int c = cv * VEC + j;
+    sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
+    sg[j] = 0.f; sgx[j] = 0.f;
+  }
+  for (; i < total; i += stride) {
+    uint32_t r = (uint32_t)(i / CV);
+    const int wc = r % Wc; r /= Wc;
+    const int hc = r % Hc; r /= Hc;
+    const int dc = r % Dc; const long n = r / Dc;
+    const bool whole = dc < Do && hc < Ho && wc < Wo;
+    float yv[8][VEC], g[VEC], m[VEC];
+    int arg[VEC];
+    long vin[8];
+    bool in[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int d = 2 * dc + (k >> 2), h = 2 * hc + ((k >> 1) & 1), w = 2 * wc + (k & 1);
+      in[k] = d < D && h < H && w < W;
+      vin[k] = ((n * D + d) * H + h) * W + w;
+      if (in[k]) load16<T>(y + vin[k] * C + cv * VEC, yv[k]);
+    }
+    if (whole) load16<T>(dp + (((n * Do + dc) * Ho + hc) * Wo + wc) * C + cv * VEC, g);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; arg[j] = 0; }
+    if (whole) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float av = round_st<T>(bn_relu1(yv[k][j], sc[j], sh[j]));
+          if (av > m[j] || (av != av && m[j] == m[j])) { m[j] = av; arg[j] = k; }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (!in[k]) continue;
+      float o[VEC];
+      load16<T>(da + vin[k] * C + cv * VEC, o);
+      if (whole) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o[j] += (arg[j] == k) ? g[j] : 0.f;
+        store16<T>(da + vin[k] * C + cv * VEC, o);
+      }
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float gg = (yv[k][j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
+        sg[j] += gg;
+        sgx[j] += gg * ((yv[k][j] - mu[j]) * is[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) { red[threadIdx.x][j][0] = sg[j]; red[threadIdx.x][j][1] = sgx[j]; }
+  __syncthreads();
+  // this block's row: channel c = cv' VEC + j sums threads t = cv' + CV k in t order
+  const int c0 = (int)(((long)blockIdx.x * blockDim.x) % CV);  // the cv of thread 0
+  for (int e = threadIdx.x; e < C * 2; e += TPB) {
+    const int c = e >> 1, q = e & 1, cvc = c / VEC, j = c % VEC;
+    const int t0 = (cvc - c0 + CV) % CV;
+    float acc = 0.f;
+    for (int t = t0; t < TPB; t += CV) acc += red[t][j][q];
+    part[((long)blockIdx.x * C + c) * 2 + q] = acc;
+  }
+}
+
 // ---------------- sum over a sub-box of an NDHWC tensor (ConvT bias grad) ----------
 // Block: 256 threads = (256 / CG) voxel lanes x CG groups of VEC channels; 16-byte loads,
 // LDS reduce over voxel lanes, one partial row [C] per block (summed in block order by
@@ -399,14 +558,28 @@ __global__ void __launch_bounds__(256) rows_sum_kernel(const float* part, int ro
 // 8 lanes per voxel, 8 channels each (Cin = 64).  act 0: logits; 1: sigmoid(logits)
 // (UNet3D.predict, models/unet3d.py:298-318); 2: (sigmoid(logits) > thr) as 0 / 1
 // (UNet3D.inference, :320-344) -- the eval outputs leave the head kernel finished.
-template <typename T, bool NT>
+// BN: ``a`` is the decoder's last pre-BN conv output y2 and the head applies that block's
+// BatchNorm + ReLU itself (models/unet3d.py:37-39 fused into :222): a = round_T(relu(y sc +
+// sh)), the value the bn_relu pass would have stored, so the logits are bit-identical and
+// the a2 tensor (the largest activation of the step) is never written or read.
+template <typename T, bool NT, bool BN>
 __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, float* logits,
-                                long nvox_per_n, int N, int ncls, int act, float thr) {
+                                long nvox_per_n, int N, int ncls, int act, float thr,
+                                const float* bn_scale, const float* bn_shift) {
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7;
+  float sc[8], sh[8];
+  if constexpr (BN) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = bn_scale[sub * 8 + j]; sh[j] = bn_shift[sub * 8 + j]; }
+  }
   auto load = [&](long v, float (&x)[8]) {
     ld16<NT>(a + v * 64 + sub * 8, x);
     if constexpr (sizeof(T) == 4) ld16<NT>(a + v * 64 + sub * 8 + 4, x + 4);
+    if constexpr (BN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = round_st<T>(bn_relu1(x[j], sc[j], sh[j]));
+    }
   };
   auto one = [&](long v, const float (&x)[8]) {
     const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
@@ -448,34 +621,67 @@ __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, floa
 // db[k] = sum_v dl
 // NT: non-temporal a / da streams (level-0 sized).  Two voxels per trip with both loads in
 // flight (accumulated in the same voxel order as one at a time: identical sums).
-template <typename T, bool NT>
+// BN (the decoder's last BatchNorm + ReLU fused, see head_fwd_kernel): ``a`` is y2; the head
+// input a2 = round_T(relu(y sc + sh)) is recomputed, da is NOT written: its round_T value
+// feeds the BatchNorm-backward partial sums directly -- per block one row [64][2] of
+// (sum g, sum g xhat), g = da [y sc + sh > 0], xhat = (y - mean) invstd -- and
+// head_bn_apply_kernel recomputes da from dlogits (rank ncls) instead of re-reading it.
+struct HeadBN {
+  const float *scale, *shift, *mean, *invstd;
+  float* part;  // [blocks][64][2]
+};
+template <typename T, bool NT, bool BN>
 __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* dlogits, const float* w,
-                                                       T* da, float* part, long nvox_per_n, int N, int ncls) {
+                                                       T* da, float* part, long nvox_per_n, int N, int ncls,
+                                                       HeadBN bn) {
   __shared__ float red[TPB / 64][4][65];
+  __shared__ float bred[TPB / 64][64][2];
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float accw[4][8], accb[4];
   for (int k = 0; k < 4; ++k) { accb[k] = 0.f; for (int j = 0; j < 8; ++j) accw[k][j] = 0.f; }
+  float sc[8], sh[8], mu[8], is[8], sg[8], sgx[8];
+  if constexpr (BN) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = sub * 8 + j;
+      sc[j] = bn.scale[c]; sh[j] = bn.shift[c]; mu[j] = bn.mean[c]; is[j] = bn.invstd[c];
+      sg[j] = 0.f; sgx[j] = 0.f;
+    }
+  }
   auto load = [&](long v, float (&x)[8]) {
     ld16<NT>(a + v * 64 + sub * 8, x);
     if constexpr (sizeof(T) == 4) ld16<NT>(a + v * 64 + sub * 8 + 4, x + 4);
   };
   auto one = [&](long v, const float (&x)[8]) {
-    float o[8];
+    float o[8], av[8];
     const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      o[j] = 0.f;
+      if constexpr (BN) av[j] = round_st<T>(bn_relu1(x[j], sc[j], sh[j]));
+      else av[j] = x[j];
+    }
     for (int k = 0; k < ncls && k < 4; ++k) {
       const float g = dlogits[(n * ncls + k) * nvox_per_n + vv];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         o[j] += g * w[k * 64 + sub * 8 + j];
-        accw[k][j] += g * x[j];
+        accw[k][j] += g * av[j];
       }
       if (sub == 0) accb[k] += g;
     }
-    st16<NT>(da + v * 64 + sub * 8, o);
-    if constexpr (sizeof(T) == 4) st16<NT>(da + v * 64 + sub * 8 + 4, o + 4);
+    if constexpr (BN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = (x[j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
+        sg[j] += g;
+        sgx[j] += g * ((x[j] - mu[j]) * is[j]);
+      }
+    } else {
+      st16<NT>(da + v * 64 + sub * 8, o);
+      if constexpr (sizeof(T) == 4) st16<NT>(da + v * 64 + sub * 8 + 4, o + 4);
+    }
   };
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
@@ -504,6 +710,16 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
     float sb = wave_sum(accb[k]);
     if (lane == 0) red[wave][k][64] = sb;
   }
+  if constexpr (BN) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s1 = sg[j], s2 = sgx[j];
+      s1 += __shfl_xor(s1, 8, 64); s2 += __shfl_xor(s2, 8, 64);
+      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 8) { bred[wave][sub * 8 + j][0] = s1; bred[wave][sub * 8 + j][1] = s2; }
+    }
+  }
   __syncthreads();
   // this block's partial row [ncls][65] (dw row k, then db[k]); rows_sum_kernel adds the
   // rows in block order
@@ -512,6 +728,73 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
     float s = 0.f;
     for (int wv = 0; wv < TPB / 64; ++wv) s += red[wv][k][c];
     part[(long)blockIdx.x * ncls * 65 + idx] = s;
+  }
+  if constexpr (BN) {
+    if (threadIdx.x < 128) {
+      const int c = threadIdx.x >> 1, q = threadIdx.x & 1;
+      float s = 0.f;
+      for (int wv = 0; wv < TPB / 64; ++wv) s += bred[wv][c][q];
+      bn.part[((long)blockIdx.x * 64 + c) * 2 + q] = s;
+    }
+  }
+}
+
+// BN-backward apply of the decoder's last BatchNorm + ReLU from the head's gradient, which is
+// recomputed per voxel from dlogits (da[v, c] = sum_k dl[k, v] w[k, c], rounded to T exactly as
+// head_bwd_kernel would have stored it) instead of being written and read back:
+// dy = k1 g + k2 xhat + k3, g = da [y sc + sh > 0] (bn_relu_bwd_apply_kernel's arithmetic).
+template <typename T, bool NT>
+__global__ void __launch_bounds__(TPB) head_bn_apply_kernel(const T* y, const float* dlogits, const float* w,
+                                                            const float* scale, const float* shift,
+                                                            const float* mean, const float* invstd,
+                                                            const float* coef, T* dy, long nvox_per_n, int N,
+                                                            int ncls) {
+  const long total = (long)N * nvox_per_n;
+  const int sub = threadIdx.x & 7;
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8], k3[8], wk[4][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = sub * 8 + j;
+    sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
+    k1[j] = coef[c * 3]; k2[j] = coef[c * 3 + 1]; k3[j] = coef[c * 3 + 2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wk[k][j] = k < ncls ? w[k * 64 + c] : 0.f;
+  }
+  auto one = [&](long v, const float (&x)[8]) {
+    const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = 0.f;
+    for (int k = 0; k < ncls && k < 4; ++k) {
+      const float g = dlogits[(n * ncls + k) * nvox_per_n + vv];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += g * wk[k][j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = (x[j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
+      o[j] = k1[j] * g + k2[j] * ((x[j] - mu[j]) * is[j]) + k3[j];
+    }
+    st16<NT>(dy + v * 64 + sub * 8, o);
+    if constexpr (sizeof(T) == 4) st16<NT>(dy + v * 64 + sub * 8 + 4, o + 4);
+  };
+  auto load = [&](long v, float (&x)[8]) {
+    ld16<NT>(y + v * 64 + sub * 8, x);
+    if constexpr (sizeof(T) == 4) ld16<NT>(y + v * 64 + sub * 8 + 4, x + 4);
+  };
+  const long stride = ((long)gridDim.x * blockDim.x) >> 3;
+  long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
+  for (; v + stride < total; v += 2 * stride) {
+    float x0[8], x1[8];
+    load(v, x0);
+    load(v + stride, x1);
+    one(v, x0);
+    one(v + stride, x1);
+  }
+  for (; v < total; v += stride) {
+    float x0[8];
+    load(v, x0);
+    one(v, x0);
   }
 }
 
@@ -673,7 +956,8 @@ __global__ void scale_kernel(float* g, long n, const float* mul) {
 constexpr int kMaxSplitSlabs = 16;  // slabs loaded together (more: summed one by one after)
 template <typename T>
 __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, int splits, const float* bias, T* y0,
-                                                             T* y1, int cy0, float* stats, int C, long nvox) {
+                                                             T* y1, int cy0, float* stats, int C, long nvox,
+                                                             int relu) {
   // stats row = (sum, M2 about the row mean), count row after the [rows][C][2] block
   constexpr int NV = TPB / 64, KPT = 64 / NV;
   __shared__ float red[NV][64][3];
@@ -701,6 +985,7 @@ __global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, i
       if (sp < splits) x += part[sp];
     for (int sp = kMaxSplitSlabs; sp < splits; ++sp) x += acc[((long)sp * nvox + v) * C + c];
     x += bc;
+    if (relu) x = fmaxf(x, 0.f);
     T* dst = c < cy0 ? y0 + v * cy0 + c : y1 + v * (C - cy0) + (c - cy0);
     Elem<T>::st(dst, x);
     xs[i] = x;
@@ -763,6 +1048,14 @@ __global__ void add_kernel(T* dst, const T* src, long nvec) {
   }
 }
 
+template <typename T, bool BN>
+void launch_head_fwd(bool nt, int grid, hipStream_t s, const void* a, const float* w, const float* b,
+                            float* out, long nvox_per_n, int N, int ncls, int act, float thr, const float* sc,
+                            const float* sh) {
+  hipLaunchKernelGGL((nt ? head_fwd_kernel<T, true, BN> : head_fwd_kernel<T, false, BN>), dim3(grid), dim3(TPB), 0,
+                     s, (const T*)a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+}
+
 }  // namespace
 
 extern "C" {
@@ -787,6 +1080,14 @@ int pcms_bn_finalize(const float* part, int rows, int C, double count, const flo
 }
 
 int pcms_bn_ws_doubles(int C) { return kRB * C * 2; }
+
+int pcms_bn_fold(const float* w, const float* b, const float* gamma, const float* beta, const float* rmean,
+                 const float* rvar, float eps, int Cout, long K, float* wo, float* bo, hipStream_t s) {
+  if (Cout <= 0 || K <= 0) return -1;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(grid_for(K, 256, 64), Cout), dim3(256), 0, s, w, b, gamma, beta, rmean, rvar,
+                     eps, Cout, K, wo, bo);
+  PCMS_CHECK_LAUNCH();
+}
 
 int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
                         int C, float* scale, float* shift, hipStream_t s) {
@@ -830,26 +1131,84 @@ int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scal
   const int rows = pcms_bn_bwd_rows(dtype, C, nvox);
   // the reduce keeps the default cache policy: what it leaves in the Infinity Cache the apply
   // pass below re-reads (measured: nt here 99 us but the apply 118 -> 135 us at level 0)
-  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL((bn_relu_bwd_reduce_kernel<bf16_t, false>), dim3(rows), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, part, C, nvox);
   else
     hipLaunchKernelGGL((bn_relu_bwd_reduce_kernel<float, false>), dim3(rows), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, part, C, nvox);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
+  return pcms_bn_relu_bwd_finish(dtype, da, y, scale, shift, mean, invstd, gamma, part, rows, coef, dgamma, dbeta,
+                                 dy, C, nvox, ws, s);
+}
+
+int pcms_bn_relu_bwd_finish(int dtype, const void* da, const void* y, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, const float* gamma, const float* part, int rows,
+                            float* coef, float* dgamma, float* dbeta, void* dy, int C, long nvox, double* ws,
+                            hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC || (TPB % (C / VEC)) != 0) return -1;
+  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C,
                      (const float*)nullptr, ws);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, s, (const double*)ws, C, (double)nvox,
                      gamma, invstd, dgamma, dbeta, coef);
   e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
+  if (e != hipSuccess || dy == nullptr) return (int)e;  // dy NULL: the consumer applies (coef)
   const int grid = ew_grid(dtype, C, nvox);
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL((nt ? bn_relu_bwd_apply_kernel<bf16_t, true> : bn_relu_bwd_apply_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0, s, (const bf16_t*)da, (const bf16_t*)y, scale, shift, mean, invstd, (const float*)coef, (bf16_t*)dy, C, nvox);
   else
     hipLaunchKernelGGL((nt ? bn_relu_bwd_apply_kernel<float, true> : bn_relu_bwd_apply_kernel<float, false>), dim3(grid), dim3(TPB), 0, s, (const float*)da, (const float*)y, scale, shift, mean, invstd, (const float*)coef, (float*)dy, C, nvox);
+  PCMS_CHECK_LAUNCH();
+}
+
+// grid of the cell kernels: a multiple of CV / gcd so every thread keeps one channel group
+static int cell_grid(long total, int CV, int cap) {
+  int g = grid_for(total, TPB, cap);
+  const int per = CV / std::__gcd(CV, TPB);  // blocks per period of cv
+  return std::max(per, g / per * per);
+}
+
+int pcms_bn_relu_pool(int dtype, const void* y, void* a, void* p, const float* scale, const float* shift, int N,
+                      int D, int H, int W, int C, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC) return -1;
+  const long cells = (long)N * ((D + 1) / 2) * ((H + 1) / 2) * ((W + 1) / 2);
+  if (cells * 8 >= (1L << 31)) return -7;  // 32-bit index math in the kernel
+  const int CV = C / VEC;
+  const int grid = cell_grid(cells * CV, CV, 8192);
+  const bool nt = (long)N * D * H * W * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((nt ? bn_relu_pool_kernel<bf16_t, true> : bn_relu_pool_kernel<bf16_t, false>), dim3(grid),
+                       dim3(TPB), 0, s, (const bf16_t*)y, (bf16_t*)a, (bf16_t*)p, scale, shift, N, D, H, W, C);
+  else
+    hipLaunchKernelGGL((nt ? bn_relu_pool_kernel<float, true> : bn_relu_pool_kernel<float, false>), dim3(grid),
+                       dim3(TPB), 0, s, (const float*)y, (float*)a, (float*)p, scale, shift, N, D, H, W, C);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_maxpool_bwd_bn_rows(int dtype, int N, int D, int H, int W, int C) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  const long cells = (long)N * ((D + 1) / 2) * ((H + 1) / 2) * ((W + 1) / 2);
+  return cell_grid(cells * (C / VEC), C / VEC, 2048);
+}
+
+int pcms_maxpool_bwd_bn(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                        const float* invstd, const void* dp, void* da, float* part, int N, int D, int H, int W,
+                        int C, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC || TPB % (C / VEC)) return -1;
+  const long cells = (long)N * ((D + 1) / 2) * ((H + 1) / 2) * ((W + 1) / 2);
+  if (cells * 8 >= (1L << 31)) return -7;
+  const int grid = pcms_maxpool_bwd_bn_rows(dtype, N, D, H, W, C);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_bn_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, scale, shift,
+                       mean, invstd, (const bf16_t*)dp, (bf16_t*)da, part, N, D, H, W, C);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_bn_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)y, scale, shift,
+                       mean, invstd, (const float*)dp, (float*)da, part, N, D, H, W, C);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -898,22 +1257,47 @@ int pcms_box_channel_sum(int dtype, const void* x, float* out, float* ws, int N,
   PCMS_CHECK_LAUNCH();
 }
 
-int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* out, long nvox_per_n, int N,
-                  int ncls, int act, float thr, hipStream_t s) {
+static int head_fwd_any(int dtype, const void* a, const float* w, const float* b, float* out, long nvox_per_n,
+                        int N, int ncls, int act, float thr, const float* sc, const float* sh, hipStream_t s) {
   if ((long)N * nvox_per_n >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   if (act < 0 || act > 2) return -1;
   const int grid = grid_for((long)N * nvox_per_n * 8, TPB);
   const bool nt = (long)N * nvox_per_n * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
-  if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL((nt ? head_fwd_kernel<bf16_t, true> : head_fwd_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0,
-                       s, (const bf16_t*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
-  else
-    hipLaunchKernelGGL((nt ? head_fwd_kernel<float, true> : head_fwd_kernel<float, false>), dim3(grid), dim3(TPB), 0, s,
-                       (const float*)a, w, b, out, nvox_per_n, N, ncls, act, thr);
+  const bool bn = sc != nullptr;
+  if (dtype == PCMS_BF16) {
+    if (bn) launch_head_fwd<bf16_t, true>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+    else launch_head_fwd<bf16_t, false>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+  } else {
+    if (bn) launch_head_fwd<float, true>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+    else launch_head_fwd<float, false>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+  }
   PCMS_CHECK_LAUNCH();
 }
 
+int pcms_head_fwd(int dtype, const void* a, const float* w, const float* b, float* out, long nvox_per_n, int N,
+                  int ncls, int act, float thr, hipStream_t s) {
+  return head_fwd_any(dtype, a, w, b, out, nvox_per_n, N, ncls, act, thr, nullptr, nullptr, s);
+}
+
+int pcms_head_bn_fwd(int dtype, const void* y, const float* scale, const float* shift, const float* w,
+                     const float* b, float* out, long nvox_per_n, int N, int ncls, int act, float thr,
+                     hipStream_t s) {
+  if (scale == nullptr || shift == nullptr) return -2;
+  return head_fwd_any(dtype, y, w, b, out, nvox_per_n, N, ncls, act, thr, scale, shift, s);
+}
+
 static int head_bwd_rows(long nvox) { return grid_for(nvox * 8, TPB, 2048); }
+
+// the head partial rows [grid][ncls][65] -> dw[k][c] += (k, c), db[k] += (k, 64)
+static int head_finish(int grid, float* ws, int ncls, float* dw, float* db, hipStream_t s) {
+  float* sums = ws + (long)grid * ncls * 65;
+  (void)hipMemsetAsync(sums, 0, sizeof(float) * ncls * 65, s);
+  hipLaunchKernelGGL(rows_sum_kernel, dim3(cdiv(ncls * 65, 8)), dim3(256), 0, s, (const float*)ws, grid, ncls * 65, sums);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(head_bwd_finish_kernel, dim3(1), dim3(320), 0, s, (const float*)sums, ncls, dw, db);
+  PCMS_CHECK_LAUNCH();
+}
 // workspace: the per-block partial rows + one summed row
 int pcms_head_bwd_ws_floats(long nvox_per_n, int N, int ncls) {
   return (head_bwd_rows((long)N * nvox_per_n) + 1) * ncls * 65;
@@ -926,20 +1310,57 @@ int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w
   if (ws == nullptr) return -2;
   const int grid = head_bwd_rows((long)N * nvox_per_n);
   const bool nt = (long)N * nvox_per_n * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  const HeadBN nobn{};
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL((nt ? head_bwd_kernel<bf16_t, true> : head_bwd_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0,
-                       s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, ws, nvox_per_n, N, ncls);
+    hipLaunchKernelGGL((nt ? head_bwd_kernel<bf16_t, true, false> : head_bwd_kernel<bf16_t, false, false>), dim3(grid),
+                       dim3(TPB), 0, s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, ws, nvox_per_n, N, ncls, nobn);
   else
-    hipLaunchKernelGGL((nt ? head_bwd_kernel<float, true> : head_bwd_kernel<float, false>), dim3(grid), dim3(TPB), 0, s,
-                       (const float*)a, dlogits, w, (float*)da, ws, nvox_per_n, N, ncls);
+    hipLaunchKernelGGL((nt ? head_bwd_kernel<float, true, false> : head_bwd_kernel<float, false, false>), dim3(grid),
+                       dim3(TPB), 0, s, (const float*)a, dlogits, w, (float*)da, ws, nvox_per_n, N, ncls, nobn);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  float* sums = ws + (long)grid * ncls * 65;
-  (void)hipMemsetAsync(sums, 0, sizeof(float) * ncls * 65, s);
-  hipLaunchKernelGGL(rows_sum_kernel, dim3(cdiv(ncls * 65, 8)), dim3(256), 0, s, (const float*)ws, grid, ncls * 65, sums);
-  e = hipGetLastError();
+  return head_finish(grid, ws, ncls, dw, db, s);
+}
+
+int pcms_head_bn_bwd_rows(long nvox_per_n, int N) { return head_bwd_rows((long)N * nvox_per_n); }
+
+int pcms_head_bn_bwd(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                     const float* invstd, const float* gamma, const float* dlogits, const float* w, float* dw,
+                     float* db, float* ws, float* bnpart, float* coef, float* dgamma, float* dbeta, void* dy,
+                     long nvox_per_n, int N, int ncls, double* bnws, hipStream_t s) {
+  if ((long)N * nvox_per_n >= (1L << 31)) return -7;  // 32-bit index math in the kernels
+  if (ncls > 4 || ncls < 1) return -1;
+  if (ws == nullptr || bnpart == nullptr || bnws == nullptr || coef == nullptr) return -2;
+  const long nvox = (long)N * nvox_per_n;
+  const int grid = head_bwd_rows(nvox);
+  const bool nt = nvox * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  const HeadBN bn{scale, shift, mean, invstd, bnpart};
+  // pass 1: head weight / bias partials + BatchNorm-backward partial sums (reads y2, dlogits)
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((head_bwd_kernel<bf16_t, false, true>), dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, dlogits,
+                       w, (bf16_t*)nullptr, ws, nvox_per_n, N, ncls, bn);
+  else
+    hipLaunchKernelGGL((head_bwd_kernel<float, false, true>), dim3(grid), dim3(TPB), 0, s, (const float*)y, dlogits, w,
+                       (float*)nullptr, ws, nvox_per_n, N, ncls, bn);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(head_bwd_finish_kernel, dim3(1), dim3(320), 0, s, (const float*)sums, ncls, dw, db);
+  if ((e = (hipError_t)head_finish(grid, ws, ncls, dw, db, s)) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(colsum2_kernel, dim3(1, kRB), dim3(256), 0, s, (const float*)bnpart, grid, 64,
+                     (const float*)nullptr, bnws);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(1), dim3(64), 0, s, (const double*)bnws, 64, (double)nvox, gamma,
+                     invstd, dgamma, dbeta, coef);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  // pass 2: dy of the BatchNorm input (reads y2, dlogits)
+  const int agrid = grid_for(nvox * 8, TPB);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((nt ? head_bn_apply_kernel<bf16_t, true> : head_bn_apply_kernel<bf16_t, false>), dim3(agrid),
+                       dim3(TPB), 0, s, (const bf16_t*)y, dlogits, w, scale, shift, mean, invstd, (const float*)coef,
+                       (bf16_t*)dy, nvox_per_n, N, ncls);
+  else
+    hipLaunchKernelGGL((nt ? head_bn_apply_kernel<float, true> : head_bn_apply_kernel<float, false>), dim3(agrid),
+                       dim3(TPB), 0, s, (const float*)y, dlogits, w, scale, shift, mean, invstd, (const float*)coef,
+                       (float*)dy, nvox_per_n, N, ncls);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -1000,12 +1421,14 @@ int pcms_grad_clip(float* g, long n, float gscale, float max_norm, int apply, do
 int pcms_split_epilogue_rows(long nvox) { return cdiv(nvox, 64); }
 
 int pcms_split_epilogue(int dtype, const float* acc, int splits, const float* bias, void* y0, void* y1, int cy0,
-                        float* stats, int C, long nvox, hipStream_t s) {
+                        float* stats, int C, long nvox, int flags, hipStream_t s) {
   if (C % 64 || splits < 1) return -1;
+  if (flags & ~PCMS_CONV_RELU || (stats && flags)) return -8;
+  const int relu = flags & PCMS_CONV_RELU;
   if (y1 == nullptr) cy0 = C;
   dim3 grid(cdiv(nvox, 64), C / 64);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(TPB), 0, s, acc, splits, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox);
-  else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(TPB), 0, s, acc, splits, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(TPB), 0, s, acc, splits, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox, relu);
+  else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(TPB), 0, s, acc, splits, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox, relu);
   PCMS_CHECK_LAUNCH();
 }
 

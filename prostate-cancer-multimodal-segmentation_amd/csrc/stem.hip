@@ -68,7 +68,9 @@ constexpr int kSDRed = kSDW + kStemSteps * 64 * 32;
 constexpr int kSDLds = kSDRed + 8 * 64 * 3 * 4;               // + stats reduction
 constexpr int kSDThr = 512;                                   // one 8-wave workgroup per CU
 
-template <int LBD, int LBH>
+// RELU: eval mode with the BatchNorm folded into the weights / bias (the output is the ReLU
+// activation; no statistics)
+template <int LBD, int LBH, bool RELU>
 __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
                                                                     uint32_t xbytes, uint32_t ybytes) {
   constexpr int NWV = kSDThr / 64;
@@ -174,7 +176,8 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   auto item_full = [&](f32x16_t (&acc)[2][2], int mt, int e, const uint32_t (&so)[2]) {
     const int g = e >> 2, rw = 4 * g + (e & 3);
     const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-    __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 2);
+    __builtin_amdgcn_raw_buffer_store_b32(RELU ? pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f)) : pack_bf16x2(v0, v1), yr,
+                                          (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 2);
     const float e0 = v0 - K[0], e1 = v1 - K[1];
     s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
     s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
@@ -205,7 +208,8 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         const uint32_t voff = valid ? (gB ? vB : vA) : kOOB;
         const float e0 = valid ? v0 - K[0] : 0.f, e1 = valid ? v1 - K[1] : 0.f;
         cnt += valid ? 1.f : 0.f;
-        __builtin_amdgcn_raw_buffer_store_b32(pack_bf16x2(v0, v1), yr, voff, so[mt] + rw * 128, 2);
+        __builtin_amdgcn_raw_buffer_store_b32(RELU ? pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f)) : pack_bf16x2(v0, v1),
+                                              yr, voff, so[mt] + rw * 128, 2);
         s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
         s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
       }
@@ -402,10 +406,22 @@ constexpr int kSWRing = kSWNS * SWGeom<kSWBD>::Buf;
 constexpr int kSWLds = kSWRing > 2 * kSWRegion ? kSWRing : 2 * kSWRegion;
 static_assert(kSWLds <= 160 * 1024, "ring / flush regions fit in LDS");
 
-template <int BD, int NS>
+// BN: the stem's BatchNorm + ReLU backward apply fused in (models/unet3d.py:29-33: inc's
+// conv.0 -> bn -> relu).  ``dy`` is then the gradient of the ReLU output (da) and ``bn.y``
+// the stem's pre-BN output: the ring receives the da tile by LDS-DMA as before, each thread
+// loads the y chunks it transforms into registers one box ahead (issued between the two
+// boxes' DMA, so the counted vmcnt waits are unchanged), and after the box's DMA has landed
+// the tile is rewritten in place as dy = k1 g + k2 xhat + k3, g = da [y sc + sh > 0]
+// (bn_relu_bwd_apply_kernel's arithmetic): the stem's dy is never stored in HBM (its only
+// consumer is this kernel: the input needs no gradient).
+struct StemBN {
+  const bf16_t* y;
+  const float *scale, *shift, *mean, *invstd, *coef;
+};
+template <int BD, int NS, bool BN>
 __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t* x, const bf16_t* dy, float* part,
                                                                     int N, int D, int H, int W, int cin_w,
-                                                                    uint32_t xbytes, uint32_t dybytes) {
+                                                                    uint32_t xbytes, uint32_t dybytes, StemBN bn) {
   typedef SWGeom<BD> Gm;
   constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
   constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
@@ -472,6 +488,59 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     }
   };
 
+  // BN transform: thread t rewrites rows r = 4 (t / 16 + 32 j) + 2 rs + b (j, b in {0, 1};
+  // rs = (t / 8) & 1) at physical 16-B slot q = t & 7 of the tile; dy_off_bf16's half swap
+  // depends on r & 2 = 2 rs only, so the slot holds the same 8 logical channels in all four
+  // rows and their coefficients stay in registers
+  constexpr int kTR = 4;
+  const int tq = tid & 7, trs = (tid >> 3) & 1, tb = tid >> 4;
+  const int tql = tq ^ (trs << 2);
+  float bsc[8], bsh[8], bmu[8], bis[8], bk1[8], bk2[8], bk3[8];
+  u32x4_t yreg[kTR];
+  auto trow = [&](int k) { return 4 * (tb + 32 * (k >> 1)) + 2 * trs + (k & 1); };
+  if constexpr (BN) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = tql * 8 + j;
+      bsc[j] = bn.scale[c]; bsh[j] = bn.shift[c]; bmu[j] = bn.mean[c]; bis[j] = bn.invstd[c];
+      bk1[j] = bn.coef[3 * c]; bk2[j] = bn.coef[3 * c + 1]; bk3[j] = bn.coef[3 * c + 2];
+    }
+  }
+  // y chunks of box b into registers (plain global loads: counted by vmcnt like the DMA)
+  auto load_y = [&](int b) {
+    int n, d0, h0, w0;
+    origin(b, n, d0, h0, w0);
+    const long vb = ((long)(n * D + d0) * H + h0) * W + w0;
+#pragma unroll
+    for (int k = 0; k < kTR; ++k) {
+      const int r = trow(k), rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
+      const bf16_t* src = bn.y + (vb + ((long)rd * H + rh) * W + rw) * 64 + tql * 8;
+      yreg[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src));
+    }
+  };
+  auto transform = [&](char* buf) {
+#pragma unroll
+    for (int k = 0; k < kTR; ++k) {
+      u32x4_t* cp = reinterpret_cast<u32x4_t*>(buf + trow(k) * 128 + tq * 16);
+      const u32x4_t gv = *cp;
+      float ga[8], yv[8], o[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ga[2 * i] = __uint_as_float(gv[i] << 16); ga[2 * i + 1] = __uint_as_float(gv[i] & 0xffff0000u);
+        yv[2 * i] = __uint_as_float(yreg[k][i] << 16); yv[2 * i + 1] = __uint_as_float(yreg[k][i] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gg = (yv[j] * bsc[j] + bsh[j] > 0.f) ? ga[j] : 0.f;
+        o[j] = bk1[j] * gg + bk2[j] * ((yv[j] - bmu[j]) * bis[j]) + bk3[j];
+      }
+      u32x4_t ov;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ov[i] = pack_bf16x2(o[2 * i], o[2 * i + 1]);
+      *cp = ov;
+    }
+  };
+
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
   f32x16_t acc[7];
 #pragma unroll
@@ -514,9 +583,12 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
 
   const int G = gridDim.x;
   int b = blockIdx.x;
+  static_assert(!BN || NS == 3, "the y loads sit between the DMA of two consecutive boxes");
 #pragma unroll
-  for (int k = 0; k < NS - 1; ++k)
+  for (int k = 0; k < NS - 1; ++k) {
     if (b + k * G < nbox) stage(b + k * G, k);
+    if (BN && k == 0 && b < nbox) load_y(b);  // order: DMA(b), y(b), DMA(b + G)
+  }
   for (int it = 0; b < nbox; b += G, ++it) {
     // retire box b's DMA (the NS - 2 boxes after it may stay in flight), then barrier:
     // every wave's share of box b has landed and every wave is done reading the slot
@@ -530,6 +602,14 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const int b2 = b + (NS - 1) * G;
+    if constexpr (BN) {
+      // box b's da tile and y chunks have landed: dy in place, then the next box's y loads
+      // (before the DMA of box b + 2 G: the wait above stays a count of that DMA alone)
+      transform(swl + (it % NS) * kSWBuf);
+      if (b + G < nbox) load_y(b + G);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     if (b2 < nbox) stage(b2, (it + NS - 1) % NS);
     compute(swl + (it % NS) * kSWBuf);
   }
@@ -647,8 +727,10 @@ int pcms_stem_fwd_rows(int N, int D, int H, int W) {
 
 // x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_stem_fwd_rows
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
-                  int N, int D, int H, int W, hipStream_t s) {
+                  int N, int D, int H, int W, int flags, hipStream_t s) {
   if (!stem_fwd_direct_shape(N, D, H, W)) return -5;
+  if (flags & ~PCMS_CONV_RELU || (stats && flags)) return -8;
+  const bool relu = flags & PCMS_CONV_RELU;
   const Box b = fwd_box(D, H, W);
   Conv3Params p;
   p.x0 = x; p.x1 = nullptr; p.c0 = 8; p.c1 = 0;
@@ -662,7 +744,8 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
   const int nbox = N * p.nbd * p.nbh * p.nbw;
   const long xbytes = p.nvox * 16, ybytes = p.nvox * 128;
   const int grid = std::min(nbox, device_cus());
-  auto kern = b.lbd == 2 ? stem_fwd_direct_kernel<2, 3> : stem_fwd_direct_kernel<3, 2>;
+  auto kern = b.lbd == 2 ? (relu ? stem_fwd_direct_kernel<2, 3, true> : stem_fwd_direct_kernel<2, 3, false>)
+                         : (relu ? stem_fwd_direct_kernel<3, 2, true> : stem_fwd_direct_kernel<3, 2, false>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSDLds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThr), kSDLds, s, p, nbox, nbox, (uint32_t)xbytes, (uint32_t)ybytes);
   PCMS_CHECK_LAUNCH();
@@ -677,24 +760,40 @@ int pcms_stem_wgrad_ws_floats(int N, int D, int H, int W, int cin_w) {
 
 // dw [64][cin_w][27] fp32 += stem weight gradient (x: 8-channel bf16 input, dy: 64 ch);
 // ws: pcms_stem_wgrad_ws_floats(...) floats (one partial row per workgroup, fixed-order sum)
-int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H, int W,
-                    hipStream_t s) {
+static int stem_wgrad_any(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H,
+                          int W, const StemBN& bn, hipStream_t s) {
   if (cin_w > 8 || cin_w < 1) return -1;
   if (!stem_wgrad_streams(N, D, H, W)) return -5;
   if (ws == nullptr) return -2;
   const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
   const int grid = std::min(nbox, device_cus());
   const long xbytes = (long)N * D * H * W * 16, dybytes = (long)N * D * H * W * 128;
-  auto kern = stem_wgrad_stream_kernel<kSWBD, kSWNS>;
+  auto kern = bn.y ? stem_wgrad_stream_kernel<kSWBD, kSWNS, true> : stem_wgrad_stream_kernel<kSWBD, kSWNS, false>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSWLds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT), kSWLds, s, (const bf16_t*)x, (const bf16_t*)dy, ws, N, D, H, W,
-                     cin_w, (uint32_t)xbytes, (uint32_t)dybytes);
+                     cin_w, (uint32_t)xbytes, (uint32_t)dybytes, bn);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int total = 64 * cin_w * 27;
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, (const float*)ws, grid, total,
                      dw);
   PCMS_CHECK_LAUNCH();
+}
+
+int pcms_stem_wgrad(const void* x, const void* dy, float* dw, float* ws, int cin_w, int N, int D, int H, int W,
+                    hipStream_t s) {
+  return stem_wgrad_any(x, dy, dw, ws, cin_w, N, D, H, W, StemBN{}, s);
+}
+
+// the same with the stem's BatchNorm + ReLU backward apply fused in: da = the gradient of the
+// stem block's first ReLU output, y = the stem's pre-BN output, BN forward coefficients and
+// coef = pcms_bn_relu_bwd's apply coefficients (k1, k2, k3 per channel)
+int pcms_stem_wgrad_bn(const void* x, const void* da, const void* y, const float* scale, const float* shift,
+                       const float* mean, const float* invstd, const float* coef, float* dw, float* ws, int cin_w,
+                       int N, int D, int H, int W, hipStream_t s) {
+  if (!y || !scale || !shift || !mean || !invstd || !coef) return -2;
+  return stem_wgrad_any(x, da, dw, ws, cin_w, N, D, H, W,
+                        StemBN{(const bf16_t*)y, scale, shift, mean, invstd, coef}, s);
 }
 
 }  // extern "C"

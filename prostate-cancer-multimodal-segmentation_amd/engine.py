@@ -125,6 +125,13 @@ class UNetEngine:
         self.wgrad_side_stream = False  # ablation: weight gradients on a side stream (measured 119.9 vs 121.6 vol/s: off)
         self._side_stream = None
         self._side_used = False
+        # eval mode: every BatchNorm folded into the conv before it (pcms_bn_fold) and the ReLU
+        # applied in the conv epilogue (PCMS_CONV_RELU): conv -> BN -> ReLU is one pass
+        # (models/unet3d.py:298-344 predict / inference).  False: the unfolded eval path.
+        self.fold_bn_eval = True
+        self._eval = None      # {conv index: (fwd pack, folded bias)}, "stem": stem pack
+        self._eval_key = None
+        self._bn_epoch = 0     # training forwards so far (each moves the running statistics)
         self._flatten()
         for bn in self.bns:
             c = bn.c
@@ -342,6 +349,55 @@ class UNetEngine:
         self._dirty = False
         self._packs_fresh = False
 
+    def _ensure_eval_packs(self):
+        """Folded eval weights: w' = w * gamma / sqrt(rvar + eps), b' = b * sc + beta - rmean * sc
+        per conv (pcms_bn_fold, then the forward pack of w'); rebuilt when the parameters or
+        the running statistics changed."""
+        self._ensure_packs()
+        key = (self.flat_p._version, self._packed_version, self.flat_bn._version, self._bn_epoch)
+        if self._eval is not None and self._eval_key == key:
+            return
+        if self._eval is None:
+            self._eval = {}
+            big = max(cs.cout * cs.cin * 27 for cs in self.convs)
+            self._eval_tmp = torch.empty(big, dtype=torch.float32, device=self.device)
+        ck = query("pcms_conv3_chunk", self.code)
+        tmp = self._eval_tmp
+        for i, (cs, bn) in enumerate(zip(self.convs, self.bns)):
+            if i not in self._eval:
+                nch = -(-cs.cin // ck)
+                self._eval[i] = (torch.empty(nch * 27 * cs.cout * ck, dtype=self.tdtype, device=self.device),
+                                 torch.empty(cs.cout, dtype=torch.float32, device=self.device))
+            pack, bias = self._eval[i]
+            m = bn.mod
+            call("pcms_bn_fold", cs.mod.weight, cs.mod.bias, m.weight, m.bias, m.running_mean, m.running_var,
+                 BN_EPS, cs.cout, cs.cin * 27, tmp, bias)
+            call("pcms_conv3_pack", self.code, tmp, pack, cs.cout, cs.cin, 0)
+            if i == 0 and self.stem_fast:
+                if "stem" not in self._eval:
+                    self._eval["stem"] = torch.empty(query("pcms_stem_pack_elems"), dtype=self.tdtype,
+                                                     device=self.device)
+                call("pcms_stem_pack", tmp, self._eval["stem"], self.nmod)
+        self._eval_key = key
+
+    def _conv_eval(self, i: int, x0, c0, x1, c1, a, N, S):
+        """a = relu(conv'(x) + b'): the folded eval conv of self.convs[i] (no statistics)."""
+        cs = self.convs[i]
+        pack, bias = self._eval[i]
+        RELU = 2  # PCMS_CONV_RELU
+        splits = self._splits(N, S, c0 + c1, cs.cout)
+        if i == 0 and self.stem_sup & 1:
+            call("pcms_stem_fwd", x0, self._eval["stem"], bias, a, None, N, S[0], S[1], S[2], RELU)
+        elif splits == 1:
+            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, pack, bias, a, None, cs.cout, None, None, RELU,
+                 N, S[0], S[1], S[2], cs.cout, 1)
+        else:
+            acc = self.bufs["yacc"]
+            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, pack, bias, a, None, cs.cout, acc, None, 0,
+                 N, S[0], S[1], S[2], cs.cout, splits)
+            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, c0 + c1, splits),
+                 bias, a, None, cs.cout, None, cs.cout, N * S[0] * S[1] * S[2], RELU)
+
     # ------------------------------------------------------------------ buffers
     def _levels(self, D, H, W):
         s = [(D, H, W)]
@@ -375,7 +431,9 @@ class UNetEngine:
                 b[f"e{l}_{k}"] = act(l, C[l])
         for l in range(4):
             for k in (("u", "a2") if self.act_ckpt else ("u", "y1", "a1", "y2", "a2")):
-                b[f"d{l}_{k}"] = act(l, C[l])
+                # the last decoder block's ReLU output is never stored: the head applies that
+                # BatchNorm + ReLU itself (pcms_head_bn_fwd / _bwd)
+                b[f"d{l}_{k}"] = act(l, C[l]) if (l, k) != (0, "a2") else None
         if self.act_ckpt:  # shared decoder set (level 0 is the largest: bytes per level ~ 4^-l)
             for k in ("y1", "a1", "y2"):
                 b[f"ck_{k}"] = act(0, C[0])
@@ -387,14 +445,17 @@ class UNetEngine:
             # second one while the side stream may still read gY; else an alias
             b[f"gZ{l}"] = act(l, C[l]) if self.wgrad_side_stream else b[f"gY{l}"]
             b[f"gU{l}"] = act(l, C[l])      # grad of up output / pooled input (scratch)
-        b["gH"] = act(0, C[0])              # grad of the decoder output (head input)
         # workspaces
         rows_f = max(max(query("pcms_conv3_mblocks", N, *S[l]) for l in range(5)),
                      query("pcms_stem_fwd_rows", N, *S[0]))
         rows_s = max(query("pcms_split_epilogue_rows", nv[l]) for l in range(5))
         rows_b = max(query("pcms_bn_bwd_rows", self.code, C[l], nv[l]) for l in range(5))
         # BN partials [rows][C][2] + [rows] voxel counts
-        b["stats"] = torch.empty(max(rows_f, rows_s, rows_b) * (1024 * 2 + 1), dtype=torch.float32, device=dev)
+        # (also the fused head's BatchNorm partial rows [rows_h][64][2])
+        rows_h = query("pcms_head_bn_bwd_rows", D * H * W, N)
+        rows_b = max([rows_b] + [query("pcms_maxpool_bwd_bn_rows", self.code, N, *S[l], C[l]) for l in range(4)])
+        b["stats"] = torch.empty(max(max(rows_f, rows_s, rows_b) * (1024 * 2 + 1), rows_h * 64 * 2),
+                                 dtype=torch.float32, device=dev)
         b["coef"] = torch.empty(3 * 1024, dtype=torch.float32, device=dev)
         b["bnws"] = torch.empty(query("pcms_bn_ws_doubles", 1024), dtype=torch.float64, device=dev)
         # weight-gradient workspace: per-split partial rows of the largest conv (and the stem)
@@ -451,7 +512,7 @@ class UNetEngine:
         st = b["stats"] if training and not recompute else None
         if cs is self.convs[0] and self.stem_sup & 1:
             with self._timed("stem_fwd"):
-                call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2])
+                call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2], 0)
             rows = query("pcms_stem_fwd_rows", N, *S)
         elif splits == 1:
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
@@ -462,7 +523,7 @@ class UNetEngine:
             call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  acc, None, 0, N, S[0], S[1], S[2], cs.cout, splits)
             call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, c0 + c1, splits),
-                 cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox)
+                 cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox, 0)
             rows = query("pcms_split_epilogue_rows", nvox)
         if recompute:
             return
@@ -479,15 +540,33 @@ class UNetEngine:
                  bn.scale, bn.shift)
 
     def _block_fwd(self, blk: BlockSpec, x0, c0, x1, c1, out: Dict[str, torch.Tensor], N, S, training,
-                   recompute: bool = False):
+                   recompute: bool = False, pool_out=None):
         """conv -> BN -> ReLU -> conv -> BN -> ReLU.  ``recompute`` (checkpointed decoder
         backward): y1, a1, y2 again from the same inputs with the forward's BN scale/shift; no
-        statistics, no running-stat update, a2 not rewritten."""
+        statistics, no running-stat update, a2 not rewritten.  ``out["a2"] is None``: the
+        second BN + ReLU is left to the consumer (the head: pcms_head_bn_fwd).  ``pool_out``
+        (encoder blocks 0-3): the output is max-pooled into it in the same pass (the next
+        Down3D's MaxPool3d, pcms_bn_relu_pool)."""
         nvox = N * S[0] * S[1] * S[2]
+        if not training and self.fold_bn_eval:
+            # eval: BN folded, ReLU in the epilogue; the last decoder block's output goes to its
+            # y2 buffer, which the plain head then reads (forward(): self._eval_folded)
+            i0 = self.convs.index(blk.c0)
+            a2 = out["a2"] if out["a2"] is not None else out["y2"]
+            self._conv_eval(i0, x0, c0, x1, c1, out["a1"], N, S)
+            self._conv_eval(i0 + 1, out["a1"], blk.c0.cout, None, 0, a2, N, S)
+            if pool_out is not None:
+                call("pcms_maxpool_fwd", self.code, a2, pool_out, N, *S, blk.c1.cout)
+            return
         self._conv(blk.c0, x0, c0, x1, c1, out["y1"], N, S, True, training, blk.b0, recompute)
         call("pcms_bn_relu", self.code, out["y1"], out["a1"], blk.b0.scale, blk.b0.shift, blk.c0.cout, nvox)
         self._conv(blk.c1, out["a1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1, recompute)
-        if not recompute:
+        if recompute or out["a2"] is None:
+            return
+        if pool_out is not None:
+            call("pcms_bn_relu_pool", self.code, out["y2"], out["a2"], pool_out, blk.b1.scale, blk.b1.shift, N, *S,
+                 blk.c1.cout)
+        else:
             call("pcms_bn_relu", self.code, out["y2"], out["a2"], blk.b1.scale, blk.b1.shift, blk.c1.cout, nvox)
 
     def _dec_acts(self, l: int) -> Dict[str, torch.Tensor]:
@@ -511,6 +590,11 @@ class UNetEngine:
             x = x.float()
         N, _, D, H, W = x.shape
         self._ensure_packs()
+        folded = not training and self.fold_bn_eval
+        if folded:
+            self._ensure_eval_packs()
+        else:
+            self._bn_epoch += training
         self._alloc(N, D, H, W)
         b = self.bufs
         S, C = b["S"], b["C"]
@@ -518,11 +602,11 @@ class UNetEngine:
         # encoder
         inp, cin = b["xin"], self.cp
         for l in range(5):
-            if l > 0:
-                call("pcms_maxpool_fwd", self.code, b[f"e{l - 1}_x"], b[f"pool{l}"], N, *S[l - 1], C[l - 1])
+            if l > 0:  # pool{l} was written by the previous block's fused BN + ReLU + MaxPool pass
                 inp, cin = b[f"pool{l}"], C[l - 1]
             out = {"y1": b[f"e{l}_y1"], "a1": b[f"e{l}_a1"], "y2": b[f"e{l}_y2"], "a2": b[f"e{l}_x"]}
-            self._block_fwd(self.enc[l], inp, cin, None, 0, out, N, S[l], training)
+            self._block_fwd(self.enc[l], inp, cin, None, 0, out, N, S[l], training,
+                            pool_out=b[f"pool{l + 1}"] if l < 4 else None)
         # decoder
         h = b["e4_x"]
         for i in range(4):
@@ -534,30 +618,56 @@ class UNetEngine:
             self._block_fwd(self.dec[i], b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], self._dec_acts(l), N, S[l],
                             training)
             h = b[f"d{l}_a2"]
+        # head = the last decoder block's BN + ReLU + outc 1x1x1 conv in one pass over its y2
         logits = torch.empty((N, self.ncls, D, H, W), dtype=torch.float32, device=self.device)
         oc = self.model.outc
-        call("pcms_head_fwd", self.code, h, oc.weight, oc.bias, logits, D * H * W, N, self.ncls, int(act),
-             float(threshold))
+        bn = self.dec[3].b1
+        if folded:  # the y2 buffer holds the folded conv's ReLU output
+            call("pcms_head_fwd", self.code, self._dec_acts(0)["y2"], oc.weight, oc.bias, logits, D * H * W, N,
+                 self.ncls, int(act), float(threshold))
+        else:
+            call("pcms_head_bn_fwd", self.code, self._dec_acts(0)["y2"], bn.scale, bn.shift, oc.weight, oc.bias,
+                 logits, D * H * W, N, self.ncls, int(act), float(threshold))
         self.epoch += 1
         if training:
             self.saved_epoch = self.epoch
         return logits
 
     # ------------------------------------------------------------------ backward
-    def _block_bwd(self, blk: BlockSpec, ga2, acts, x0, c0, x1, c1, gx_out0, gx_out1, cy0, N, S, lvl):
-        """Backward of one DoubleConv block. ga2: grad of block output.  Writes the grad of
-        the block input into gx_out0 (channels [0, cy0)) / gx_out1 (rest); None = skip."""
+    def _block_bwd(self, blk: BlockSpec, ga2, acts, x0, c0, x1, c1, gx_out0, gx_out1, cy0, N, S, lvl,
+                   bn1_rows: int = 0):
+        """Backward of one DoubleConv block. ga2: grad of block output (None: the second
+        BN + ReLU backward was already done by its consumer, gY{lvl} holds dy2).  Writes the
+        grad of the block input into gx_out0 (channels [0, cy0)) / gx_out1 (rest); None = skip.
+        ``bn1_rows``: the second BatchNorm's backward partial rows are already in the stats
+        buffer (written by pcms_maxpool_bwd_bn), only its finish + apply run here."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
         gY, gZ, gA = b[f"gY{lvl}"], b[f"gZ{lvl}"], b[f"gA{lvl}"]
         # BN1/ReLU backward -> dy2; its weight gradient on the side stream
-        self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
+        if ga2 is not None and bn1_rows:
+            m = blk.b1.mod
+            call("pcms_bn_relu_bwd_finish", self.code, ga2, acts["y2"], blk.b1.scale, blk.b1.shift, blk.b1.mean,
+                 blk.b1.invstd, m.weight, b["stats"], bn1_rows, b["coef"], m.weight.grad, m.bias.grad, gY, blk.b1.c,
+                 nvox, b["bnws"])
+        elif ga2 is not None:
+            self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         with self._side():
             call("pcms_conv3_wgrad", self.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
                  b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target)
         # dgrad conv1 -> grad of a1
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
         # BN0/ReLU backward -> dy1 (a second buffer: the side stream may still read gY)
+        if blk is self.enc[0] and self.stem_sup & 2:
+            # the stem: its BN0 apply runs inside the weight-gradient kernel (dy never stored)
+            bn = blk.b0
+            m = bn.mod
+            call("pcms_bn_relu_bwd", self.code, gA, acts["y1"], bn.scale, bn.shift, bn.mean, bn.invstd, m.weight,
+                 b["stats"], b["coef"], m.weight.grad, m.bias.grad, None, bn.c, nvox, b["bnws"])
+            with self._side(), self._timed("stem_wgrad"):
+                call("pcms_stem_wgrad_bn", x0, gA, acts["y1"], bn.scale, bn.shift, bn.mean, bn.invstd, b["coef"],
+                     blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
+            return
         self._bn_bwd(blk.b0, gA, acts["y1"], gZ, nvox)
         with self._side():
             if blk is self.enc[0] and self.stem_sup & 2:
@@ -587,7 +697,7 @@ class UNetEngine:
             call("pcms_conv3_fwd", self.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  acc, None, 0, N, *S, cs.cin, splits)
             call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, cs.cout, splits),
-                 None, out0, out1, cy0, None, cs.cin, nvox)
+                 None, out0, out1, cy0, None, cs.cin, nvox, 0)
 
     def backward(self, dlogits: torch.Tensor):
         if self.saved_epoch != self.epoch:
@@ -600,10 +710,16 @@ class UNetEngine:
         dlogits = dlogits.contiguous().float()
         oc = self.model.outc
         D, H, W = S[0]
-        call("pcms_head_bwd", self.code, b["d0_a2"], dlogits, oc.weight, b["gH"], oc.weight.grad, oc.bias.grad,
-             b["redws"], D * H * W, N, self.ncls)
+        # head + the last decoder block's BN + ReLU backward in two passes over its y2 (the
+        # forward's level-0 y2: under checkpointing the shared set still holds it, and the
+        # recompute below rewrites the same bits); dy2 -> gY0
+        bn = self.dec[3].b1
+        m = bn.mod
+        call("pcms_head_bn_bwd", self.code, self._dec_acts(0)["y2"], bn.scale, bn.shift, bn.mean, bn.invstd, m.weight,
+             dlogits, oc.weight, oc.weight.grad, oc.bias.grad, b["redws"], b["stats"], b["coef"], m.weight.grad,
+             m.bias.grad, b["gY0"], D * H * W, N, self.ncls, b["bnws"])
         self._grads_done("outc")
-        g = b["gH"]
+        g = None
         # decoder, last block first
         for i in reversed(range(4)):
             l = 3 - i
@@ -630,16 +746,22 @@ class UNetEngine:
                  up.out_channels, *S[l])
             g = gnext
         # encoder, deepest first; gx{l} holds the skip gradient already (l < 4)
+        rows = 0
         for l in reversed(range(5)):
             blk = self.enc[l]
             acts = {"y1": b[f"e{l}_y1"], "a1": b[f"e{l}_a1"], "y2": b[f"e{l}_y2"]}
             if l == 0:
-                self._block_bwd(blk, b["gx0"], acts, b["xin"], self.cp, None, 0, None, None, 0, N, S[0], 0)
+                self._block_bwd(blk, b["gx0"], acts, b["xin"], self.cp, None, 0, None, None, 0, N, S[0], 0,
+                                bn1_rows=rows)
                 self._grads_done("inc")
             else:
                 gp = b[f"gU{l}"]
                 self._block_bwd(blk, b[f"gx{l}"], acts, b[f"pool{l}"], C[l - 1], None, 0, gp, None, C[l - 1], N,
-                                S[l], l)
+                                S[l], l, bn1_rows=rows)
                 self._grads_done(f"down{l}")
-                call("pcms_maxpool_bwd", self.code, b[f"e{l - 1}_x"], gp, b[f"gx{l - 1}"], N, *S[l - 1], C[l - 1])
+                # MaxPool3d backward + the next block's second BN-backward reduction, one pass
+                bn = self.enc[l - 1].b1
+                call("pcms_maxpool_bwd_bn", self.code, b[f"e{l - 1}_y2"], bn.scale, bn.shift, bn.mean, bn.invstd, gp,
+                     b[f"gx{l - 1}"], b["stats"], N, *S[l - 1], C[l - 1])
+                rows = query("pcms_maxpool_bwd_bn_rows", self.code, N, *S[l - 1], C[l - 1])
         self.saved_epoch = -1

@@ -1,4 +1,6 @@
-"""Time the stem kernels (fwd / wgrad) at config 2 in isolation (for rocprofv3 PMC runs)."""
+"""Time the stem kernels (fwd / wgrad) at config 2 in isolation (for rocprofv3 PMC runs).
+``wgrad`` is the product's weight gradient: pcms_stem_wgrad_bn (the stem's BatchNorm-backward
+apply fused in: reads dA and the pre-BN Y instead of dY)."""
 import sys
 
 import torch
@@ -22,6 +24,8 @@ def main():
     bias = torch.zeros(64, device="cuda")
     stats = torch.empty(L.query("pcms_conv3_mblocks", N, D, H, W) * 129, device="cuda")
     dw = torch.zeros(64 * 5 * 27, device="cuda")
+    bnv = [torch.rand(64, device="cuda") + 0.5 for _ in range(4)]  # scale, shift, mean, invstd
+    coef = torch.randn(3 * 64, device="cuda") * 0.01
     ws = torch.empty(max(1, L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5)), device="cuda")
     for name in ("fwd", "wgrad", "calib"):
         if which not in ("both", name) and not (which == "all"):
@@ -31,9 +35,9 @@ def main():
             if name == "calib":
                 y.copy_(dy)          # 268 MB read + 268 MB write (torch copy kernel)
             elif name == "fwd":
-                L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W)
+                L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W, 0)
             else:
-                L.call("pcms_stem_wgrad", x, dy, dw, ws, 5, N, D, H, W)
+                L.call("pcms_stem_wgrad_bn", x, dy, y, *bnv, coef, dw, ws, 5, N, D, H, W)
         for i in range(3):
             f(i)
         torch.cuda.synchronize()
@@ -44,7 +48,8 @@ def main():
         e1.record()
         e1.synchronize()
         t = e0.elapsed_time(e1) / reps * 1e-3
-        byts = nvox * 5 * 2 + nvox * 64 * 2 if name != "calib" else 2 * nvox * 64 * 2
+        byts = {"fwd": nvox * 5 * 2 + nvox * 64 * 2, "wgrad": nvox * 5 * 2 + 2 * nvox * 64 * 2,
+                "calib": 2 * nvox * 64 * 2}[name]
         print(f"stem {name}: {t * 1e6:.1f} us  {byts / t / 1e9:.0f} GB/s algorithmic", flush=True)
     if which in ("all", "calib"):
         x, y, dy = sets[0]

@@ -39,7 +39,7 @@ def main():
     # correctness: ws vs product
     x, y1, _ = sets[0]
     y2 = torch.empty_like(y1)
-    L.call("pcms_stem_fwd", x, wp, bias, y1, st1, N, D, H, W)
+    L.call("pcms_stem_fwd", x, wp, bias, y1, st1, N, D, H, W, 0)
     rc = ex.exp_stem_fwd_ws(0, P(x), P(wp), P(bias), P(y2), P(st2), P(err), N, D, H, W, st())
     torch.cuda.synchronize()
     print("ws rc", rc, "err", err.tolist(), "y equal:", torch.equal(y1.view(torch.int16), y2.view(torch.int16)),
@@ -73,7 +73,7 @@ def main():
         print(f"{name:48s} {t * 1e6:8.1f} us {nbytes / t / 1e9:7.0f} GB/s", flush=True)
         return t
     fb = nvox * 10 + nvox * 128
-    bench("fwd product (direct)", lambda i: L.call("pcms_stem_fwd", sets[i][0], wp, bias, sets[i][1], st1, N, D, H, W), fb)
+    bench("fwd product (direct)", lambda i: L.call("pcms_stem_fwd", sets[i][0], wp, bias, sets[i][1], st1, N, D, H, W, 0), fb)
     for mode, label in [(0, ""), (1, " no BN sums"), (2, " no MFMA"), (3, " no BN sums, no MFMA")]:
         bench("fwd ws (4 compute + 4 memory waves)" + label,
               lambda i, m=mode: ex.exp_stem_fwd_ws(m, P(sets[i][0]), P(wp), P(bias), P(sets[i][1]), P(st2), P(err), N, D,
@@ -82,7 +82,7 @@ def main():
     # v3: correctness vs product, then timing
     y3 = torch.empty_like(y1)
     st3 = torch.zeros(rows * 129, device="cuda")
-    L.call("pcms_stem_fwd", x, wp, bias, y1, st1, N, D, H, W)
+    L.call("pcms_stem_fwd", x, wp, bias, y1, st1, N, D, H, W, 0)
     rc = ex.exp_stem_fwd_v3(0, P(x), P(wp), P(bias), P(y3), P(st3), N, D, H, W, st())
     torch.cuda.synchronize()
     m3, v3, c3 = mom(st3)

@@ -35,7 +35,7 @@ def main():
     tl = torch.zeros(256 * 8 * nb * 8, dtype=torch.int64, device="cuda")
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     y1 = torch.empty_like(ys[0])
-    L.call("pcms_stem_fwd", x, wp, bias, y1, st, N, D, H, W)
+    L.call("pcms_stem_fwd", x, wp, bias, y1, st, N, D, H, W, 0)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rep in range(12):
         if rep == 11:

@@ -32,6 +32,10 @@ def main():
     write, nw = means(os.path.join(d, "write"), "WRITE_SIZE")
     total = 2 * sum(fetch.values()) * 1024 + sum(write.values()) * 1024
     rec = {"shape": [2, 128, 128, 64], "kernels": list(KERNELS.values()),
+           # the roofline kernel string bench.py reports for this pair (it uses the record only
+           # when they match)
+           "kernel": "stem conv3d 5->64 fwd + wgrad with the BN0 backward apply fused in (stem_fwd_direct_kernel + "
+                     "stem_wgrad_stream_kernel<BN>)",
            "FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "dispatches": {"fetch": nf, "write": nw},
            "correction": "FETCH_SIZE x2 (gfx950 reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md "
                          "HBM section); WRITE_SIZE as reported",

@@ -136,6 +136,45 @@ def test_predict_and_inference_head_kernel():
     assert not m.training
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_eval_bn_folding(precision):
+    """Eval mode folds every BatchNorm into the conv before it (w sc, b sc + sh) with the ReLU
+    in the conv epilogue (models/unet3d.py:298-344).  Folded vs the unfolded eval
+    path of the same engine: fp32 within 1e-5 (one fp32 rounding of w sc and of the folded
+    bias), bf16 within the bf16 bar; both vs the oracle's eval forward.  The folded packs are
+    rebuilt after a training step moved the running statistics."""
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    torch.manual_seed(4)
+    m = UNet3D(n_modalities=5, n_classes=1, precision=precision).cuda()
+    x = torch.rand(2, 5, 32, 32, 16)
+    y = (torch.rand(2, 1, 32, 32, 16) < 0.4).float()
+    eng = m.engine()
+    opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
+    for step in range(2):
+        m.train()
+        opt.zero_grad()
+        BCEDiceLoss()(m(x.cuda()), y.cuda()).backward()
+        opt.step()
+        m.eval()
+        with torch.no_grad():
+            eng.fold_bn_eval = True
+            lf = m(x.cuda()).cpu()
+            eng.fold_bn_eval = False
+            lu = m(x.cuda()).cpu()
+            eng.fold_bn_eval = True
+        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        lr = ref.forward(sd, x, training=False)
+        scale = float(lr.abs().max())
+        if precision == "fp32":
+            assert float((lf - lu).abs().max()) <= 1e-5 * max(scale, 1.0), step
+            assert float((lf - lr).abs().max()) <= ATOL, step
+        else:
+            e_f, e_u = float((lf - lr).abs().max()), float((lu - lr).abs().max())
+            assert e_f <= 2 * e_u + 1e-2, (step, e_f, e_u)
+
+
 def test_predictor_pipeline(tmp_path):
     from pcms_amd.data import read_nifti, read_nifti_header, write_nifti
     from pcms_amd.predict import MODALITIES, ModelPredictor, load_multimodal_images, preprocess_image

@@ -100,14 +100,14 @@ def test_conv3_fwd(dt, code, tol, N, cin, cout, S, split):
         acc = torch.full((ns * nvox * cout,), float("nan"), device=DEV)
         L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, acc, None, 0,
                N, *S, cout, split)
-        L.call("pcms_split_epilogue", code, acc, ns, b.to(DEV), y, None, cout, stats, cout, nvox)
+        L.call("pcms_split_epilogue", code, acc, ns, b.to(DEV), y, None, cout, stats, cout, nvox, 0)
         rows = L.query("pcms_split_epilogue_rows", nvox)
         # split-K sums its slabs in a fixed order: a second run is bit-identical
         y2 = torch.empty_like(y)
         stats2 = torch.zeros_like(stats)
         L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wpack, b.to(DEV), y2, None, cout, acc, None, 0,
                N, *S, cout, split)
-        L.call("pcms_split_epilogue", code, acc, ns, b.to(DEV), y2, None, cout, stats2, cout, nvox)
+        L.call("pcms_split_epilogue", code, acc, ns, b.to(DEV), y2, None, cout, stats2, cout, nvox, 0)
         torch.cuda.synchronize()
         assert torch.equal(y.view(torch.uint8), y2.view(torch.uint8))
         assert torch.equal(stats, stats2)
@@ -147,7 +147,7 @@ def test_bn_stats_large_mean(N, S, split):
         acc = torch.empty(ns * nvox * cout, device=DEV)
         L.call("pcms_conv3_fwd", 0, xd, cin, None, 0, wpack, b.to(DEV), y, None, cout, acc, None, 0,
                N, *S, cout, split)
-        L.call("pcms_split_epilogue", 0, acc, ns, b.to(DEV), y, None, cout, stats, cout, nvox)
+        L.call("pcms_split_epilogue", 0, acc, ns, b.to(DEV), y, None, cout, stats, cout, nvox, 0)
     torch.cuda.synchronize()
     mean, var = bn_moments(stats, rows, cout, nvox)
     yref = ref.transpose(0, 1).reshape(cout, -1)
@@ -359,7 +359,75 @@ def test_maxpool_fwd_bwd(dt, code, tol):
 
 
 @pytest.mark.parametrize("dt,code,tol", DTS)
-@pytest.mark.parametrize("Sin,Sout,cin,cout", [((4, 4, 2), (8, 8, 4), 128, 64), ((2, 2, 3), (5, 4, 7), 128, 64),
+@pytest.mark.parametrize("S,C", [((8, 6, 10), 64), ((7, 5, 9), 128), ((3, 4, 5), 512)])
+def test_bn_relu_pool_and_maxpool_bwd_bn(dt, code, tol, S, C):
+    """Down3D boundary fusion vs the unfused passes on the same inputs, odd (floor-mode)
+    sizes included: pcms_bn_relu_pool == pcms_bn_relu + pcms_maxpool_fwd bit for bit;
+    pcms_maxpool_bwd_bn leaves the same da as pcms_maxpool_bwd (bit for bit) and its BN
+    partial rows, finished by pcms_bn_relu_bwd_finish, give pcms_bn_relu_bwd's dy / dgamma /
+    dbeta up to summation order; and the whole chain against fp64 autograd of
+    maxpool(relu(batch_norm(y)))."""
+    L = _lib()
+    g = torch.Generator().manual_seed(6)
+    N = 2
+    nvox = N * S[0] * S[1] * S[2]
+    y = (torch.randn(N, C, *S, generator=g) * 1.5).to(dt)
+    y[:, :, :2, :2, :2] = -3.0  # ReLU ties at zero inside a pooling cell
+    y = y.to(dt)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.1
+    P = tuple(s // 2 for s in S)
+    dp = torch.randn(N, C, *P, generator=g).to(dt)
+    skip = torch.randn(N, C, *S, generator=g).to(dt)   # the skip-path part of the output gradient
+    yr = y.double().requires_grad_(True)
+    gr, brr = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    a_ref = F.relu(F.batch_norm(yr, None, None, gr, brr, True, 0.1, 1e-5))
+    p_ref = F.max_pool3d(a_ref, 2)
+    torch.autograd.backward([p_ref, a_ref], [dp.double(), skip.double()])
+    m = y.double().mean((0, 2, 3, 4))
+    inv = 1.0 / torch.sqrt(y.double().var((0, 2, 3, 4), unbiased=False) + 1e-5)
+    sc = (gamma.double() * inv).float().to(DEV)
+    sh = (beta.double() - m * gamma.double() * inv).float().to(DEV)
+    mean, invstd, gd = m.float().to(DEV), inv.float().to(DEV), gamma.to(DEV)
+    yd, dpd = ndhwc(y).to(DEV), ndhwc(dp).to(DEV)
+    # forward
+    a0, p0 = torch.empty_like(yd), torch.empty(N, *P, C, dtype=dt, device=DEV)
+    L.call("pcms_bn_relu", code, yd, a0, sc, sh, C, nvox)
+    L.call("pcms_maxpool_fwd", code, a0, p0, N, *S, C)
+    a1, p1 = torch.full_like(a0, float("nan")), torch.full_like(p0, float("nan"))
+    L.call("pcms_bn_relu_pool", code, yd, a1, p1, sc, sh, N, *S, C)
+    # backward
+    rows = max(L.query("pcms_bn_bwd_rows", code, C, nvox), L.query("pcms_maxpool_bwd_bn_rows", code, N, *S, C))
+    part = torch.empty(rows * C * 2, device=DEV)
+    coef = torch.empty(3 * C, device=DEV)
+    bnws = torch.empty(L.query("pcms_bn_ws_doubles", C), dtype=torch.float64, device=DEV)
+    da0 = ndhwc(skip).to(DEV)
+    L.call("pcms_maxpool_bwd", code, a0, dpd, da0, N, *S, C)
+    dg0, db0, dy0 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.empty_like(yd)
+    L.call("pcms_bn_relu_bwd", code, da0, yd, sc, sh, mean, invstd, gd, part, coef, dg0, db0, dy0, C, nvox, bnws)
+    da1 = ndhwc(skip).to(DEV)
+    L.call("pcms_maxpool_bwd_bn", code, yd, sc, sh, mean, invstd, dpd, da1, part, N, *S, C)
+    r1 = L.query("pcms_maxpool_bwd_bn_rows", code, N, *S, C)
+    dg1, db1, dy1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.full_like(yd, float("nan"))
+    L.call("pcms_bn_relu_bwd_finish", code, da1, yd, sc, sh, mean, invstd, gd, part, r1, coef, dg1, db1, dy1, C, nvox,
+           bnws)
+    torch.cuda.synchronize()
+    assert torch.equal(a0, a1) and torch.equal(p0, p1)
+    assert torch.equal(da0, da1)
+    close(dg1.cpu(), dg0.cpu(), 1e-5, "dgamma fused vs unfused")
+    close(db1.cpu(), db0.cpu(), 1e-5, "dbeta fused vs unfused")
+    close(ncdhw(dy1.cpu()), ncdhw(dy0.cpu()), 1e-5 if not code else 1e-2, "dy fused vs unfused")
+    close(ncdhw(p1.cpu()), p_ref.detach(), 1e-5 if not code else 1e-2, "pool vs fp64")
+    if code == 0:  # bf16: rounding makes ties among a cell's outputs, so the argmax (and with
+        # it where dp lands) legitimately differs from the fp64 run; the fused == unfused checks
+        # above are the bf16 bar
+        close(ncdhw(dy1.cpu()), yr.grad, 1e-4, "dy vs fp64")
+        close(dg1.cpu(), gr.grad, 1e-4, "dgamma vs fp64")
+        close(db1.cpu(), brr.grad, 1e-4, "dbeta vs fp64")
+
+
+@pytest.mark.parametrize("dt,code,tol", DTS)
+@pytest.mark.parametrize("Sin,Sout,cin,cout",[((4, 4, 2), (8, 8, 4), 128, 64), ((2, 2, 3), (5, 4, 7), 128, 64),
                                                ((8, 8, 6), (16, 16, 12), 256, 128),  # > 1 tile, 2 co chunks
                                                ((8, 8, 4), (16, 16, 8), 1024, 512)])  # level 4 (split dgrad)
 def test_convt(dt, code, tol, Sin, Sout, cin, cout):
@@ -450,6 +518,78 @@ def test_head(dt, code, tol, ncls):
     close(db.cpu(), br.grad, 1e-5, "head bias grad")
 
 
+@pytest.mark.parametrize("dt,code,tol", DTS)
+@pytest.mark.parametrize("ncls", [1, 2])
+def test_head_bn_fused(dt, code, tol, ncls):
+    """The last decoder block's BN + ReLU fused into the head (pcms_head_bn_fwd / _bwd) vs
+    the unfused sequence (pcms_bn_relu -> pcms_head_fwd; pcms_head_bwd -> pcms_bn_relu_bwd):
+    bit-identical logits and head weight / bias gradients, the BatchNorm gradients and dy
+    equal up to the BN partial sums' order; and both against fp64 autograd of
+    relu(batch_norm(y)) -> conv1x1."""
+    L = _lib()
+    g = torch.Generator().manual_seed(4)
+    N, S, C = 2, (6, 5, 8), 64
+    V = S[0] * S[1] * S[2]
+    nvox = N * V
+    y = (torch.randn(N, C, *S, generator=g) * 2 + 0.3).to(dt)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.1
+    w = torch.randn(ncls, 64, 1, 1, 1, generator=g) * 0.1
+    b = torch.randn(ncls, generator=g)
+    dl = torch.randn(N, ncls, *S, generator=g)
+    # fp64 reference
+    yr = y.double().requires_grad_(True)
+    gr, brr = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    wr, br = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    out = F.conv3d(F.relu(F.batch_norm(yr, None, None, gr, brr, True, 0.1, 1e-5)), wr, br)
+    out.backward(dl.double())
+    # device: BN statistics -> scale / shift / mean / invstd (pcms_bn_finalize from exact partials)
+    yd = ndhwc(y).to(DEV)
+    m = y.double().mean((0, 2, 3, 4))
+    var = y.double().var((0, 2, 3, 4), unbiased=False)
+    inv = 1.0 / torch.sqrt(var + 1e-5)
+    sc = (gamma.double() * inv).float().to(DEV)
+    sh = (beta.double() - m * gamma.double() * inv).float().to(DEV)
+    mean, invstd = m.float().to(DEV), inv.float().to(DEV)
+    W2, bd, dld = w.reshape(ncls, 64).to(DEV), b.to(DEV), dl.to(DEV)
+    gd = gamma.to(DEV)
+    # unfused
+    a = torch.empty_like(yd)
+    L.call("pcms_bn_relu", code, yd, a, sc, sh, C, nvox)
+    lg0 = torch.empty(N, ncls, *S, device=DEV)
+    L.call("pcms_head_fwd", code, a, W2, bd, lg0, V, N, ncls, 0, 0.5)
+    ws = torch.empty(L.query("pcms_head_bwd_ws_floats", V, N, ncls), device=DEV)
+    da = torch.empty_like(yd)
+    dw0, db0 = torch.zeros(ncls, 64, device=DEV), torch.zeros(ncls, device=DEV)
+    L.call("pcms_head_bwd", code, a, dld, W2, da, dw0, db0, ws, V, N, ncls)
+    rows = max(L.query("pcms_bn_bwd_rows", code, C, nvox), L.query("pcms_head_bn_bwd_rows", V, N))
+    part = torch.empty(rows * C * 2, device=DEV)
+    coef = torch.empty(3 * C, device=DEV)
+    bnws = torch.empty(L.query("pcms_bn_ws_doubles", C), dtype=torch.float64, device=DEV)
+    dg0, dbt0 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dy0 = torch.empty_like(yd)
+    L.call("pcms_bn_relu_bwd", code, da, yd, sc, sh, mean, invstd, gd, part, coef, dg0, dbt0, dy0, C, nvox, bnws)
+    # fused
+    lg1 = torch.empty_like(lg0)
+    L.call("pcms_head_bn_fwd", code, yd, sc, sh, W2, bd, lg1, V, N, ncls, 0, 0.5)
+    dw1, db1 = torch.zeros_like(dw0), torch.zeros_like(db0)
+    dg1, dbt1 = torch.zeros_like(dg0), torch.zeros_like(dbt0)
+    dy1 = torch.full_like(yd, float("nan"))
+    L.call("pcms_head_bn_bwd", code, yd, sc, sh, mean, invstd, gd, dld, W2, dw1, db1, ws, part, coef, dg1, dbt1,
+           dy1, V, N, ncls, bnws)
+    torch.cuda.synchronize()
+    assert torch.equal(lg0, lg1)
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+    close(dg1.cpu(), dg0.cpu(), 1e-5, "dgamma fused vs unfused")
+    close(dbt1.cpu(), dbt0.cpu(), 1e-5, "dbeta fused vs unfused")
+    close(ncdhw(dy1.cpu()), ncdhw(dy0.cpu()), 1e-5 if not code else 1e-2, "dy fused vs unfused")
+    close(lg1.cpu(), out.detach(), 1e-5 if not code else 2e-2, "fused logits vs fp64")
+    close(ncdhw(dy1.cpu()), yr.grad, 1e-4 if not code else 3e-2, "fused dy vs fp64")
+    close(dg1.cpu(), gr.grad, 1e-4 if not code else 3e-2, "fused dgamma vs fp64")
+    close(dbt1.cpu(), brr.grad, 1e-4 if not code else 3e-2, "fused dbeta vs fp64")
+    close(dw1.cpu(), wr.grad.reshape(ncls, 64), 1e-5 if not code else 2e-2, "fused head wgrad vs fp64")
+
+
 @pytest.mark.parametrize("wb,wd", [(0.0, 1.0), (0.5, 0.5)])
 def test_loss(wb, wd):
     L = _lib()
@@ -523,7 +663,7 @@ def test_stem_fwd_wgrad_bf16(N, S):
         assert sup == 3, (S, sup)
     if sup == 0:
         with pytest.raises(L.HipError):
-            L.call("pcms_stem_fwd", None, None, None, None, None, N, *S)
+            L.call("pcms_stem_fwd", None, None, None, None, None, N, *S, 0)
         return
     g = torch.Generator().manual_seed(sum(S))
     x = torch.rand(N, 5, *S, generator=g).to(torch.bfloat16)
@@ -543,7 +683,7 @@ def test_stem_fwd_wgrad_bf16(N, S):
         y = torch.empty(N, *S, 64, dtype=torch.bfloat16, device=DEV)
         rows = L.query("pcms_stem_fwd_rows", N, *S)
         stats = torch.zeros(rows * (64 * 2 + 1), device=DEV)
-        L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y, stats, N, *S)
+        L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y, stats, N, *S, 0)
         torch.cuda.synchronize()
         close(ncdhw(y.cpu()), ref.detach(), 1e-2, "stem fwd")
         mean, var = bn_moments(stats, rows, 64, N * S[0] * S[1] * S[2])
@@ -558,6 +698,60 @@ def test_stem_fwd_wgrad_bf16(N, S):
         torch.cuda.synchronize()
         assert dw[-guard:].abs().max().item() == 0.0
         close(dw[:-guard].cpu().view(64, 5, 3, 3, 3), wr.grad, 1e-4, "stem wgrad")
+
+
+@pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (3, (4, 4, 16)), (1, (12, 16, 32)), (2, (32, 64, 64))])
+def test_stem_wgrad_bn_fused(N, S):
+    """The stem's BatchNorm + ReLU backward apply fused into its weight gradient
+    (pcms_stem_wgrad_bn) vs the unfused pair (pcms_bn_relu_bwd's apply pass -> dy in HBM ->
+    pcms_stem_wgrad) on the same bf16 inputs -- the in-LDS dy uses the apply kernel's
+    arithmetic, so the weight gradients agree to fp32 summation noise -- and vs fp64 autograd of
+    conv3d -> batch_norm -> relu."""
+    L = _lib()
+    assert L.query("pcms_stem_supported", N, *S) & 2
+    g = torch.Generator().manual_seed(11 + sum(S))
+    nvox = N * S[0] * S[1] * S[2]
+    x = torch.rand(N, 5, *S, generator=g).to(torch.bfloat16)
+    w = torch.randn(64, 5, 3, 3, 3, generator=g) * 0.2
+    gamma = torch.rand(64, generator=g) + 0.5
+    beta = torch.randn(64, generator=g) * 0.1
+    xs = torch.zeros(N, 8, *S, dtype=torch.bfloat16)
+    xs[:, :5] = x
+    xd = ndhwc(xs).to(DEV)
+    y = F.conv3d(x.double(), w.to(torch.bfloat16).double(), None, padding=1).to(torch.bfloat16)  # stem output
+    da = torch.randn(N, 64, *S, generator=g).to(torch.bfloat16)                                  # grad of ReLU out
+    # fp64 reference: dW of conv -> BN(train) -> ReLU given y (rounded) and da
+    yr = y.double().requires_grad_(True)
+    F.relu(F.batch_norm(yr, None, None, gamma.double(), beta.double(), True, 0.1, 1e-5)).backward(da.double())
+    dw_ref = torch.nn.grad.conv3d_weight(x.double(), (64, 5, 3, 3, 3), yr.grad, padding=1)
+    m = y.double().mean((0, 2, 3, 4))
+    inv = 1.0 / torch.sqrt(y.double().var((0, 2, 3, 4), unbiased=False) + 1e-5)
+    sc = (gamma.double() * inv).float().to(DEV)
+    sh = (beta.double() - m * gamma.double() * inv).float().to(DEV)
+    mean, invstd, gd = m.float().to(DEV), inv.float().to(DEV), gamma.to(DEV)
+    yd, dad = ndhwc(y).to(DEV), ndhwc(da).to(DEV)
+    rows = L.query("pcms_bn_bwd_rows", 1, 64, nvox)
+    part = torch.empty(rows * 64 * 2, device=DEV)
+    coef = torch.empty(3 * 64, device=DEV)
+    bnws = torch.empty(L.query("pcms_bn_ws_doubles", 64), dtype=torch.float64, device=DEV)
+    ws = torch.empty(L.query("pcms_stem_wgrad_ws_floats", N, *S, 5), device=DEV)
+    # unfused
+    dg0, db0, dy0 = torch.zeros(64, device=DEV), torch.zeros(64, device=DEV), torch.empty_like(yd)
+    L.call("pcms_bn_relu_bwd", 1, dad, yd, sc, sh, mean, invstd, gd, part, coef, dg0, db0, dy0, 64, nvox, bnws)
+    dw0 = torch.zeros(64 * 5 * 27, device=DEV)
+    L.call("pcms_stem_wgrad", xd, dy0, dw0, ws, 5, N, *S)
+    # fused: reduce + finalize only (dy NULL), then the wgrad applies in LDS
+    dg1, db1 = torch.zeros(64, device=DEV), torch.zeros(64, device=DEV)
+    coef1 = torch.full((3 * 64,), float("nan"), device=DEV)
+    L.call("pcms_bn_relu_bwd", 1, dad, yd, sc, sh, mean, invstd, gd, part, coef1, dg1, db1, None, 64, nvox, bnws)
+    dw1 = torch.zeros(64 * 5 * 27, device=DEV)
+    L.call("pcms_stem_wgrad_bn", xd, dad, yd, sc, sh, mean, invstd, coef1, dw1, ws, 5, N, *S)
+    torch.cuda.synchronize()
+    assert torch.equal(dg0, dg1) and torch.equal(db0, db1) and torch.equal(coef, coef1)
+    # (the in-LDS dy and the apply kernel may contract k1 g + k2 xhat + k3 differently: a rare
+    # one-ulp bf16 difference in dy)
+    close(dw1.cpu(), dw0.cpu(), 1e-4, "fused vs unfused stem wgrad")
+    close(dw1.cpu().view(64, 5, 3, 3, 3), dw_ref, 2e-2, "fused stem wgrad vs fp64")
 
 
 @pytest.mark.parametrize("cout,cin", [(64, 64), (128, 256), (64, 128), (512, 1024)])

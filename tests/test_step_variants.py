@@ -223,7 +223,9 @@ def _oracle_amp_clip_step(x, y, max_norm, init_scale=2.0 ** 16):
     torch.manual_seed(0)
     g64 = gu.oracle_grads64(ref.init_params(5, 1), x, y)
     norm64 = float(torch.sqrt(sum((g.double() ** 2).sum() for g in g64.values())))
+    clip64 = min(1.0, max_norm / (norm64 + 1e-6))
     return {"loss": float(loss), "norm": norm, "norm64": norm64, "grads": grads, "p0": p0,
+            "grads64": {k: g * clip64 for k, g in g64.items()},
             "post": {k: v.detach().clone() for k, v in sd.items()}, "scale": scaler.get_scale()}
 
 

@@ -23,7 +23,7 @@ def main():
     stats = torch.empty(L.query("pcms_stem_fwd_rows", N, D, H, W) * 129, device="cuda")
     dw = torch.zeros(64 * 5 * 27, device="cuda")
     ws = torch.empty(L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5), device="cuda")
-    fns = {"fwd": lambda s: L.call("pcms_stem_fwd", s[0], wp, bias, s[1], stats, N, D, H, W),
+    fns = {"fwd": lambda s: L.call("pcms_stem_fwd", s[0], wp, bias, s[1], stats, N, D, H, W, 0),
            "wgrad": lambda s: L.call("pcms_stem_wgrad", s[0], s[2], dw, ws, 5, N, D, H, W)}
     res = {}
     for rep in range(3):
