@@ -399,7 +399,7 @@ __global__ void __launch_bounds__(TPB) bn_relu_pool_kernel(const T* y, T* a, T* 
 // per channel: one [C][2] row per block (bn_relu_bwd_reduce_kernel's quantities), so the
 // BatchNorm backward needs no reduction pass over da and y of its own.
 template <typename T>
-__global__ void __launch_bounds__(TPB) maxpool_bwd_bn_kernel(const T* y, const float* scale, const float* shift,
+__global__ void __launch_bounds__(TPB, 3) maxpool_bwd_bn_kernel(const T* y, const float* scale, const float* shift,
                                                              const float* mean, const float* invstd, const T* dp,
                                                              T* da, float* part, int N, int D, int H, int W,
                                                              int C) {
@@ -418,50 +418,72 @@ __global__ void __launch_bounds__(TPB) maxpool_bwd_bn_kernel(const T* y, const f
     sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
     sg[j] = 0.f; sgx[j] = 0.f;
   }
+  // a cell's 8 y chunks, 8 da chunks and its dp chunk are all loaded (raw 16-B vectors) before
+  // the first use: one memory round trip per cell instead of one per child
+  auto unpack = [](const u32x4_t r, float (&o)[VEC]) {
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { o[2 * q] = __uint_as_float(r[q] << 16); o[2 * q + 1] = __uint_as_float(r[q] & 0xffff0000u); }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = __uint_as_float(r[q]);
+    }
+  };
   for (; i < total; i += stride) {
     uint32_t r = (uint32_t)(i / CV);
     const int wc = r % Wc; r /= Wc;
     const int hc = r % Hc; r /= Hc;
     const int dc = r % Dc; const long n = r / Dc;
     const bool whole = dc < Do && hc < Ho && wc < Wo;
-    float yv[8][VEC], g[VEC], m[VEC];
-    int arg[VEC];
-    long vin[8];
-    bool in[8];
+    u32x4_t yr[8], dr[8], gr = {0u, 0u, 0u, 0u};
+    // child k: voxel v0 + (k >> 2) H W + ((k >> 1) & 1) W + (k & 1) (recomputed where used)
+    const long v0 = ((n * D + 2 * dc) * H + 2 * hc) * W + 2 * wc;
+    const bool ind = 2 * dc + 1 < D, inh = 2 * hc + 1 < H, inw = 2 * wc + 1 < W;
+    auto vk = [&](int k) { return v0 + (long)(k >> 2) * H * W + ((k >> 1) & 1) * W + (k & 1); };
+    auto ink = [&](int k) { return (!(k & 4) || ind) && (!(k & 2) || inh) && (!(k & 1) || inw); };
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int d = 2 * dc + (k >> 2), h = 2 * hc + ((k >> 1) & 1), w = 2 * wc + (k & 1);
-      in[k] = d < D && h < H && w < W;
-      vin[k] = ((n * D + d) * H + h) * W + w;
-      if (in[k]) load16<T>(y + vin[k] * C + cv * VEC, yv[k]);
+      yr[k] = (u32x4_t){0u, 0u, 0u, 0u};
+      dr[k] = yr[k];
+      if (ink(k)) {
+        yr[k] = *reinterpret_cast<const u32x4_t*>(y + vk(k) * C + cv * VEC);
+        dr[k] = *reinterpret_cast<const u32x4_t*>(da + vk(k) * C + cv * VEC);
+      }
     }
-    if (whole) load16<T>(dp + (((n * Do + dc) * Ho + hc) * Wo + wc) * C + cv * VEC, g);
+    if (whole) gr = *reinterpret_cast<const u32x4_t*>(dp + (((n * Do + dc) * Ho + hc) * Wo + wc) * C + cv * VEC);
+    float g[VEC], m[VEC];
+    int arg[VEC];
+    unpack(gr, g);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; arg[j] = 0; }
     if (whole) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < 8; ++k) {
+        float yv[VEC];
+        unpack(yr[k], yv);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
-          const float av = round_st<T>(bn_relu1(yv[k][j], sc[j], sh[j]));
+          const float av = round_st<T>(bn_relu1(yv[j], sc[j], sh[j]));
           if (av > m[j] || (av != av && m[j] == m[j])) { m[j] = av; arg[j] = k; }
         }
+      }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      if (!in[k]) continue;
-      float o[VEC];
-      load16<T>(da + vin[k] * C + cv * VEC, o);
+      if (!ink(k)) continue;
+      float yv[VEC], o[VEC];
+      unpack(yr[k], yv);
+      unpack(dr[k], o);
       if (whole) {
 #pragma unroll
         for (int j = 0; j < VEC; ++j) o[j] += (arg[j] == k) ? g[j] : 0.f;
-        store16<T>(da + vin[k] * C + cv * VEC, o);
+        store16<T>(da + vk(k) * C + cv * VEC, o);
       }
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        const float gg = (yv[k][j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
+        const float gg = (yv[j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
         sg[j] += gg;
-        sgx[j] += gg * ((yv[k][j] - mu[j]) * is[j]);
+        sgx[j] += gg * ((yv[j] - mu[j]) * is[j]);
       }
     }
   }
@@ -555,38 +577,54 @@ __global__ void __launch_bounds__(256) rows_sum_kernel(const float* part, int ro
 }
 
 // ---------------- output head: logits (NCDHW fp32) = b + a . w ----------------
-// 8 lanes per voxel, 8 channels each (Cin = 64).  act 0: logits; 1: sigmoid(logits)
-// (UNet3D.predict, models/unet3d.py:298-318); 2: (sigmoid(logits) > thr) as 0 / 1
-// (UNet3D.inference, :320-344) -- the eval outputs leave the head kernel finished.
+// 8 lanes per voxel, 8 channels each (Cin = 64); NC = n_classes (<= 4, a template argument
+// so per-class registers exist only for real classes).  Every kernel walks kHU voxels per
+// trip with all of their loads (activations and, backward, dlogits) issued before the first
+// use: these are pure streams, bound by bytes in flight per CU.
+constexpr int kHU = 4;
+
+template <typename T, bool NT>
+__device__ __forceinline__ void head_ld(const T* p, float (&x)[8]) {
+  ld16<NT>(p, x);
+  if constexpr (sizeof(T) == 4) ld16<NT>(p + 4, x + 4);
+}
+template <typename T, bool NT>
+__device__ __forceinline__ void head_st(T* p, const float (&x)[8]) {
+  st16<NT>(p, x);
+  if constexpr (sizeof(T) == 4) st16<NT>(p + 4, x + 4);
+}
+
+// act 0: logits; 1: sigmoid(logits) (UNet3D.predict, models/unet3d.py:298-318); 2:
+// (sigmoid(logits) > thr) as 0 / 1 (UNet3D.inference, :320-344) -- the eval outputs leave the
+// head kernel finished.
 // BN: ``a`` is the decoder's last pre-BN conv output y2 and the head applies that block's
 // BatchNorm + ReLU itself (models/unet3d.py:37-39 fused into :222): a = round_T(relu(y sc +
 // sh)), the value the bn_relu pass would have stored, so the logits are bit-identical and
 // the a2 tensor (the largest activation of the step) is never written or read.
-template <typename T, bool NT, bool BN>
-__global__ void head_fwd_kernel(const T* a, const float* w, const float* b, float* logits,
-                                long nvox_per_n, int N, int ncls, int act, float thr,
-                                const float* bn_scale, const float* bn_shift) {
+template <typename T, bool NT, bool BN, int NC>
+__global__ void __launch_bounds__(TPB, 3) head_fwd_kernel(const T* a, const float* w, const float* b, float* logits,
+                                                       long nvox_per_n, int N, int act, float thr,
+                                                       const float* bn_scale, const float* bn_shift) {
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7;
-  float sc[8], sh[8];
-  if constexpr (BN) {
+  float sc[8], sh[8], wk[NC][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { sc[j] = bn_scale[sub * 8 + j]; sh[j] = bn_shift[sub * 8 + j]; }
+  for (int j = 0; j < 8; ++j) {
+    if constexpr (BN) { sc[j] = bn_scale[sub * 8 + j]; sh[j] = bn_shift[sub * 8 + j]; }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) wk[k][j] = w[k * 64 + sub * 8 + j];
   }
-  auto load = [&](long v, float (&x)[8]) {
-    ld16<NT>(a + v * 64 + sub * 8, x);
-    if constexpr (sizeof(T) == 4) ld16<NT>(a + v * 64 + sub * 8 + 4, x + 4);
+  auto one = [&](long v, float (&x)[8]) {
     if constexpr (BN) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = round_st<T>(bn_relu1(x[j], sc[j], sh[j]));
     }
-  };
-  auto one = [&](long v, const float (&x)[8]) {
     const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
-    for (int k = 0; k < ncls; ++k) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
       float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += x[j] * w[k * 64 + sub * 8 + j];
+      for (int j = 0; j < 8; ++j) s += x[j] * wk[k][j];
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
       s += __shfl_xor(s, 4, 64);
@@ -596,80 +634,79 @@ __global__ void head_fwd_kernel(const T* a, const float* w, const float* b, floa
           const float pr = 1.f / (1.f + expf(-o));
           o = act == 1 ? pr : (pr > thr ? 1.f : 0.f);
         }
-        logits[(n * ncls + k) * nvox_per_n + vv] = o;
+        logits[(n * NC + k) * nvox_per_n + vv] = o;
       }
     }
   };
-  // two voxels per trip, both loads in flight
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
-  for (; v + stride < total; v += 2 * stride) {
-    float x0[8], x1[8];
-    load(v, x0);
-    load(v + stride, x1);
-    one(v, x0);
-    one(v + stride, x1);
+  for (; v + (kHU - 1) * stride < total; v += kHU * stride) {
+    float x[kHU][8];
+#pragma unroll
+    for (int u = 0; u < kHU; ++u) head_ld<T, NT>(a + (v + u * stride) * 64 + sub * 8, x[u]);
+#pragma unroll
+    for (int u = 0; u < kHU; ++u) one(v + u * stride, x[u]);
   }
   for (; v < total; v += stride) {
-    float x0[8];
-    load(v, x0);
-    one(v, x0);
+    float x[8];
+    head_ld<T, NT>(a + v * 64 + sub * 8, x);
+    one(v, x);
   }
 }
 
 // da[v, c] = sum_k dl[k, v] w[k, c]  (written);  per-block partials of dw[k, c] = sum_v dl a,
-// db[k] = sum_v dl
-// NT: non-temporal a / da streams (level-0 sized).  Two voxels per trip with both loads in
-// flight (accumulated in the same voxel order as one at a time: identical sums).
+// db[k] = sum_v dl.  NT: non-temporal a / da streams (level-0 sized).
 // BN (the decoder's last BatchNorm + ReLU fused, see head_fwd_kernel): ``a`` is y2; the head
 // input a2 = round_T(relu(y sc + sh)) is recomputed, da is NOT written: its round_T value
 // feeds the BatchNorm-backward partial sums directly -- per block one row [64][2] of
 // (sum g, sum g xhat), g = da [y sc + sh > 0], xhat = (y - mean) invstd -- and
-// head_bn_apply_kernel recomputes da from dlogits (rank ncls) instead of re-reading it.
+// head_bn_apply_kernel recomputes da from dlogits (rank NC) instead of re-reading it.
 struct HeadBN {
   const float *scale, *shift, *mean, *invstd;
   float* part;  // [blocks][64][2]
 };
-template <typename T, bool NT, bool BN>
-__global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* dlogits, const float* w,
-                                                       T* da, float* part, long nvox_per_n, int N, int ncls,
-                                                       HeadBN bn) {
-  __shared__ float red[TPB / 64][4][65];
+template <typename T, bool NT, bool BN, int NC>
+__global__ void __launch_bounds__(TPB, (BN && NC > 2) ? 2 : 3) head_bwd_kernel(const T* a, const float* dlogits, const float* w,
+                                                       T* da, float* part, long nvox_per_n, int N, HeadBN bn) {
+  __shared__ float red[TPB / 64][NC][65];
   __shared__ float bred[TPB / 64][64][2];
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float accw[4][8], accb[4];
-  for (int k = 0; k < 4; ++k) { accb[k] = 0.f; for (int j = 0; j < 8; ++j) accw[k][j] = 0.f; }
+  float accw[NC][8], accb[NC], wk[NC][8];
   float sc[8], sh[8], mu[8], is[8], sg[8], sgx[8];
-  if constexpr (BN) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) { accw[k][j] = 0.f; wk[k][j] = w[k * 64 + sub * 8 + j]; }
+    if constexpr (BN) {
       const int c = sub * 8 + j;
       sc[j] = bn.scale[c]; sh[j] = bn.shift[c]; mu[j] = bn.mean[c]; is[j] = bn.invstd[c];
       sg[j] = 0.f; sgx[j] = 0.f;
     }
   }
-  auto load = [&](long v, float (&x)[8]) {
-    ld16<NT>(a + v * 64 + sub * 8, x);
-    if constexpr (sizeof(T) == 4) ld16<NT>(a + v * 64 + sub * 8 + 4, x + 4);
-  };
-  auto one = [&](long v, const float (&x)[8]) {
-    float o[8], av[8];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) accb[k] = 0.f;
+  auto ld_dl = [&](long v, float (&dl)[NC]) {
     const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) dl[k] = dlogits[(n * NC + k) * nvox_per_n + vv];
+  };
+  auto one = [&](long v, const float (&x)[8], const float (&dl)[NC]) {
+    float o[8], av[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       o[j] = 0.f;
       if constexpr (BN) av[j] = round_st<T>(bn_relu1(x[j], sc[j], sh[j]));
       else av[j] = x[j];
     }
-    for (int k = 0; k < ncls && k < 4; ++k) {
-      const float g = dlogits[(n * ncls + k) * nvox_per_n + vv];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        o[j] += g * w[k * 64 + sub * 8 + j];
-        accw[k][j] += g * av[j];
+        o[j] += dl[k] * wk[k][j];
+        accw[k][j] += dl[k] * av[j];
       }
-      if (sub == 0) accb[k] += g;
+      if (sub == 0) accb[k] += dl[k];
     }
     if constexpr (BN) {
 #pragma unroll
@@ -679,26 +716,32 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
         sgx[j] += g * ((x[j] - mu[j]) * is[j]);
       }
     } else {
-      st16<NT>(da + v * 64 + sub * 8, o);
-      if constexpr (sizeof(T) == 4) st16<NT>(da + v * 64 + sub * 8 + 4, o + 4);
+      head_st<T, NT>(da + v * 64 + sub * 8, o);
     }
   };
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
-  for (; v + stride < total; v += 2 * stride) {
-    float x0[8], x1[8];
-    load(v, x0);
-    load(v + stride, x1);
-    one(v, x0);
-    one(v + stride, x1);
+  constexpr int U = NC > 2 ? 1 : (BN || NC > 1) ? 2 : kHU;  // (registers: the BN form holds 6 x 8 per-channel values)
+#pragma unroll 1
+  for (; v + (U - 1) * stride < total; v += U * stride) {
+    float x[U][8], dl[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      head_ld<T, NT>(a + (v + u * stride) * 64 + sub * 8, x[u]);
+      ld_dl(v + u * stride, dl[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(v + u * stride, x[u], dl[u]);
   }
   for (; v < total; v += stride) {
-    float x0[8];
-    load(v, x0);
-    one(v, x0);
+    float x[8], dl[NC];
+    head_ld<T, NT>(a + v * 64 + sub * 8, x);
+    ld_dl(v, dl);
+    one(v, x, dl);
   }
   // reduce accw over the 8 voxel-lanes of each wave that share `sub`
-  for (int k = 0; k < ncls && k < 4; ++k) {
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float s = accw[k][j];
@@ -721,13 +764,13 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
     }
   }
   __syncthreads();
-  // this block's partial row [ncls][65] (dw row k, then db[k]); rows_sum_kernel adds the
-  // rows in block order
-  for (int idx = threadIdx.x; idx < ncls * 65 && idx < 4 * 65; idx += TPB) {
+  // this block's partial row [NC][65] (dw row k, then db[k]); rows_sum_kernel adds the rows
+  // in block order
+  for (int idx = threadIdx.x; idx < NC * 65; idx += TPB) {
     const int k = idx / 65, c = idx % 65;
     float s = 0.f;
     for (int wv = 0; wv < TPB / 64; ++wv) s += red[wv][k][c];
-    part[(long)blockIdx.x * ncls * 65 + idx] = s;
+    part[(long)blockIdx.x * NC * 65 + idx] = s;
   }
   if constexpr (BN) {
     if (threadIdx.x < 128) {
@@ -743,58 +786,65 @@ __global__ void __launch_bounds__(TPB) head_bwd_kernel(const T* a, const float* 
 // recomputed per voxel from dlogits (da[v, c] = sum_k dl[k, v] w[k, c], rounded to T exactly as
 // head_bwd_kernel would have stored it) instead of being written and read back:
 // dy = k1 g + k2 xhat + k3, g = da [y sc + sh > 0] (bn_relu_bwd_apply_kernel's arithmetic).
-template <typename T, bool NT>
-__global__ void __launch_bounds__(TPB) head_bn_apply_kernel(const T* y, const float* dlogits, const float* w,
+template <typename T, bool NT, int NC>
+__global__ void __launch_bounds__(TPB, NC > 2 ? 2 : 3) head_bn_apply_kernel(const T* y, const float* dlogits, const float* w,
                                                             const float* scale, const float* shift,
                                                             const float* mean, const float* invstd,
-                                                            const float* coef, T* dy, long nvox_per_n, int N,
-                                                            int ncls) {
+                                                            const float* coef, T* dy, long nvox_per_n, int N) {
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7;
-  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8], k3[8], wk[4][8];
+  // dy = k1 g + A y + B with A = k2 invstd, B = k3 - k2 invstd mean (five per-channel values
+  // held instead of seven: the seven-value form spilled at three waves per SIMD)
+  float sc[8], sh[8], k1[8], A[8], B[8], wk[NC][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = sub * 8 + j;
-    sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
-    k1[j] = coef[c * 3]; k2[j] = coef[c * 3 + 1]; k3[j] = coef[c * 3 + 2];
+    sc[j] = scale[c]; sh[j] = shift[c];
+    k1[j] = coef[c * 3];
+    A[j] = coef[c * 3 + 1] * invstd[c];
+    B[j] = coef[c * 3 + 2] - A[j] * mean[c];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) wk[k][j] = k < ncls ? w[k * 64 + c] : 0.f;
+    for (int k = 0; k < NC; ++k) wk[k][j] = w[k * 64 + c];
   }
-  auto one = [&](long v, const float (&x)[8]) {
+  auto ld_dl = [&](long v, float (&dl)[NC]) {
     const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) dl[k] = dlogits[(n * NC + k) * nvox_per_n + vv];
+  };
+  auto one = [&](long v, const float (&x)[8], const float (&dl)[NC]) {
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = 0.f;
-    for (int k = 0; k < ncls && k < 4; ++k) {
-      const float g = dlogits[(n * ncls + k) * nvox_per_n + vv];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] += g * wk[k][j];
-    }
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += dl[k] * wk[k][j];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float g = (x[j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
-      o[j] = k1[j] * g + k2[j] * ((x[j] - mu[j]) * is[j]) + k3[j];
+      o[j] = k1[j] * g + (A[j] * x[j] + B[j]);
     }
-    st16<NT>(dy + v * 64 + sub * 8, o);
-    if constexpr (sizeof(T) == 4) st16<NT>(dy + v * 64 + sub * 8 + 4, o + 4);
-  };
-  auto load = [&](long v, float (&x)[8]) {
-    ld16<NT>(y + v * 64 + sub * 8, x);
-    if constexpr (sizeof(T) == 4) ld16<NT>(y + v * 64 + sub * 8 + 4, x + 4);
+    head_st<T, NT>(dy + v * 64 + sub * 8, o);
   };
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
-  for (; v + stride < total; v += 2 * stride) {
-    float x0[8], x1[8];
-    load(v, x0);
-    load(v + stride, x1);
-    one(v, x0);
-    one(v + stride, x1);
+  constexpr int U = NC > 1 ? 1 : 2;  // (registers: 5 x 8 per-channel values + NC x 8 weights held)
+#pragma unroll 1
+  for (; v + (U - 1) * stride < total; v += U * stride) {
+    float x[U][8], dl[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      head_ld<T, NT>(y + (v + u * stride) * 64 + sub * 8, x[u]);
+      ld_dl(v + u * stride, dl[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(v + u * stride, x[u], dl[u]);
   }
   for (; v < total; v += stride) {
-    float x0[8];
-    load(v, x0);
-    one(v, x0);
+    float x[8], dl[NC];
+    head_ld<T, NT>(y + v * 64 + sub * 8, x);
+    ld_dl(v, dl);
+    one(v, x, dl);
   }
 }
 
@@ -1048,12 +1098,43 @@ __global__ void add_kernel(T* dst, const T* src, long nvec) {
   }
 }
 
+// the head kernels with n_classes as a template argument (1..4)
+template <int NC, typename F>
+int with_ncls(int ncls, F&& f) {
+  if constexpr (NC > 4) {
+    return -1;
+  } else {
+    if (ncls == NC) { f(std::integral_constant<int, NC>{}); return 0; }
+    return with_ncls<NC + 1>(ncls, f);
+  }
+}
 template <typename T, bool BN>
-void launch_head_fwd(bool nt, int grid, hipStream_t s, const void* a, const float* w, const float* b,
-                            float* out, long nvox_per_n, int N, int ncls, int act, float thr, const float* sc,
-                            const float* sh) {
-  hipLaunchKernelGGL((nt ? head_fwd_kernel<T, true, BN> : head_fwd_kernel<T, false, BN>), dim3(grid), dim3(TPB), 0,
-                     s, (const T*)a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+int launch_head_fwd(bool nt, int grid, hipStream_t s, const void* a, const float* w, const float* b, float* out,
+                    long nvox_per_n, int N, int ncls, int act, float thr, const float* sc, const float* sh) {
+  return with_ncls<1>(ncls, [&](auto nc) {
+    constexpr int NC = decltype(nc)::value;
+    hipLaunchKernelGGL((nt ? head_fwd_kernel<T, true, BN, NC> : head_fwd_kernel<T, false, BN, NC>), dim3(grid),
+                       dim3(TPB), 0, s, (const T*)a, w, b, out, nvox_per_n, N, act, thr, sc, sh);
+  });
+}
+template <typename T, bool BN>
+int launch_head_bwd(bool nt, int grid, hipStream_t s, const void* a, const float* dl, const float* w, void* da,
+                    float* part, long nvox_per_n, int N, int ncls, const HeadBN& bn) {
+  return with_ncls<1>(ncls, [&](auto nc) {
+    constexpr int NC = decltype(nc)::value;
+    hipLaunchKernelGGL((nt ? head_bwd_kernel<T, true, BN, NC> : head_bwd_kernel<T, false, BN, NC>), dim3(grid),
+                       dim3(TPB), 0, s, (const T*)a, dl, w, (T*)da, part, nvox_per_n, N, bn);
+  });
+}
+template <typename T>
+int launch_head_apply(bool nt, int grid, hipStream_t s, const void* y, const float* dl, const float* w,
+                      const float* sc, const float* sh, const float* mu, const float* is, const float* coef, void* dy,
+                      long nvox_per_n, int N, int ncls) {
+  return with_ncls<1>(ncls, [&](auto nc) {
+    constexpr int NC = decltype(nc)::value;
+    hipLaunchKernelGGL((nt ? head_bn_apply_kernel<T, true, NC> : head_bn_apply_kernel<T, false, NC>), dim3(grid),
+                       dim3(TPB), 0, s, (const T*)y, dl, w, sc, sh, mu, is, coef, (T*)dy, nvox_per_n, N);
+  });
 }
 
 }  // namespace
@@ -1264,13 +1345,14 @@ static int head_fwd_any(int dtype, const void* a, const float* w, const float* b
   const int grid = grid_for((long)N * nvox_per_n * 8, TPB);
   const bool nt = (long)N * nvox_per_n * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   const bool bn = sc != nullptr;
-  if (dtype == PCMS_BF16) {
-    if (bn) launch_head_fwd<bf16_t, true>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
-    else launch_head_fwd<bf16_t, false>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
-  } else {
-    if (bn) launch_head_fwd<float, true>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
-    else launch_head_fwd<float, false>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
-  }
+  int rc;
+  if (dtype == PCMS_BF16)
+    rc = bn ? launch_head_fwd<bf16_t, true>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh)
+            : launch_head_fwd<bf16_t, false>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+  else
+    rc = bn ? launch_head_fwd<float, true>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh)
+            : launch_head_fwd<float, false>(nt, grid, s, a, w, b, out, nvox_per_n, N, ncls, act, thr, sc, sh);
+  if (rc) return rc;
   PCMS_CHECK_LAUNCH();
 }
 
@@ -1311,12 +1393,8 @@ int pcms_head_bwd(int dtype, const void* a, const float* dlogits, const float* w
   const int grid = head_bwd_rows((long)N * nvox_per_n);
   const bool nt = (long)N * nvox_per_n * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   const HeadBN nobn{};
-  if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL((nt ? head_bwd_kernel<bf16_t, true, false> : head_bwd_kernel<bf16_t, false, false>), dim3(grid),
-                       dim3(TPB), 0, s, (const bf16_t*)a, dlogits, w, (bf16_t*)da, ws, nvox_per_n, N, ncls, nobn);
-  else
-    hipLaunchKernelGGL((nt ? head_bwd_kernel<float, true, false> : head_bwd_kernel<float, false, false>), dim3(grid),
-                       dim3(TPB), 0, s, (const float*)a, dlogits, w, (float*)da, ws, nvox_per_n, N, ncls, nobn);
+  if (dtype == PCMS_BF16) launch_head_bwd<bf16_t, false>(nt, grid, s, a, dlogits, w, da, ws, nvox_per_n, N, ncls, nobn);
+  else launch_head_bwd<float, false>(nt, grid, s, a, dlogits, w, da, ws, nvox_per_n, N, ncls, nobn);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return head_finish(grid, ws, ncls, dw, db, s);
@@ -1336,12 +1414,8 @@ int pcms_head_bn_bwd(int dtype, const void* y, const float* scale, const float* 
   const bool nt = nvox * 64 * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   const HeadBN bn{scale, shift, mean, invstd, bnpart};
   // pass 1: head weight / bias partials + BatchNorm-backward partial sums (reads y2, dlogits)
-  if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL((head_bwd_kernel<bf16_t, false, true>), dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, dlogits,
-                       w, (bf16_t*)nullptr, ws, nvox_per_n, N, ncls, bn);
-  else
-    hipLaunchKernelGGL((head_bwd_kernel<float, false, true>), dim3(grid), dim3(TPB), 0, s, (const float*)y, dlogits, w,
-                       (float*)nullptr, ws, nvox_per_n, N, ncls, bn);
+  if (dtype == PCMS_BF16) launch_head_bwd<bf16_t, true>(false, grid, s, y, dlogits, w, nullptr, ws, nvox_per_n, N, ncls, bn);
+  else launch_head_bwd<float, true>(false, grid, s, y, dlogits, w, nullptr, ws, nvox_per_n, N, ncls, bn);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   if ((e = (hipError_t)head_finish(grid, ws, ncls, dw, db, s)) != hipSuccess) return (int)e;
@@ -1354,13 +1428,9 @@ int pcms_head_bn_bwd(int dtype, const void* y, const float* scale, const float* 
   // pass 2: dy of the BatchNorm input (reads y2, dlogits)
   const int agrid = grid_for(nvox * 8, TPB);
   if (dtype == PCMS_BF16)
-    hipLaunchKernelGGL((nt ? head_bn_apply_kernel<bf16_t, true> : head_bn_apply_kernel<bf16_t, false>), dim3(agrid),
-                       dim3(TPB), 0, s, (const bf16_t*)y, dlogits, w, scale, shift, mean, invstd, (const float*)coef,
-                       (bf16_t*)dy, nvox_per_n, N, ncls);
+    launch_head_apply<bf16_t>(nt, agrid, s, y, dlogits, w, scale, shift, mean, invstd, coef, dy, nvox_per_n, N, ncls);
   else
-    hipLaunchKernelGGL((nt ? head_bn_apply_kernel<float, true> : head_bn_apply_kernel<float, false>), dim3(agrid),
-                       dim3(TPB), 0, s, (const float*)y, dlogits, w, scale, shift, mean, invstd, (const float*)coef,
-                       (float*)dy, nvox_per_n, N, ncls);
+    launch_head_apply<float>(nt, agrid, s, y, dlogits, w, scale, shift, mean, invstd, coef, dy, nvox_per_n, N, ncls);
   PCMS_CHECK_LAUNCH();
 }
 
