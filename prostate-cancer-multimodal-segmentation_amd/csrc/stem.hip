@@ -488,40 +488,42 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     }
   };
 
-  // BN transform: thread t rewrites rows r = 4 (t / 16 + 32 j) + 2 rs + b (j, b in {0, 1};
-  // rs = (t / 8) & 1) at physical 16-B slot q = t & 7 of the tile; dy_off_bf16's half swap
-  // depends on r & 2 = 2 rs only, so the slot holds the same 8 logical channels in all four
-  // rows and their coefficients stay in registers
-  constexpr int kTR = 4;
-  const int tq = tid & 7, trs = (tid >> 3) & 1, tb = tid >> 4;
-  const int tql = tq ^ (trs << 2);
+  // BN transform: every wave rewrites exactly the dy elements its own MFMAs read -- wave
+  // (ks, ct) reads channels [32 ct, 32 ct + 32) of the rows of k-steps ks + 4 i, i < BD (rows
+  // 16 (ks + 4 i) + rs, rs < 16), so no other wave waits for it (no workgroup barrier between
+  // the transform and the MFMAs).  Lane: 16-B chunk q = lane & 3 of the row's 64-B half
+  // (channels 32 ct + 8 q ..), rs = lane >> 2; dy_off_bf16's half swap depends on row bit 1 =
+  // rs bit 1 only, so the lane's LDS column and its 8 channels' coefficients are fixed.
+  constexpr int kTR = BD;
+  const int tq = lane & 3, trs = lane >> 2;
+  const int tcol = ((ct ^ ((trs >> 1) & 1)) * 64) + tq * 16;  // byte offset in the 128-B row
+  const int tch = ct * 32 + tq * 8;                            // first logical channel
   float bsc[8], bsh[8], bmu[8], bis[8], bk1[8], bk2[8], bk3[8];
   u32x4_t yreg[kTR];
-  auto trow = [&](int k) { return 4 * (tb + 32 * (k >> 1)) + 2 * trs + (k & 1); };
   if constexpr (BN) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = tql * 8 + j;
+      const int c = tch + j;
       bsc[j] = bn.scale[c]; bsh[j] = bn.shift[c]; bmu[j] = bn.mean[c]; bis[j] = bn.invstd[c];
       bk1[j] = bn.coef[3 * c]; bk2[j] = bn.coef[3 * c + 1]; bk3[j] = bn.coef[3 * c + 2];
     }
   }
-  // y chunks of box b into registers (plain global loads: counted by vmcnt like the DMA)
+  // y chunks of box b into registers (plain global loads: counted by vmcnt like the DMA);
+  // row 16 (ks + 4 i) + rs of the box = voxel (d0 + i, h0 + ks, w0 + rs)
   auto load_y = [&](int b) {
     int n, d0, h0, w0;
     origin(b, n, d0, h0, w0);
-    const long vb = ((long)(n * D + d0) * H + h0) * W + w0;
+    const long vb = ((long)(n * D + d0) * H + h0 + ks) * W + w0 + trs;
 #pragma unroll
     for (int k = 0; k < kTR; ++k) {
-      const int r = trow(k), rd = r >> 6, rh = (r >> 4) & 3, rw = r & 15;
-      const bf16_t* src = bn.y + (vb + ((long)rd * H + rh) * W + rw) * 64 + tql * 8;
+      const bf16_t* src = bn.y + (vb + (long)k * H * W) * 64 + tch;
       yreg[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src));
     }
   };
   auto transform = [&](char* buf) {
 #pragma unroll
     for (int k = 0; k < kTR; ++k) {
-      u32x4_t* cp = reinterpret_cast<u32x4_t*>(buf + trow(k) * 128 + tq * 16);
+      u32x4_t* cp = reinterpret_cast<u32x4_t*>(buf + (16 * (ks + 4 * k) + trs) * 128 + tcol);
       const u32x4_t gv = *cp;
       float ga[8], yv[8], o[8];
 #pragma unroll
@@ -603,14 +605,13 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     __builtin_amdgcn_s_barrier();
     const int b2 = b + (NS - 1) * G;
     if constexpr (BN) {
-      // box b's da tile and y chunks have landed: dy in place, then the next box's y loads
-      // (before the DMA of box b + 2 G: the wait above stays a count of that DMA alone)
+      // box b's da tile and y chunks have landed: this wave's dy in place, then the next box's
+      // y loads (before the DMA of box b + 2 G: the wait above stays a count of that DMA alone)
       transform(swl + (it % NS) * kSWBuf);
       if (b + G < nbox) load_y(b + G);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
     }
     if (b2 < nbox) stage(b2, (it + NS - 1) % NS);
+    if constexpr (BN) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own dy writes before own reads
     compute(swl + (it % NS) * kSWBuf);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
