@@ -132,7 +132,7 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
             L.call("pcms_stem_wgrad_bn", s[0], s[2], s[1], bn.scale, bn.shift, bn.mean, bn.invstd, coef, dw, dwt, 5,
                    N, D, H, W)
         else:
-            L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512)
+            L.call("pcms_conv3_wgrad", code, s[0], eng.cp, None, 0, s[2], dw, dwt, N, D, H, W, 64, 5, 512, 0)
 
     res = dict(in_step) if in_step else {}
     for name, fn in (("fwd", fwd), ("wgrad", wgrad)):

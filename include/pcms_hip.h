@@ -28,6 +28,9 @@ extern "C" {
  * weights and bias (pcms_bn_fold), no statistics                                          */
 #define PCMS_CONV_ACCUMULATE 1
 #define PCMS_CONV_RELU 2
+/* gradient writer flags (pcms_conv3_wgrad): STORE writes dw instead of adding into it -- the
+ * first writer after zero_grad(set_to_none=True), so the gradient needs no zero fill       */
+#define PCMS_GRAD_STORE 1
 
 /* ---- layout ---------------------------------------------------------------------- */
 /* batch['image'] (N, Cin, D, H, W) fp32 NCDHW -> NDHWC, channels zero-padded to Cp.
@@ -64,13 +67,14 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
                    float* yacc, float* stats, int flags,
                    int N, int D, int H, int W, int Cout, int splits, hipStream_t s);
-/* dw [Cout][cin_w][27] fp32 += sum_v dy[v, co] * x[v + tap, ci] (ci < cin_w <= c0 + c1);
+/* dw [Cout][cin_w][27] fp32 += sum_v dy[v, co] * x[v + tap, ci] (ci < cin_w <= c0 + c1;
+ * flags PCMS_GRAD_STORE: dw = ...);
  * dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (one partial row per voxel split,
  * summed in a fixed order: deterministic)                                               */
 int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout, int target_wgs);
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
-                     int target_wgs, hipStream_t s);
+                     int target_wgs, int flags, hipStream_t s);
 /* Stem (inc.conv.0, bf16 build): input stored with 8 channels (n_modalities <= 8).
  * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32).
  * pcms_stem_supported: bit 0 = pcms_stem_fwd runs this shape, bit 1 = pcms_stem_wgrad
@@ -240,6 +244,9 @@ int pcms_adam_ranges(float* p, float* g, float* m, float* v, const long long* ra
  * apply != 0: g *= mul in place (else pass mul to pcms_adam as gmul).  A non-finite norm
  * flags inf/NaN gradients (GradScaler's found_inf).  ws: pcms_grad_clip_ws_doubles().      */
 int pcms_grad_clip_ws_doubles(void);
+/* p[b, e) = v for each int64 [b, e) pair of ranges (the gradient ranges no STORE writer
+ * covers, zeroed before a backward into a fresh gradient)                                 */
+int pcms_fill_ranges(float* p, const long long* ranges, int nranges, long max_len, float v, hipStream_t s);
 int pcms_grad_clip(float* g, long n, float gscale, float max_norm, int apply, double* ws, float* norm_out,
                    float* mul_out, hipStream_t s);
 

@@ -27,7 +27,7 @@ SIGNATURES = {
     "pcms_conv3_splits": "iii",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
-    "pcms_conv3_wgrad": "ipipipppiiiiiiis",
+    "pcms_conv3_wgrad": "ipipipppiiiiiiiis",
     "pcms_stem_pack_elems": "",
     "pcms_stem_pack": "ppis",
     "pcms_stem_supported": "iiii",
@@ -74,6 +74,7 @@ SIGNATURES = {
     "pcms_adam_pack_convt": "pppppiifffffffps",
     "pcms_adam_ranges": "pppppilfffffffps",
     "pcms_grad_clip_ws_doubles": "",
+    "pcms_fill_ranges": "ppilfs",
     "pcms_grad_clip": "plffippps",
     "pcms_add": "ippls",
     "pcms_unpack_output": "ippiiils",

@@ -21,6 +21,8 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 enum { PCMS_F32 = 0, PCMS_BF16 = 1 };
 // conv epilogue flags (pcms_conv3_fwd, pcms_split_epilogue, pcms_stem_fwd)
 enum { PCMS_CONV_ACCUMULATE = 1, PCMS_CONV_RELU = 2 };
+// gradient writer flags (pcms_conv3_wgrad): store instead of accumulating
+enum { PCMS_GRAD_STORE = 1 };
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) {

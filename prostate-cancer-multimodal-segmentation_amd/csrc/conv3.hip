@@ -422,6 +422,7 @@ struct WgradParams {
   uint32_t x0bytes, x1bytes, dybytes;
   float* dw;             // direct (one split, bf16): dw [Cout][cw][27] += through an LDS transpose
   int cw, direct;
+  int store;             // PCMS_GRAD_STORE: dw = (the first writer of a fresh gradient), not +=
 };
 
 
@@ -818,7 +819,8 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
 #pragma unroll
           for (int k = 0; k < kPer; ++k) {
             const int q4 = tid + k * kWThreads, row = q4 / 216, q = q4 % 216;
-            if (q4 < kQ)
+            g[k] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+            if (q4 < kQ && !p.store)  // store: plain stores, nothing to read back
               g[k] = *reinterpret_cast<const f32x4_t*>(p.dw + ((long)(co_base + ct * 32 + row) * p.cw + ci_base) * 27 + 4 * q);
           }
 #pragma unroll
@@ -832,7 +834,10 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           for (int i = tid; i < 32 * 32 * 27; i += kWThreads) {
             const int col = i / 864, r = i % 864;  // r = ci * 27 + tap
             const int co = co_base + ct * 32 + col;
-            if (co < p.Cout && r < nci * 27) p.dw[((long)co * p.cw + ci_base) * 27 + r] += tile[i];
+            if (co < p.Cout && r < nci * 27) {
+              float* d = p.dw + ((long)co * p.cw + ci_base) * 27 + r;
+              *d = p.store ? tile[i] : *d + tile[i];
+            }
           }
         }
       }
@@ -880,7 +885,7 @@ __global__ void __launch_bounds__(256) wgrad_group_sum_kernel(float* part, int S
 // [27][32] tiles are read as 128-B rows, transposed through LDS, added to the contiguous
 // 32 x 27 run of dw.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, int R, int stride, float* dw,
-                                                           int Cout, int Cin, int Cw) {
+                                                           int Cout, int Cin, int Cw, int store) {
   __shared__ float tile[27][33];
   const int co = blockIdx.x, ci0 = blockIdx.y * 32;
   const long rstep = (long)stride * 27 * Cout * Cin;
@@ -895,7 +900,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, in
   __syncthreads();
   float* dst = dw + ((long)co * Cw + ci0) * 27;
   const int n = min(32, Cw - ci0) * 27;
-  for (int e = threadIdx.x; e < n; e += 256) dst[e] += tile[e % 27][e / 27];
+  for (int e = threadIdx.x; e < n; e += 256) dst[e] = store ? tile[e % 27][e / 27] : dst[e] + tile[e % 27][e / 27];
 }
 
 // master fp32 W[Cout][Cin][27] -> packed T [chunk][27][J][CK]
@@ -1591,9 +1596,10 @@ int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, in
 // fixed order: the result is deterministic).
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w, int target_wgs,
-                     hipStream_t s) {
+                     int flags, hipStream_t s) {
   const int Cin = c0 + c1;
   if (cin_w <= 0 || cin_w > Cin) return -4;
+  if (flags & ~PCMS_GRAD_STORE) return -8;
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (Cout % 64 != 0 || c0 % VEC != 0 || c1 % VEC != 0) return -1;
   const WgradPlan q = wgrad_plan(dtype, N, D, H, W, Cin, Cout, target_wgs);
@@ -1615,6 +1621,7 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   p.dw = dw;
   p.cw = cin_w;
   p.direct = splits == 1 && dtype == PCMS_BF16;
+  p.store = flags & PCMS_GRAD_STORE;
   dim3 grid(splits * p.nco * p.nci);
   size_t lds;
   if (dtype == PCMS_BF16) {
@@ -1644,7 +1651,7 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
     stride = 16;
   }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(Cout, cdiv(cin_w, 32)), dim3(256), 0, s, (const float*)dwt, R, stride,
-                     dw, Cout, Cin, cin_w);
+                     dw, Cout, Cin, cin_w, p.store);
   PCMS_CHECK_LAUNCH();
 }
 

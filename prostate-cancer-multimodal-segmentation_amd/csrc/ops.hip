@@ -937,6 +937,12 @@ __global__ void adam_kernel(float* p, float* g, float* m, float* v, long n, Adam
 
 // The same over a list of [begin, end) element ranges of the flat buffers (the parameters the
 // fused Adam + weight-pack kernels do not cover): blockIdx.y = range.
+// p[b, e) = v for every [b, e) row of ranges (int64 pairs); grid.y = range
+__global__ void fill_ranges_kernel(float* p, const long long* ranges, float v) {
+  const long b = ranges[2 * blockIdx.y], e = ranges[2 * blockIdx.y + 1];
+  for (long i = b + blockIdx.x * (long)blockDim.x + threadIdx.x; i < e; i += (long)gridDim.x * blockDim.x) p[i] = v;
+}
+
 __global__ void adam_ranges_kernel(float* p, float* g, float* m, float* v, const long long* ranges, AdamCoef c,
                                    const float* gmul) {
   const float s = gmul ? c.gscale * gmul[0] : c.gscale;
@@ -1468,6 +1474,12 @@ int pcms_adam_ranges(float* p, float* g, float* m, float* v, const long long* ra
   const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
   hipLaunchKernelGGL(adam_ranges_kernel, dim3(grid_for(max_len, TPB, 2048), nranges), dim3(TPB), 0, s, p, g, m, v,
                      ranges, c, gmul);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_fill_ranges(float* p, const long long* ranges, int nranges, long max_len, float v, hipStream_t s) {
+  if (nranges <= 0) return 0;
+  hipLaunchKernelGGL(fill_ranges_kernel, dim3(grid_for(max_len, TPB, 1024), nranges), dim3(TPB), 0, s, p, ranges, v);
   PCMS_CHECK_LAUNCH();
 }
 

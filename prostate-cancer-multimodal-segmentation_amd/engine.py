@@ -132,6 +132,8 @@ class UNetEngine:
         self._eval = None      # {conv index: (fwd pack, folded bias)}, "stem": stem pack
         self._eval_key = None
         self._bn_epoch = 0     # training forwards so far (each moves the running statistics)
+        self._store_ranges = None  # (stem_sup, fill plan) of _store_plan
+        self._gstore = False       # this backward writes conv weight gradients (PCMS_GRAD_STORE)
         self._flatten()
         for bn in self.bns:
             c = bn.c
@@ -214,15 +216,27 @@ class UNetEngine:
             torch.cuda.current_stream(self.device).wait_stream(self._side_stream)
             self._side_used = False
 
-    def sync_params(self, full: bool = True):
+    def sync_params(self, full: bool = True, fresh_ok: bool = False) -> bool:
         """Re-flatten if a module op (``.to()``, ``.cuda()``, param reassignment) replaced
         storage, and make every ``param.grad`` a view of the flat gradient again.
         ``full=False`` (the calls inside one step after the forward's full check) skips the
-        module walk that detects replaced Parameter objects."""
+        module walk that detects replaced Parameter objects.  ``fresh_ok`` (the backward):
+        when EVERY gradient is None (``zero_grad(set_to_none=True)``, torch's default) the views
+        are attached without zeroing and True is returned -- the backward then writes the
+        gradient instead of accumulating into it (no 361 MB zero fill)."""
         if [p.data_ptr() for p in self.params] != self._flat_ptrs or (
                 full and list(self.model.parameters()) != self.params):
             self._flatten()
-            return
+            return False
+        if all(p.grad is None for p in self.params):
+            if not fresh_ok:
+                return False  # stay None (torch semantics) until a backward attaches them
+            off = 0
+            for p in self.params:
+                n = p.numel()
+                p.grad = self.flat_g[off:off + n].view_as(p)
+                off += n
+            return True
         off = 0
         for p in self.params:
             n = p.numel()
@@ -236,6 +250,33 @@ class UNetEngine:
                         view.copy_(g)
                 p.grad = view
             off += n
+        return False
+
+    def _store_plan(self):
+        """The flat-gradient ranges a fresh backward does NOT write with PCMS_GRAD_STORE (every
+        parameter but the weights of the convs that go through pcms_conv3_wgrad): zeroed by one
+        pcms_fill_ranges launch before such a backward.  Depends on the stem path (stem_sup)."""
+        key = self.stem_sup
+        if self._store_ranges is not None and self._store_ranges[0] == key:
+            return self._store_ranges[1]
+        base = self.flat_g.data_ptr()
+        stored = []
+        for i, cs in enumerate(self.convs):
+            if i == 0 and self.stem_sup & 2:
+                continue  # the stem's streaming kernel accumulates
+            w = cs.mod.weight
+            stored.append(((w.data_ptr() - self.flat_p.data_ptr()) // 4, w.numel()))
+        ranges, pos = [], 0
+        for off, n in sorted(stored):
+            if off > pos:
+                ranges.append([pos, off])
+            pos = off + n
+        if pos < self.flat_g.numel():
+            ranges.append([pos, self.flat_g.numel()])
+        plan = (torch.tensor(ranges, dtype=torch.int64, device=self.device), len(ranges),
+                max(e - b for b, e in ranges))
+        self._store_ranges = (key, plan)
+        return plan
 
     def mark_dirty(self, packs_fresh: bool = False):
         """The master weights changed.  ``packs_fresh``: the fused Adam (adam_plan) already
@@ -654,7 +695,7 @@ class UNetEngine:
             self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         with self._side():
             call("pcms_conv3_wgrad", self.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
-                 b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target)
+                 b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target, int(self._gstore))
         # dgrad conv1 -> grad of a1
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
         # BN0/ReLU backward -> dy1 (a second buffer: the side stream may still read gY)
@@ -675,7 +716,7 @@ class UNetEngine:
                     call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
             else:
                 call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gZ, blk.c0.mod.weight.grad, b["dwt"], N,
-                     *S, blk.c0.cout, blk.c0.cin, self.wgrad_target)
+                     *S, blk.c0.cout, blk.c0.cin, self.wgrad_target, int(self._gstore))
         if gx_out0 is not None:
             self._dgrad(blk.c0, gZ, gx_out0, gx_out1, cy0, N, S)
 
@@ -703,7 +744,11 @@ class UNetEngine:
         if self.saved_epoch != self.epoch:
             raise RuntimeError("UNet3D backward must follow its own training forward (the engine keeps "
                                "only the activations of the latest forward)")
-        self.sync_params(full=False)
+        fresh = self.sync_params(full=False, fresh_ok=True)
+        self._gstore = fresh
+        if fresh:
+            ranges, nr, mx = self._store_plan()
+            call("pcms_fill_ranges", self.flat_g, ranges, nr, mx, 0.0)
         b = self.bufs
         S, C = b["S"], b["C"]
         N = self.buf_key[0]

@@ -50,6 +50,8 @@ class FlatAdam(torch.optim.Optimizer):
         if len(self.param_groups) != 1:
             raise ValueError("FlatAdam supports a single parameter group")
         g = self.param_groups[0]
+        if all(p.grad is None for p in self.param_groups[0]["params"]):
+            return loss  # torch.optim.Adam skips parameters without a gradient
         eng = self.model.engine(full_sync=False)
         m, v = self._moments(eng)
         self.step_count += 1
@@ -75,8 +77,11 @@ class FlatAdam(torch.optim.Optimizer):
         return loss
 
     def zero_grad(self, set_to_none: bool = True):
+        """torch semantics: ``set_to_none`` (the default) leaves every ``param.grad`` None --
+        the next backward then writes the flat gradient instead of accumulating into it, so
+        no zero fill runs; ``set_to_none=False`` zeroes the flat gradient in place."""
         eng = self.model._engine
-        if eng is not None:
+        if eng is not None and not set_to_none:
             eng.flat_g.zero_()
             eng.sync_params(full=False)
         else:

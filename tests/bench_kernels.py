@@ -100,7 +100,7 @@ def main():
             out.append(f"dgrad {t * 1e6:8.1f}us {flop / t / 1e12:7.1f}TF")
         if not only or "wgrad" in only:
             def f(i):
-                L.call("pcms_conv3_wgrad", code, xs[i], cin, None, 0, dys[i], dw, dwt, N, D, H, W, cout, cin, 512)
+                L.call("pcms_conv3_wgrad", code, xs[i], cin, None, 0, dys[i], dw, dwt, N, D, H, W, cout, cin, 512, 1)
             t = timeit(f, a.reps)
             out.append(f"wgrad {t * 1e6:8.1f}us {flop / t / 1e12:7.1f}TF")
         print(f"{name:26s} " + " | ".join(out), flush=True)

@@ -27,7 +27,7 @@ def main():
     bnv = [torch.rand(64, device="cuda") + 0.5 for _ in range(4)]  # scale, shift, mean, invstd
     coef = torch.randn(3 * 64, device="cuda") * 0.01
     ws = torch.empty(max(1, L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5)), device="cuda")
-    for name in ("fwd", "wgrad", "calib"):
+    for name in ("fwd", "wgrad", "wgrad0", "calib"):
         if which not in ("both", name) and not (which == "all"):
             continue
         def f(i):
@@ -36,6 +36,8 @@ def main():
                 y.copy_(dy)          # 268 MB read + 268 MB write (torch copy kernel)
             elif name == "fwd":
                 L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W, 0)
+            elif name == "wgrad0":  # the plain weight gradient over a stored dy (unfused path)
+                L.call("pcms_stem_wgrad", x, dy, dw, ws, 5, N, D, H, W)
             else:
                 L.call("pcms_stem_wgrad_bn", x, dy, y, *bnv, coef, dw, ws, 5, N, D, H, W)
         for i in range(3):
@@ -49,7 +51,7 @@ def main():
         e1.synchronize()
         t = e0.elapsed_time(e1) / reps * 1e-3
         byts = {"fwd": nvox * 5 * 2 + nvox * 64 * 2, "wgrad": nvox * 5 * 2 + 2 * nvox * 64 * 2,
-                "calib": 2 * nvox * 64 * 2}[name]
+                "wgrad0": nvox * 5 * 2 + nvox * 64 * 2, "calib": 2 * nvox * 64 * 2}[name]
         print(f"stem {name}: {t * 1e6:.1f} us  {byts / t / 1e9:.0f} GB/s algorithmic", flush=True)
     if which in ("all", "calib"):
         x, y, dy = sets[0]

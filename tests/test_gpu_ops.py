@@ -254,7 +254,10 @@ def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S, wgs):
     (2, 256, 0, 64, (1, 2, 1)),
     (1, 64, 64, 128, (4, 8, 8)),        # one box: the unsplit direct flush (16-B RMW of dw)
 ])
-def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
+@pytest.mark.parametrize("store", [0, 1])
+def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S, store):
+    """dw += (flags 0) or dw = (PCMS_GRAD_STORE: the first writer of a fresh gradient; the
+    buffer's old contents must not leak through) the weight gradient."""
     L = _lib()
     g = torch.Generator().manual_seed(c0 + 3 * cout)
     cin = c0 + c1
@@ -269,19 +272,19 @@ def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S):
     # the stored input may carry zero pad channels (stem: 5 of 8); dw has the weight's Cin
     guard = 4096
     dw_full = torch.zeros(cout * cin_real * 27 + guard, device=DEV)
-    init = torch.randn(cout * cin_real * 27, generator=g)  # dw accumulates (+=)
+    init = torch.randn(cout * cin_real * 27, generator=g)  # dw accumulates (+=) / is overwritten
     dw_full[:-guard] = init.to(DEV)
     ws = torch.empty(L.query("pcms_conv3_wgrad_ws_floats", code, N, *S, c0, c1, cout, 256), device=DEV)
     xs = ndhwc(x).to(DEV)
     if c1:
         L.call("pcms_conv3_wgrad", code, ndhwc(x[:, :c0]).to(DEV), c0, ndhwc(x[:, c0:]).to(DEV), c1,
-               ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, cin_real, 256)
+               ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, cin_real, 256, store)
     else:
         L.call("pcms_conv3_wgrad", code, xs, c0, None, 0, ndhwc(dy).to(DEV), dw_full, ws, N, *S, cout, cin_real,
-               256)
+               256, store)
     torch.cuda.synchronize()
     assert dw_full[-guard:].abs().max().item() == 0.0, "wgrad wrote past the weight gradient"
-    got = (dw_full[:-guard].cpu() - init).view(cout, cin_real, 3, 3, 3)
+    got = (dw_full[:-guard].cpu() - (0 if store else init)).view(cout, cin_real, 3, 3, 3)
     close(got, wr.grad, 1e-4 if code else 2e-5, "wgrad")
 
 

@@ -281,3 +281,36 @@ def test_amp_clip_step_matches_oracle_torch_gradscaler(path):
     assert scale == r["scale"]
     grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
     gu.check_step_against_oracle(m, grads, r, grad_rl2=5e-2, min_confident=0.2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_fresh_gradient_store_equals_zero_fill(precision):
+    """zero_grad() (set_to_none, torch's default) leaves param.grad None and the next backward
+    WRITES the conv weight gradients (PCMS_GRAD_STORE) after zeroing only the other ranges;
+    zero_grad(set_to_none=False) zero-fills and the backward accumulates.  Both give the same
+    gradient bit for bit; a second backward without zero_grad accumulates (sum of both)."""
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    gen = torch.Generator().manual_seed(3)
+    x = torch.rand(2, 5, 32, 32, 16, generator=gen).cuda()
+    y = (torch.rand(2, 1, 32, 32, 16, generator=gen) < 0.4).float().cuda()
+    torch.manual_seed(0)
+    m = UNet3D(n_modalities=5, n_classes=1, precision=precision).cuda()
+    opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
+    eng = m.engine()
+    eng.flat_g.fill_(float("nan"))  # stale contents must not leak into a fresh gradient
+    opt.zero_grad()
+    assert all(p.grad is None for p in m.parameters())
+    BCEDiceLoss()(m(x), y).backward()
+    assert eng._gstore
+    g_store = eng.flat_g.clone()
+    assert torch.isfinite(g_store).all()
+    opt.zero_grad(set_to_none=False)
+    BCEDiceLoss()(m(x), y).backward()
+    assert not eng._gstore
+    assert torch.equal(eng.flat_g, g_store)
+    BCEDiceLoss()(m(x), y).backward()  # accumulates
+    torch.testing.assert_close(eng.flat_g, 2 * g_store, rtol=1e-6, atol=0)
+    assert all(p.grad is not None and p.grad.data_ptr() >= eng.flat_g.data_ptr() for p in m.parameters())
