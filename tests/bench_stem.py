@@ -28,7 +28,8 @@ def main():
     coef = torch.randn(3 * 64, device="cuda") * 0.01
     ws = torch.empty(max(1, L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5)), device="cuda")
     for name in ("fwd", "wgrad", "wgrad0", "calib"):
-        if which not in ("both", name) and not (which == "all"):
+        # both: the product pair (fwd + fused wgrad); all: every variant and the calibrations
+        if not (which == "all" or which == name or (which == "both" and name in ("fwd", "wgrad"))):
             continue
         def f(i):
             x, y, dy = sets[i % 3]
