@@ -38,7 +38,12 @@ extern "C" {
 int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long V, int Cp, hipStream_t s);
 
 /* ---- Conv3d(k=3, padding=1): models/unet3d.py:29,35 ------------------------------- */
+/* The conv3 entry points also take dtype 2 (PCMS_F32X3): fp32 data, bf16x3 arithmetic
+ * (hi*hi + lo*hi + hi*lo, ~10x fp32 rounding error); dtype 0 there computes with bf16x6
+ * (three bf16 parts per operand, fp32-grade: the parity build).                        */
 int pcms_conv3_chunk(int dtype);                  /* input channels per K-chunk        */
+/* elements (activation dtype) of one weight pack, J rows x Kdim input channels          */
+int pcms_conv3_pack_elems(int dtype, int J, int Kdim);
 int pcms_conv3_mblocks(int N, int D, int H, int W);/* general-kernel M blocks (an upper
                                                       bound on the BN partial rows)      */
 /* BN partial rows an unsplit pcms_conv3_fwd over sources (c0, c1) writes: the persistent

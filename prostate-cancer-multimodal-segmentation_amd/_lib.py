@@ -12,12 +12,13 @@ import torch
 
 LIB_PATH = os.environ.get("PCMS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpcms_hip.so")
 
-F32, BF16 = 0, 1
+F32, BF16, F32X3 = 0, 1, 2  # F32X3: conv3 entry points only (fp32 data, bf16x3 arithmetic)
 
 # name -> argument codes: i int32, l int64, d double, f float, p pointer, s hipStream_t
 SIGNATURES = {
     "pcms_pack_input": "ippiilis",
     "pcms_conv3_chunk": "i",
+    "pcms_conv3_pack_elems": "iii",
     "pcms_conv3_mblocks": "iiii",
     "pcms_conv3_fwd_rows": "iiiiiiii",
     "pcms_conv3_big_min_boxes": "i",

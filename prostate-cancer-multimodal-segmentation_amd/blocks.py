@@ -60,8 +60,7 @@ class _Runner:
         cout = conv.out_channels
         if cout % 64:
             raise ValueError("the HIP conv kernels need a multiple of 64 output channels")
-        ck = query("pcms_conv3_chunk", self.code)
-        wpack = self.buf(-(-(c0 + c1) // ck) * 27 * cout * ck)
+        wpack = self.buf(query("pcms_conv3_pack_elems", self.code, cout, c0 + c1))
         call("pcms_conv3_pack", self.code, conv.weight.detach(), wpack, cout, conv.in_channels, 0)
         nvox = N * S[0] * S[1] * S[2]
         y = self.buf(nvox * cout)

@@ -18,7 +18,9 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 
 #define LDS_AS __attribute__((address_space(3)))
 
-enum { PCMS_F32 = 0, PCMS_BF16 = 1 };
+// dtype codes.  Activations: 0 fp32, 1 bf16.  The 3x3x3 conv entry points also take 2: fp32
+// data with the faster bf16x3 arithmetic (dtype 0 there means bf16x6, fp32-grade).
+enum { PCMS_F32 = 0, PCMS_BF16 = 1, PCMS_F32X3 = 2 };
 // conv epilogue flags (pcms_conv3_fwd, pcms_split_epilogue, pcms_stem_fwd)
 enum { PCMS_CONV_ACCUMULATE = 1, PCMS_CONV_RELU = 2 };
 // gradient writer flags (pcms_conv3_wgrad): store instead of accumulating

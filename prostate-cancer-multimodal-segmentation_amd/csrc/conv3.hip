@@ -64,20 +64,22 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
   }
   const bool wave_active = wave * 128 < boxvol;
 
-  // fp32 build: three-level summation (one MFMA chain per tap = 16 products, per-chunk sum,
-  // master) keeps the error at the level of a blocked CPU conv; bf16 build: one chain.
-  constexpr bool kF32 = sizeof(T) == 4;
-  f32x16_t acc[4][2], cacc[4][2], macc[4][2];
+  // fp32 data (x3_t / x6_t): the fp32 halo split into bf16 parts in LDS, three MFMAs per
+  // (M-tile, N-tile, tap) instead of two
+  constexpr bool kX3 = std::is_same<T, x3_t>::value, kX6 = std::is_same<T, x6_t>::value;
+  constexpr bool kSplit = kX3 || kX6;
+  typedef typename Tr::Mem M;
+  f32x16_t acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) { acc[i][j][e] = 0.f; cacc[i][j][e] = 0.f; macc[i][j][e] = 0.f; }
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const T* x0 = (const T*)p.x0;
-  const T* x1 = (const T*)p.x1;
-  const T* wp = (const T*)p.w;
+  const M* x0 = (const M*)p.x0;
+  const M* x1 = (const M*)p.x1;
+  const bf16_t* wp = (const bf16_t*)p.w;
   const long plane = (long)p.H * p.W;
 
   for (int chunk = cbeg; chunk < cend; ++chunk) {
@@ -95,7 +97,8 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
         const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
         const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
         const int c = chunk * Tr::CK + ql * Tr::VEC;
-        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
+        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin &&
+            ql * Tr::VEC < Tr::CK) {  // (x6: the row's slots 2, 3 stay zero)
           const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
           src = (c < p.c0) ? (const void*)(x0 + vox * p.c0 + c) : (const void*)(x1 + vox * p.c1 + (c - p.c0));
         }
@@ -104,45 +107,107 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (kX6) {
+      // split every 8-channel fp32 row in place into logical slots [h | m | l | 0]
+      for (int r = tid; r < HV; r += kThreads) {
+        char* row = lds + r * kRowBytes;
+        const int sw = swz(r);
+        const f32x4_t q0 = *reinterpret_cast<const f32x4_t*>(row + ((0 ^ sw) * 16));
+        const f32x4_t q1 = *reinterpret_cast<const f32x4_t*>(row + ((1 ^ sw) * 16));
+        const float f[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+        u32x4_t h, m, l;
+        split3x8(f, h, m, l);
+        *reinterpret_cast<u32x4_t*>(row + ((0 ^ sw) * 16)) = h;
+        *reinterpret_cast<u32x4_t*>(row + ((1 ^ sw) * 16)) = m;
+        *reinterpret_cast<u32x4_t*>(row + ((2 ^ sw) * 16)) = l;
+      }
+      __syncthreads();
+    }
+    if constexpr (kX3) {
+      // split every 16-channel fp32 row in place: logical 16-B slot s of the row (physical
+      // s ^ swz) = [hi 0-7, hi 8-15, lo 0-7, lo 8-15], so lds_a(ks = 0 / 1) reads hi / lo
+      for (int r = tid; r < HV; r += kThreads) {
+        char* row = lds + r * kRowBytes;
+        const int sw = swz(r);
+        f32x4_t q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const f32x4_t*>(row + ((k ^ sw) * 16));
+        u32x4_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const u32x2_t hl = split2(q[k][2 * i], q[k][2 * i + 1]);
+            o[k >> 1][(k & 1) * 2 + i] = hl[0];
+            o[2 + (k >> 1)][(k & 1) * 2 + i] = hl[1];
+          }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) *reinterpret_cast<u32x4_t*>(row + ((s ^ sw) * 16)) = o[s];
+      }
+      __syncthreads();
+    }
     if (!wave_active) continue;
 
-    const T* wchunk = wp + (long)chunk * 27 * p.Cout * Tr::CK;
-    // B fragments rotate through 3 register sets: the loads of tap t+2 are issued while
-    // tap t computes (kw unrolled, so every set index is a compile-time constant).
-    Frag bset[3][2][Tr::KS];
+    const bf16_t* wchunk = wp + (long)chunk * 27 * p.Cout * Tr::WK;
+    Frag bset[2][2][Tr::KS];
     auto load_b = [&](Frag (&dst)[2][Tr::KS], int tap) {
-      const T* wt = wchunk + ((long)tap * p.Cout + co_base + r_lane) * Tr::CK;
+      const bf16_t* wt = wchunk + ((long)tap * p.Cout + co_base + r_lane) * Tr::WK;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int ks = 0; ks < Tr::KS; ++ks) dst[nt][ks] = gl_b(wt + nt * 32 * Tr::CK, ks, hsel);
+        for (int ks = 0; ks < Tr::KS; ++ks) dst[nt][ks] = gl_b(wt + nt * 32 * Tr::WK, ks, hsel);
     };
     load_b(bset[0], 0);
-    load_b(bset[1], 1);
-    if constexpr (!kF32) {
-      // bf16: the A fragments roll through one register set: right after M-tile mt's MFMAs of
-      // tap t its fragment of tap t + 1 is read (15 MFMAs of slack before its first use)
-      // instead of one read -> wait -> two MFMAs per fragment.  B: two register sets, tap t + 1
-      // loaded while tap t computes (a third set, two taps ahead, pushed the kernel past 256
-      // VGPRs into spills with a reload inside this loop); taps walked two (kd, kh) rows per
-      // trip so every set index is a compile-time constant.
-      s16x8_t a[2][4];
+    // The A fragments roll through one register set: right after M-tile mt's MFMAs of tap t
+    // its fragment of tap t + 1 is read (15 MFMAs of slack before its first use) instead of
+    // one read -> wait -> two MFMAs per fragment.  B: two register sets, tap t + 1 loaded
+    // while tap t computes (a third set, two taps ahead, pushed the kernel past 256 VGPRs into
+    // spills with a reload inside this loop); taps walked two (kd, kh) rows per trip so every
+    // set index is a compile-time constant.
+    // x6: a[0] = [h|m], a[1] = [h|l] (logical slot 2 * hsel)
+    auto frag1 = [&](int row) __attribute__((always_inline)) {
+      if constexpr (kX6) return lds_slot(lds, row, 2 * hsel);
+      else return lds_a(lds, row, 1, hsel);
+    };
+    s16x8_t a[2][4];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+    for (int mt = 0; mt < 4; ++mt) {
+      a[0][mt] = lds_a(lds, hb[mt], 0, hsel);
+      a[1][mt] = frag1(hb[mt]);
+    }
+    auto tap_step = [&](int tap, int set, const int (&hbk)[4]) {
+      load_b(bset[set ^ 1], min(tap + 1, 26));
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
+      const int tn = tap + 1 < 27 ? tap + 1 : 0;
+      const int offn = ((tn / 9) * HH + (tn / 3) % 3) * HW + tn % 3;
+      if constexpr (kSplit) {
+        // x3: hi*hi + lo*hi + hi*lo (a[0] = hi, a[1] = lo; B ks 0 = hi, 1 = lo)
+        // x6: [h|m].[h|h] + [h|l].[m|h] + [h|m].[l|m] (a[0], a[1]; B ks 0, 1, 2)
+        constexpr int b1 = kX6 ? 1 : 0, b2 = kX6 ? 2 : 1;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) a[ks][mt] = lds_a(lds, hb[mt], ks, hsel, (T*)nullptr);
-      auto tap_step = [&](int tap, int set, const int (&hbk)[4]) {
-        load_b(bset[set ^ 1], min(tap + 1, 26));
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
-        const int tn = tap + 1 < 27 ? tap + 1 : 0;
-        const int offn = ((tn / 9) * HH + (tn / 3) % 3) * HW + tn % 3;
+        for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[0][mt], bset[set][nt][0], acc[mt][nt]);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[1][mt], bset[set][nt][b1], acc[mt][nt]);
+          a[1][mt] = frag1(hbk[mt] + offn);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[0][mt], bset[set][nt][b2], acc[mt][nt]);
+          a[0][mt] = lds_a(lds, hbk[mt] + offn, 0, hsel);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // 3 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+      } else {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[ks][mt], bset[set][nt][ks], acc[mt][nt]);
-            a[ks][mt] = lds_a(lds, hbk[mt] + offn, ks, hsel, (T*)nullptr);
+            a[ks][mt] = lds_a(lds, hbk[mt] + offn, ks, hsel);
           }
         // (the scheduler would otherwise sink all eight reads below the last MFMA)
 #pragma unroll
@@ -150,74 +215,24 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
         }
-      };
-      for (int kdh = 0; kdh < 8; kdh += 2) {
-        // row bases from an opaque copy: the fragment addresses are recomputed per trip rather
-        // than hoisted out of the loops (and spilled)
-        int hbk[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) tap_step(kdh * 3 + j, j & 1, hbk);
       }
-      {
-        int hbk[4];
+    };
+    for (int kdh = 0; kdh < 8; kdh += 2) {
+      // row bases from an opaque copy: the fragment addresses are recomputed per trip rather
+      // than hoisted out of the loops (and spilled)
+      int hbk[4];
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
+      for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) tap_step(24 + j, j & 1, hbk);
-      }
-      continue;
+      for (int j = 0; j < 6; ++j) tap_step(kdh * 3 + j, j & 1, hbk);
     }
-    for (int kdh = 0; kdh < 9; ++kdh) {
-      const int kd = kdh / 3, kh = kdh % 3;
+    {
+      int hbk[4];
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int tap = kdh * 3 + kw;
-        if (tap + 2 < 27) load_b(bset[(kw + 2) % 3], tap + 2);
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
-        const int off = (kd * HH + kh) * HW + kw;
-        if constexpr (kF32) {
+      for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-        }
-#pragma unroll
-        for (int ks = 0; ks < Tr::KS; ++ks) {
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) {
-            Frag a = lds_a(lds, hb[mt] + off, ks, hsel, (T*)nullptr);
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a, bset[kw][nt][ks], acc[mt][nt]);
-          }
-        }
-        if constexpr (kF32) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) cacc[i][j] += acc[i][j];
-        }
-      }
+      for (int j = 0; j < 3; ++j) tap_step(24 + j, j & 1, hbk);
     }
-    if constexpr (kF32) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          macc[i][j] += cacc[i][j];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) cacc[i][j][e] = 0.f;
-        }
-    }
-  }
-  if constexpr (kF32) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = macc[i][j];
   }
 
   // ---- epilogue ----
@@ -252,7 +267,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
   constexpr int kRedOff = 512 * 64 * 2;  // bf16 C tile [512][64] occupies the first 64 KiB
   // (PCMS_CONV_RELU, eval with the BatchNorm folded into w / b: tested where used, from the
   // kernel argument -- a flag held across the epilogue cost a spill)
-  if (!kF32 && !p.yacc && !(p.accumulate & PCMS_CONV_ACCUMULATE)) {
+  if (!kSplit && !p.yacc && !(p.accumulate & PCMS_CONV_ACCUMULATE)) {
     // bf16 fast path: + bias, stats from the fp32 values, C tile -> LDS (box order), then
     // 16-byte coalesced stores (one box row = a contiguous w-run of voxels).
     __syncthreads();  // every wave is done reading the halo
@@ -282,7 +297,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
       if (!interior && (gd >= p.D || gh >= p.H || gw >= p.W)) continue;
       const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
       const int co = co_base + q * 8;
-      T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
+      M* dst = (co < p.cy0) ? (M*)p.y0 + vox * p.cy0 + co : (M*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
       u32x4_t o = *reinterpret_cast<const u32x4_t*>(ct + r * 64 + q * 8);
       if (p.accumulate & PCMS_CONV_RELU) o = relu_bf16x8(o);
       *reinterpret_cast<u32x4_t*>(dst) = o;
@@ -307,11 +322,11 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
             continue;
           }
           v += bias_l[nt];
-          T* dst = (co < p.cy0) ? (T*)p.y0 + vox * p.cy0 + co
-                                : (T*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
-          if (p.accumulate & PCMS_CONV_ACCUMULATE) v += Elem<T>::ld(dst);  // (stats are refused with accumulate)
+          M* dst = (co < p.cy0) ? (M*)p.y0 + vox * p.cy0 + co
+                                : (M*)p.y1 + vox * (p.Cout - p.cy0) + (co - p.cy0);
+          if (p.accumulate & PCMS_CONV_ACCUMULATE) v += Elem<M>::ld(dst);  // (stats are refused with accumulate)
           if (p.accumulate & PCMS_CONV_RELU) v = fmaxf(v, 0.f);
-          Elem<T>::st(dst, v);
+          Elem<M>::st(dst, v);
           s1[nt] += v;
         }
       }
@@ -343,7 +358,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
         }
     }
     __syncthreads();  // halo / C tile no longer read: reuse LDS for the cross-wave reduction
-    float* red = reinterpret_cast<float*>(lds + (kF32 ? 0 : kRedOff));
+    float* red = reinterpret_cast<float*>(lds + (kSplit ? 0 : kRedOff));
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       s2[nt] += __shfl_xor(s2[nt], 32, 64);
@@ -398,16 +413,31 @@ template <> struct WTraits<bf16_t> {
   static constexpr int DYROW = 128;     // 64 co x 2 B
   static constexpr int XROW = 64;       // 32 ci x 2 B
   static constexpr int VEC = 8;
+  static constexpr int HALO = kWHaloMax;
+  static constexpr int NPART = 1;
   typedef s16x8_t Frag;
 };
-template <> struct WTraits<float> {
-  static constexpr int BV = 128;
-  static constexpr int KV = 2;
+template <> struct WTraits<x6_t> {
+  static constexpr int BV = 128;        // voxels per staged box (h, m, l tiles: 3 x 43 KB)
+  static constexpr int KV = 8;          // voxels per MFMA k-step (K halves concatenated)
   static constexpr int NBUF = 1;
-  static constexpr int DYROW = 256;     // 64 co x 4 B
-  static constexpr int XROW = 128;      // 32 ci x 4 B
+  static constexpr int DYROW = 128;
+  static constexpr int XROW = 64;
   static constexpr int VEC = 4;
-  typedef float Frag;
+  static constexpr int HALO = 432;
+  static constexpr int NPART = 3;
+  typedef s16x8_t Frag;
+};
+template <> struct WTraits<x3_t> {
+  static constexpr int BV = 128;        // voxels per staged box (hi + lo tiles: 2 x 62 KB)
+  static constexpr int KV = 16;
+  static constexpr int NBUF = 1;
+  static constexpr int DYROW = 128;     // LDS rows as bf16 (one tile per half)
+  static constexpr int XROW = 64;
+  static constexpr int VEC = 4;         // fp32 elements per 16-B global piece
+  static constexpr int HALO = kWHaloMax;
+  static constexpr int NPART = 2;
+  typedef s16x8_t Frag;
 };
 
 struct WgradParams {
@@ -432,18 +462,18 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   typedef WTraits<T> Tr;
   typedef typename Tr::Frag Frag;
   constexpr int DYBYTES = Tr::BV * Tr::DYROW;
-  constexpr int XBYTES = kWHaloMax * Tr::XROW;
+  constexpr int XBYTES = Tr::HALO * Tr::XROW;
   constexpr int BUFBYTES = DYBYTES + XBYTES;
   extern __shared__ __attribute__((aligned(16))) char wlds[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hsel = lane >> 5;
-  const int cot = wave & 1;           // co tile (32 rows of the 64-wide dy tile)
-  const int tg = wave >> 1;           // taps tg, tg+4, ...
-  const int ntap = (tg == 3) ? 6 : 7;
-  // bf16 layout: wave w owns taps w, w + 8, w + 16 (, w + 24) for BOTH co tiles, so each B
-  // (x) fragment feeds 2 MFMAs: 1.5 LDS reads per MFMA instead of 2.3 (8 accumulators)
-  constexpr bool kW2 = sizeof(T) == 2;
+  // wave w owns taps w, w + 8, w + 16 (, w + 24) for BOTH co tiles, so each B (x) fragment
+  // feeds 2 MFMAs: 1.5 LDS reads per MFMA instead of 2.3 (8 accumulators)
+  // fp32 data, split-bf16 products: x3 (hi, lo tiles) / x6 (h, m, l tiles), the parts
+  // BUFBYTES apart
+  constexpr bool kX3 = std::is_same<T, x3_t>::value, kX6 = std::is_same<T, x6_t>::value;
+  typedef typename std::conditional<kX3 || kX6, float, bf16_t>::type M;
   const int ntap2 = wave < 3 ? 4 : 3;
   // 1-D grid, logical id XCD-aware (dispatch is round-robin over 8 XCDs: consecutive logical
   // ids land on one XCD at about the same time), tile (co block, ci block) fastest: the
@@ -458,9 +488,9 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   const int HV = (bd + 2) * HH * HW;
   const int boxvol = bd * bh * bw;
   const long plane = (long)p.H * p.W;
-  const T* x0 = (const T*)p.x0;
-  const T* x1 = (const T*)p.x1;
-  const T* dy = (const T*)p.dy;
+  const M* x0 = (const M*)p.x0;
+  const M* x1 = (const M*)p.x1;
+  const M* dy = (const M*)p.dy;
 
   const int b_beg = split * p.boxes_per_split;
   const int b_end = min(p.nbox, b_beg + p.boxes_per_split);
@@ -535,38 +565,63 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     }
   };
 
-  // fp32 build: stage without a register array (one 16-B piece in flight per thread)
-  auto stage_direct = [&](char* buf, int b) {
+  // fp32 build: every 16-B piece (4 fp32) of the box's dy tile and x halo loaded into
+  // registers (all in flight), then split into the hi tile at buf and the lo tile at
+  // buf + BUFBYTES (the bf16 layouts: dy_off_bf16 rows, 64-B halo rows)
+  auto stage_x3 = [&](char* buf, int b) {
     int n, d0, h0, w0;
     box_origin(b, n, d0, h0, w0);
-    for (int pc = tid; pc < DYP + XP; pc += kWThreads) {
-      u32x4_t v = {0u, 0u, 0u, 0u};
-      int off;
-      if (pc < DYP) {
-        const int r = pc / (Tr::DYROW / 16), q = pc % (Tr::DYROW / 16);
-        off = r * Tr::DYROW + q * 16;
-        if (r < boxvol) {
+    constexpr int DYQ = Tr::BV * 16;                      // 64 co / 4 per piece
+    constexpr int XQMAX = Tr::HALO * 8;                   // 32 ci / 4
+    constexpr int PER = (DYQ + XQMAX + kWThreads - 1) / kWThreads;
+    constexpr int RND = 8;                                // pieces in flight per thread (VGPRs)
+    const int XQ = HV * 8;
+#pragma unroll
+    for (int i0 = 0; i0 < PER; i0 += RND) {
+      f32x4_t v[RND];
+#pragma unroll
+      for (int i = 0; i < RND; ++i) {
+        const int pc = tid + (i0 + i) * kWThreads;
+        const float* src = reinterpret_cast<const float*>(g_zero16);
+        if (pc < DYQ) {
+          const int r = pc >> 4, q = pc & 15;
           const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
           const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
-          if (gd < p.D && gh < p.H && gw < p.W) {
+          if (r < boxvol && gd < p.D && gh < p.H && gw < p.W)
+            src = reinterpret_cast<const float*>(dy) + (((long)n * p.D + gd) * plane + (long)gh * p.W + gw) * p.Cout + co_base + q * 4;
+        } else if (pc < DYQ + XQ) {
+          const int hp = pc - DYQ, hv = hp >> 3, q = hp & 7;
+          const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+          const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+          const int c = ci_base + q * 4;
+          if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
             const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
-            v = *reinterpret_cast<const u32x4_t*>(dy + vox * p.Cout + co_base + q * Tr::VEC);
+            src = (c < p.c0) ? reinterpret_cast<const float*>(x0) + vox * p.c0 + c
+                             : reinterpret_cast<const float*>(x1) + vox * p.c1 + (c - p.c0);
           }
         }
-      } else {
-        const int hp = pc - DYP;
-        off = DYBYTES + hp * 16;
-        const int hv = hp / (Tr::XROW / 16), q = hp % (Tr::XROW / 16);
-        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
-        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
-        const int c = ci_base + q * Tr::VEC;
-        if (gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && c < p.Cin) {
-          const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
-          const T* src = (c < p.c0) ? x0 + vox * p.c0 + c : x1 + vox * p.c1 + (c - p.c0);
-          v = *reinterpret_cast<const u32x4_t*>(src);
+        v[i] = *reinterpret_cast<const f32x4_t*>(src);
+      }
+#pragma unroll
+      for (int i = 0; i < RND; ++i) {
+        const int pc = tid + (i0 + i) * kWThreads;
+        int off;
+        if (pc < DYQ) off = dy_off_bf16(pc >> 4, (pc & 15) * 4);
+        else if (pc < DYQ + XQ) off = DYBYTES + (pc - DYQ) * 8;
+        else continue;
+        if constexpr (kX6) {
+          const float f[8] = {v[i][0], v[i][1], v[i][2], v[i][3], 0.f, 0.f, 0.f, 0.f};
+          u32x4_t h, m, l;
+          split3x8(f, h, m, l);
+          *reinterpret_cast<u32x2_t*>(buf + off) = (u32x2_t){h[0], h[1]};
+          *reinterpret_cast<u32x2_t*>(buf + BUFBYTES + off) = (u32x2_t){m[0], m[1]};
+          *reinterpret_cast<u32x2_t*>(buf + 2 * BUFBYTES + off) = (u32x2_t){l[0], l[1]};
+        } else {
+          const u32x2_t h01 = split2(v[i][0], v[i][1]), h23 = split2(v[i][2], v[i][3]);
+          *reinterpret_cast<u32x2_t*>(buf + off) = (u32x2_t){h01[0], h23[0]};
+          *reinterpret_cast<u32x2_t*>(buf + BUFBYTES + off) = (u32x2_t){h01[1], h23[1]};
         }
       }
-      *reinterpret_cast<u32x4_t*>(buf + off) = v;
     }
   };
 
@@ -576,57 +631,85 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     return (rd * HH + rh) * HW + rw;
   };
 
+  // generic box: one 16-voxel k-step at a time.  x3: the lo tiles sit BUFBYTES past the hi
+  // tiles; per (co tile, tap) hi*hi + lo*hi + hi*lo
   auto compute = [&](const char* buf) {
     const char* xb = buf + DYBYTES;
 #pragma unroll 2
     for (int k0 = 0; k0 < boxvol; k0 += Tr::KV) {
-      Frag a;
-      Frag bf[7];
-      if constexpr (kW2) {
-        const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-        const int v_a = k0 + 8 * hsel + qq;
-        s16x8_t a2[2];
+      const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
+      auto frag = [](const char* base, int o0, int o1) __attribute__((always_inline)) {
+        const s16x4_t l = tr_read(base, o0), h = tr_read(base, o1);
+        return (s16x8_t){l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+      };
+      if constexpr (kX6) {
+        // 8 voxels per k-step, both K halves over the same voxels from different parts:
+        // A1 = [dy h | dy m], A2 = [dy h | dy l]; B1 = [x h | x h], B2 = [x m | x h],
+        // B3 = [x l | x m]; A1.B1 + A2.B2 + A1.B3 = hh + mh + hm + lh + hl + mm
+        const int v_a = k0 + qq;
+        const char* dA1 = buf + hsel * BUFBYTES;
+        const char* dA2 = buf + hsel * 2 * BUFBYTES;
+        s16x8_t a1[2], a2[2];
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
           const int co = ct * 32 + g * 16 + pp * 4;
-          s16x4_t lo = tr_read(buf, dy_off_bf16(v_a, co));
-          s16x4_t hi = tr_read(buf, dy_off_bf16(v_a + 4, co));
-          a2[ct] = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const int o0 = dy_off_bf16(v_a, co), o1 = dy_off_bf16(v_a + 4, co);
+          a1[ct] = frag(dA1, o0, o1);
+          a2[ct] = frag(dA2, o0, o1);
         }
-        const int hr0 = LBW >= 4 ? halo_row(k0) + 8 * hsel + qq : halo_row(v_a);
-        const int hr1 = LBW >= 4 ? hr0 + 4 : halo_row(v_a + 4);
+        const int hr0 = halo_row(v_a), hr1 = halo_row(v_a + 4);
         const int ci = g * 16 + pp * 4;
+        const char* xb1 = xb;                                     // B1: h | h
+        const char* xb2 = xb + (hsel ? 0 : BUFBYTES);            // B2: m | h
+        const char* xb3 = xb + (hsel ? BUFBYTES : 2 * BUFBYTES);  // B3: l | m
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j < ntap2) {
             const int tap = wave + 8 * j;
             const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
             const int off = (kd * HH + kh) * HW + kw;
-            s16x4_t l2 = tr_read(xb, (hr0 + off) * Tr::XROW + ci * 2);
-            s16x4_t h2 = tr_read(xb, (hr1 + off) * Tr::XROW + ci * 2);
-            const s16x8_t b = (s16x8_t){l2[0], l2[1], l2[2], l2[3], h2[0], h2[1], h2[2], h2[3]};
-            acc[j] = mfma(a2[0], b, acc[j]);
-            acc[4 + j] = mfma(a2[1], b, acc[4 + j]);
+            const int o0 = (hr0 + off) * Tr::XROW + ci * 2, o1 = (hr1 + off) * Tr::XROW + ci * 2;
+            const s16x8_t b1 = frag(xb1, o0, o1), b2 = frag(xb2, o0, o1), b3 = frag(xb3, o0, o1);
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+              acc[4 * ct + j] = mfma(a1[ct], b1, acc[4 * ct + j]);
+              acc[4 * ct + j] = mfma(a2[ct], b2, acc[4 * ct + j]);
+              acc[4 * ct + j] = mfma(a1[ct], b3, acc[4 * ct + j]);
+            }
           }
         }
         continue;
-      } else {
-        const int v = k0 + hsel;
-        a = *reinterpret_cast<const float*>(buf + v * Tr::DYROW + (cot * 32 + (lane & 31)) * 4);
-        const int hr = halo_row(v);
+      }
+      const int v_a = k0 + 8 * hsel + qq;
+      s16x8_t a2[2], a2l[2];
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {
-          if (j < ntap) {
-            const int tap = tg + 4 * j;
-            const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-            const int off = (kd * HH + kh) * HW + kw;
-            bf[j] = *reinterpret_cast<const float*>(xb + (hr + off) * Tr::XROW + (lane & 31) * 4);
+      for (int ct = 0; ct < 2; ++ct) {
+        const int co = ct * 32 + g * 16 + pp * 4;
+        a2[ct] = frag(buf, dy_off_bf16(v_a, co), dy_off_bf16(v_a + 4, co));
+        if constexpr (kX3) a2l[ct] = frag(buf + BUFBYTES, dy_off_bf16(v_a, co), dy_off_bf16(v_a + 4, co));
+      }
+      const int hr0 = LBW >= 4 ? halo_row(k0) + 8 * hsel + qq : halo_row(v_a);
+      const int hr1 = LBW >= 4 ? hr0 + 4 : halo_row(v_a + 4);
+      const int ci = g * 16 + pp * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < ntap2) {
+          const int tap = wave + 8 * j;
+          const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+          const int off = (kd * HH + kh) * HW + kw;
+          const int o0 = (hr0 + off) * Tr::XROW + ci * 2, o1 = (hr1 + off) * Tr::XROW + ci * 2;
+          const s16x8_t b = frag(xb, o0, o1);
+          acc[j] = mfma(a2[0], b, acc[j]);
+          acc[4 + j] = mfma(a2[1], b, acc[4 + j]);
+          if constexpr (kX3) {
+            const s16x8_t bl = frag(xb + BUFBYTES, o0, o1);
+            acc[j] = mfma(a2l[0], b, acc[j]);
+            acc[4 + j] = mfma(a2l[1], b, acc[4 + j]);
+            acc[j] = mfma(a2[0], bl, acc[j]);
+            acc[4 + j] = mfma(a2[1], bl, acc[4 + j]);
           }
         }
       }
-#pragma unroll
-      for (int j = 0; j < 7; ++j)
-        if (j < ntap) acc[j] = mfma(a, bf[j], acc[j]);
     }
   };
 
@@ -691,7 +774,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     });
   };
   auto compute_box = [&](const char* buf) __attribute__((always_inline)) {
-    if constexpr (kW2 && LBW >= 3) compute_fixed(buf);
+    if constexpr (!kX3 && !kX6 && LBW >= 3) compute_fixed(buf);
     else compute(buf);
   };
 
@@ -761,26 +844,14 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         __syncthreads();
       }
     } else {
-      // fp32 build: per-box MFMA chains summed into a master accumulator (two-level sum)
-      f32x16_t macc[7];
-#pragma unroll
-      for (int t = 0; t < 7; ++t)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) macc[t][e] = 0.f;
+      // fp32 build: synchronous staging (all of a box's loads in flight, split on the way
+      // into LDS), then the box's MFMAs
       for (int b = b_beg; b < b_end; ++b) {
         __syncthreads();
-        stage_direct(wlds, b);
+        stage_x3(wlds, b);
         __syncthreads();
-#pragma unroll
-        for (int t = 0; t < 7; ++t)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
         compute(wlds);
-#pragma unroll
-        for (int t = 0; t < 7; ++t) macc[t] += acc[t];
       }
-#pragma unroll
-      for (int t = 0; t < 7; ++t) acc[t] = macc[t];
     }
   }
 
@@ -790,7 +861,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // split into one [27][Cout][Cin] image serialised on the contended addresses: 2-4x the
   // kernel's own time at level 0.)
   float* prow = p.dwt + (long)split * 27 * p.Cout * p.Cin;
-  if constexpr (kW2) {
+  {
     if (p.direct) {
       // one split: no partial rows to reduce.  Per 32-row co half, the workgroup's
       // [32 co][32 ci][27 taps] tile is transposed through LDS (the staging buffers are free)
@@ -856,18 +927,6 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           if (co < p.Cout && ci < p.Cin) prow[((long)tap * p.Cout + co) * p.Cin + ci] = acc[ct * 4 + j][e];
         }
     }
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    if (j >= ntap) continue;
-    const int tap = tg + 4 * j;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int co = co_base + cot * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
-      const int ci = ci_base + (lane & 31);
-      if (co < p.Cout && ci < p.Cin) prow[((long)tap * p.Cout + co) * p.Cin + ci] = acc[j][e];
-    }
   }
 }
 
@@ -930,7 +989,24 @@ __global__ void __launch_bounds__(256) pack_conv3_kernel(const float* w, T* out,
     const int k = e % CK, jj = (e / CK) % 8, t = e / (CK * 8);
     if (j0 + jj >= J) continue;
     const float v = flip ? tile[jj][k][26 - t] : tile[jj][k][t];
-    out[(((long)chunk * 27 + t) * J + j0 + jj) * CK + k] = Elem<T>::cvt(v);
+    if constexpr (std::is_same<T, x3_t>::value) {
+      // split-bf16 pack row [hi k = 0..15 | lo k = 0..15]
+      bf16_t* o = reinterpret_cast<bf16_t*>(out) + (((long)chunk * 27 + t) * J + j0 + jj) * 2 * CK;
+      const bf16_t hi = f2bf(v);
+      o[k] = hi;
+      o[CK + k] = f2bf(v - bf2f(hi));
+    } else if constexpr (std::is_same<T, x6_t>::value) {
+      // three-part pack row: the B fragments [h|h] [m|h] [l|m] (k = 0..7 each half)
+      bf16_t* o = reinterpret_cast<bf16_t*>(out) + (((long)chunk * 27 + t) * J + j0 + jj) * 6 * CK;
+      const bf16_t h = f2bf(v);
+      const float r = v - bf2f(h);
+      const bf16_t m = f2bf(r), l = f2bf(r - bf2f(m));
+      o[k] = h; o[CK + k] = h;
+      o[2 * CK + k] = m; o[3 * CK + k] = h;
+      o[4 * CK + k] = l; o[5 * CK + k] = m;
+    } else {
+      out[(((long)chunk * 27 + t) * J + j0 + jj) * CK + k] = Elem<T>::cvt(v);
+    }
   }
 }
 
@@ -1464,7 +1540,18 @@ int pcms_conv3_big_max_wgs(int v) {
   return old;
 }
 
-int pcms_conv3_chunk(int dtype) { return dtype == PCMS_BF16 ? Traits<bf16_t>::CK : Traits<float>::CK; }
+int pcms_conv3_chunk(int dtype) {
+  return dtype == PCMS_BF16 ? Traits<bf16_t>::CK : dtype == PCMS_F32X3 ? Traits<x3_t>::CK : Traits<x6_t>::CK;
+}
+
+// elements (of the activation dtype: bf16, or fp32 for both split modes) of one conv weight
+// pack with J output rows and Kdim input channels: [ceil(Kdim / CK)][27][J][WK] bf16
+int pcms_conv3_pack_elems(int dtype, int J, int Kdim) {
+  const int ck = pcms_conv3_chunk(dtype);
+  const int wk = dtype == PCMS_BF16 ? Traits<bf16_t>::WK : dtype == PCMS_F32X3 ? Traits<x3_t>::WK : Traits<x6_t>::WK;
+  const long bf16s = (long)cdiv(Kdim, ck) * 27 * J * wk;
+  return (int)(dtype == PCMS_BF16 ? bf16s : bf16s / 2);
+}
 
 // forward and dgrad packs together (one weight read); other shapes / dtypes: the two packs
 int pcms_conv3_pack2(int dtype, const float* w, void* fwd, void* dgrad, int Cout, int Cin, hipStream_t s) {
@@ -1497,8 +1584,10 @@ int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int
     hipLaunchKernelGGL(pack_conv3_bf16_kernel, grid, dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip);
   else if (dtype == PCMS_BF16)
     hipLaunchKernelGGL((pack_conv3_kernel<bf16_t, 32>), grid, dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip);
+  else if (dtype == PCMS_F32X3)
+    hipLaunchKernelGGL((pack_conv3_kernel<x3_t, 16>), grid, dim3(256), 0, s, w, (x3_t*)out, Cout, Cin, flip);
   else
-    hipLaunchKernelGGL((pack_conv3_kernel<float, 16>), grid, dim3(256), 0, s, w, (float*)out, Cout, Cin, flip);
+    hipLaunchKernelGGL((pack_conv3_kernel<x6_t, 8>), grid, dim3(256), 0, s, w, (x6_t*)out, Cout, Cin, flip);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -1559,8 +1648,12 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   if (dtype == PCMS_BF16) {
     if (hot) hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2, 2, 3, 4>), grid, dim3(kThreads), 0, s, p);
     else hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
+  } else if (dtype == PCMS_F32X3) {
+    if (hot) hipLaunchKernelGGL((conv3_fwd_kernel<x3_t, 2, 2, 3, 4>), grid, dim3(kThreads), 0, s, p);
+    else hipLaunchKernelGGL((conv3_fwd_kernel<x3_t, 2, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
   } else {
-    hipLaunchKernelGGL((conv3_fwd_kernel<float, 1, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
+    if (hot) hipLaunchKernelGGL((conv3_fwd_kernel<x6_t, 2, 2, 3, 4>), grid, dim3(kThreads), 0, s, p);
+    else hipLaunchKernelGGL((conv3_fwd_kernel<x6_t, 2, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
   }
   PCMS_CHECK_LAUNCH();
 }
@@ -1572,8 +1665,9 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
 struct WgradPlan { Box b; int nbd, nbh, nbw, nbox, bps, splits; };
 static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int Cout, int target_wgs) {
   WgradPlan q;
-  const int bv = dtype == PCMS_BF16 ? WTraits<bf16_t>::BV : WTraits<float>::BV;
-  q.b = choose_box(D, H, W, bv, kWHaloMax, 4, 16);
+  const int bv = dtype == PCMS_BF16 ? WTraits<bf16_t>::BV : dtype == PCMS_F32X3 ? WTraits<x3_t>::BV : WTraits<x6_t>::BV;
+  const int halo = dtype == PCMS_F32 ? WTraits<x6_t>::HALO : kWHaloMax;
+  q.b = choose_box(D, H, W, bv, halo, 4, 16);
   q.nbd = cdiv(D, 1 << q.b.lbd); q.nbh = cdiv(H, 1 << q.b.lbh); q.nbw = cdiv(W, 1 << q.b.lbw);
   q.nbox = N * q.nbd * q.nbh * q.nbw;
   const int tiles = (Cout / 64) * cdiv(Cin, 32);
@@ -1620,7 +1714,7 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   p.nci = cdiv(Cin, 32);
   p.dw = dw;
   p.cw = cin_w;
-  p.direct = splits == 1 && dtype == PCMS_BF16;
+  p.direct = splits == 1;
   p.store = flags & PCMS_GRAD_STORE;
   dim3 grid(splits * p.nco * p.nci);
   size_t lds;
@@ -1632,10 +1726,16 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
     else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
+  } else if (dtype == PCMS_F32X3) {
+    typedef WTraits<x3_t> X;
+    lds = (size_t)X::NPART * (X::BV * X::DYROW + X::HALO * X::XROW);
+    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<x3_t, -1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((conv3_wgrad_kernel<x3_t, -1, -1, -1>), grid, dim3(kWThreads), lds, s, p);
   } else {
-    lds = (size_t)WTraits<float>::NBUF * (WTraits<float>::BV * WTraits<float>::DYROW + kWHaloMax * WTraits<float>::XROW);
-    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<float, -1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((conv3_wgrad_kernel<float, -1, -1, -1>), grid, dim3(kWThreads), lds, s, p);
+    typedef WTraits<x6_t> X;
+    lds = (size_t)X::NPART * (X::BV * X::DYROW + X::HALO * X::XROW);
+    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<x6_t, -1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((conv3_wgrad_kernel<x6_t, -1, -1, -1>), grid, dim3(kWThreads), lds, s, p);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;

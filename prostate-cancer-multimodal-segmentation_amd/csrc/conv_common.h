@@ -13,26 +13,65 @@ constexpr int kHaloMax = 1152;     // halo voxels per workgroup (72 KiB LDS, 2 W
 __device__ __attribute__((aligned(16))) uint32_t g_zero16[4];  // zero page for LDS-DMA padding
 constexpr uint32_t kOOB = 0x80000000u;  // buffer voffset past num_records: reads zeros
 
+// fp32 data in HBM, split-bf16 arithmetic on the bf16 MFMA (the halo is split in LDS once per
+// chunk, the weights in their pack):
+//  x6_t (dtype PCMS_F32, the parity build): v = h + m + l, three bf16 parts (24 significant
+//       bits: v to fp32 rounding); a product keeps the six terms down to 2^-16 of it (hh, hm,
+//       mh, hl, lh, mm) in THREE MFMAs over 8 channels, by concatenating K halves:
+//       [h|m].[h|h] + [h|l].[m|h] + [h|m].[l|m];
+//  x3_t (dtype PCMS_F32X3): v = h + l (16 bits), hh + lh + hl in three MFMAs over 16
+//       channels: twice the rate, ~10x the fp32 rounding error (measured: misses the
+//       north-star 1e-3 logit bar by ~30 %; kept as an explicit faster mode).
+struct x3_t {};
+struct x6_t {};
+
 template <typename T> struct Traits;
 template <> struct Traits<bf16_t> {
   static constexpr int CK = 32;    // channels per chunk (64 B rows)
   static constexpr int KS = 2;     // MFMA k-steps per chunk and tap (K = 16 each)
   static constexpr int VEC = 8;    // elements per 16-byte piece
+  static constexpr int WK = 32;    // bf16 weights per pack row
   typedef s16x8_t Frag;
+  typedef bf16_t Mem;              // activation element in HBM
 };
-template <> struct Traits<float> {
-  static constexpr int CK = 16;
-  static constexpr int KS = 8;     // K = 2 each
+template <> struct Traits<x3_t> {
+  static constexpr int CK = 16;    // fp32 channels per chunk (64 B rows, split in place into
+  static constexpr int KS = 2;     //   [hi 0-7 | hi 8-15 | lo 0-7 | lo 8-15]: "k-step" 0 = hi, 1 = lo)
   static constexpr int VEC = 4;
-  typedef float Frag;
+  static constexpr int WK = 32;    // pack row: 16 hi weights, then their 16 lo parts
+  typedef s16x8_t Frag;
+  typedef float Mem;
 };
+template <> struct Traits<x6_t> {
+  static constexpr int CK = 8;     // fp32 channels per chunk (32 B of a 64-B row, split in
+  static constexpr int KS = 3;     //   place into logical slots [h 0-7 | m 0-7 | l 0-7 | -])
+  static constexpr int VEC = 4;
+  static constexpr int WK = 48;    // pack row: the three B fragments [h|h] [m|h] [l|m]
+  typedef s16x8_t Frag;
+  typedef float Mem;
+};
+// three bf16 parts of 8 floats (h, m, l: 8 packed bf16 each)
+__device__ __forceinline__ void split3x8(const float* f, u32x4_t& h, u32x4_t& m, u32x4_t& l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = f[2 * i], b = f[2 * i + 1];
+    const uint32_t hh = pack_bf16x2(a, b);
+    const float ra = a - __uint_as_float(hh << 16), rb = b - __uint_as_float(hh & 0xffff0000u);
+    const uint32_t mm = pack_bf16x2(ra, rb);
+    h[i] = hh;
+    m[i] = mm;
+    l[i] = pack_bf16x2(ra - __uint_as_float(mm << 16), rb - __uint_as_float(mm & 0xffff0000u));
+  }
+}
 
 __device__ __forceinline__ f32x16_t mfma(s16x8_t a, s16x8_t b, f32x16_t c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
-__device__ __forceinline__ f32x16_t mfma(float a, float b, f32x16_t c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+// two floats -> {hi, lo}: their bf16 halves, each packed bf16x2 (element 0 in the low half)
+__device__ __forceinline__ u32x2_t split2(float a, float b) {
+  const uint32_t hi = pack_bf16x2(a, b);
+  return (u32x2_t){hi, pack_bf16x2(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u))};
 }
 
 // 16-byte slot swizzle inside a 64-byte halo row (spreads ds_read_b128 lane groups).
@@ -52,20 +91,18 @@ __device__ __forceinline__ int perm32(int r) {
 }
 
 // A fragment from the halo tile. ks = k-step inside the chunk, h = lane >> 5.
-__device__ __forceinline__ s16x8_t lds_a(const char* lds, int row, int ks, int h, bf16_t*) {
+__device__ __forceinline__ s16x8_t lds_a(const char* lds, int row, int ks, int h) {
   int slot = (ks * 2 + h) ^ swz(row);
   return *reinterpret_cast<const s16x8_t*>(lds + row * kRowBytes + slot * 16);
 }
-__device__ __forceinline__ float lds_a(const char* lds, int row, int ks, int h, float*) {
-  int c = ks * 2 + h;  // channel in chunk (0..15)
-  int slot = (c >> 2) ^ swz(row);
-  return *reinterpret_cast<const float*>(lds + row * kRowBytes + slot * 16 + (c & 3) * 4);
+// the 16-B logical slot s of a halo row
+__device__ __forceinline__ s16x8_t lds_slot(const char* lds, int row, int s) {
+  return *reinterpret_cast<const s16x8_t*>(lds + row * kRowBytes + (s ^ swz(row)) * 16);
 }
-// B fragment (weights) straight from global: packed [chunk][27][Cout][CK].
+// B fragment (weights) straight from global: packed [chunk][27][Cout][WK] bf16.
 __device__ __forceinline__ s16x8_t gl_b(const bf16_t* wrow, int ks, int h) {
   return *reinterpret_cast<const s16x8_t*>(wrow + ks * 16 + h * 8);
 }
-__device__ __forceinline__ float gl_b(const float* wrow, int ks, int h) { return wrow[ks * 2 + h]; }
 
 struct Conv3Params {
   const void* x0; const void* x1; int c0; int c1;

@@ -24,7 +24,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import BF16, F32, call, query
+from ._lib import BF16, F32, F32X3, call, query
 from .dp import module_grad_ranges
 
 BN_EPS = 1e-5
@@ -34,12 +34,15 @@ _DT = {"bf16": (torch.bfloat16, BF16), "fp32": (torch.float32, F32)}
 
 
 class ConvSpec:
-    __slots__ = ("mod", "cin", "cout", "cin_store", "fwd", "dgrad")
+    __slots__ = ("mod", "cin", "cout", "cin_store", "fwd", "dgrad", "code")
 
     def __init__(self, mod, cin, cout, cin_store):
         self.mod, self.cin, self.cout, self.cin_store = mod, cin, cout, cin_store
         self.fwd = None
         self.dgrad = None
+        # conv-kernel dtype code: BF16, or for fp32 data F32 (bf16x6 arithmetic, fp32-grade)
+        # / F32X3 (bf16x3, faster, ~10x the fp32 rounding error)
+        self.code = None
 
 
 class BNSpec:
@@ -97,6 +100,8 @@ class UNetEngine:
         for b in self.enc + self.dec:
             self.convs += [b.c0, b.c1]
             self.bns += [b.b0, b.b1]
+        for cs in self.convs:
+            cs.code = self.code
         self.convt_packs: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
         # bf16 build: the stem runs on dedicated tap-packed kernels (HBM-bound)
         self.stem_fast = self.code == BF16 and self.cp == 8
@@ -138,6 +143,20 @@ class UNetEngine:
         for bn in self.bns:
             c = bn.c
             bn.scale, bn.shift, bn.mean, bn.invstd = (torch.empty(c, device=device) for _ in range(4))
+
+    def set_fp32_conv_mode(self, mode: str, convs=None):
+        """fp32 build: the arithmetic of the 3x3x3 convs (all, or the indices ``convs`` of
+        self.convs): "x6" (bf16x6, fp32-grade, the default) or "x3" (bf16x3)."""
+        if self.code == BF16:
+            raise ValueError("the bf16 build has one conv arithmetic")
+        code = {"x6": F32, "x3": F32X3}[mode]
+        for i, cs in enumerate(self.convs):
+            if convs is None or i in convs:
+                cs.code = code
+                cs.fwd = cs.dgrad = None
+        self._dirty = True
+        self._eval = None
+        self.buf_key = None
 
     # ------------------------------------------------------------------ parameters
     def _flatten(self):
@@ -353,27 +372,26 @@ class UNetEngine:
             # the fused Adam rewrote every conv / ConvT pack: only the stem's are left
             cs = self.convs[0]
             if cs.dgrad is None:
-                call("pcms_conv3_pack", self.code, cs.mod.weight, cs.fwd, cs.cout, cs.cin, 0)
+                call("pcms_conv3_pack", cs.code, cs.mod.weight, cs.fwd, cs.cout, cs.cin, 0)
             else:
-                call("pcms_conv3_pack2", self.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
+                call("pcms_conv3_pack2", cs.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
             if self.stem_fast:
                 call("pcms_stem_pack", cs.mod.weight, self.stem_pack, self.nmod)
             self._dirty = False
             self._packs_fresh = False
             return
-        ck = query("pcms_conv3_chunk", self.code)
         for i, cs in enumerate(self.convs):
             w = cs.mod.weight
             if cs.fwd is None:
-                nch = -(-cs.cin // ck)
-                cs.fwd = torch.empty(nch * 27 * cs.cout * ck, dtype=self.tdtype, device=self.device)
+                cs.fwd = torch.empty(query("pcms_conv3_pack_elems", cs.code, cs.cout, cs.cin), dtype=self.tdtype,
+                                     device=self.device)
                 if i != 0:  # the stem's input needs no gradient -> no dgrad pack
-                    nchd = -(-cs.cout // ck)
-                    cs.dgrad = torch.empty(nchd * 27 * cs.cin * ck, dtype=self.tdtype, device=self.device)
+                    cs.dgrad = torch.empty(query("pcms_conv3_pack_elems", cs.code, cs.cin, cs.cout),
+                                           dtype=self.tdtype, device=self.device)
             if cs.dgrad is not None:
-                call("pcms_conv3_pack2", self.code, w, cs.fwd, cs.dgrad, cs.cout, cs.cin)
+                call("pcms_conv3_pack2", cs.code, w, cs.fwd, cs.dgrad, cs.cout, cs.cin)
             else:
-                call("pcms_conv3_pack", self.code, w, cs.fwd, cs.cout, cs.cin, 0)
+                call("pcms_conv3_pack", cs.code, w, cs.fwd, cs.cout, cs.cin, 0)
         if self.stem_fast:
             if self.stem_pack is None:
                 self.stem_pack = torch.empty(query("pcms_stem_pack_elems"), dtype=self.tdtype, device=self.device)
@@ -402,18 +420,17 @@ class UNetEngine:
             self._eval = {}
             big = max(cs.cout * cs.cin * 27 for cs in self.convs)
             self._eval_tmp = torch.empty(big, dtype=torch.float32, device=self.device)
-        ck = query("pcms_conv3_chunk", self.code)
         tmp = self._eval_tmp
         for i, (cs, bn) in enumerate(zip(self.convs, self.bns)):
             if i not in self._eval:
-                nch = -(-cs.cin // ck)
-                self._eval[i] = (torch.empty(nch * 27 * cs.cout * ck, dtype=self.tdtype, device=self.device),
+                self._eval[i] = (torch.empty(query("pcms_conv3_pack_elems", cs.code, cs.cout, cs.cin),
+                                             dtype=self.tdtype, device=self.device),
                                  torch.empty(cs.cout, dtype=torch.float32, device=self.device))
             pack, bias = self._eval[i]
             m = bn.mod
             call("pcms_bn_fold", cs.mod.weight, cs.mod.bias, m.weight, m.bias, m.running_mean, m.running_var,
                  BN_EPS, cs.cout, cs.cin * 27, tmp, bias)
-            call("pcms_conv3_pack", self.code, tmp, pack, cs.cout, cs.cin, 0)
+            call("pcms_conv3_pack", cs.code, tmp, pack, cs.cout, cs.cin, 0)
             if i == 0 and self.stem_fast:
                 if "stem" not in self._eval:
                     self._eval["stem"] = torch.empty(query("pcms_stem_pack_elems"), dtype=self.tdtype,
@@ -426,17 +443,17 @@ class UNetEngine:
         cs = self.convs[i]
         pack, bias = self._eval[i]
         RELU = 2  # PCMS_CONV_RELU
-        splits = self._splits(N, S, c0 + c1, cs.cout)
+        splits = self._splits(N, S, c0 + c1, cs.cout, cs.code)
         if i == 0 and self.stem_sup & 1:
             call("pcms_stem_fwd", x0, self._eval["stem"], bias, a, None, N, S[0], S[1], S[2], RELU)
         elif splits == 1:
-            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, pack, bias, a, None, cs.cout, None, None, RELU,
+            call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, pack, bias, a, None, cs.cout, None, None, RELU,
                  N, S[0], S[1], S[2], cs.cout, 1)
         else:
             acc = self.bufs["yacc"]
-            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, pack, bias, a, None, cs.cout, acc, None, 0,
+            call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, pack, bias, a, None, cs.cout, acc, None, 0,
                  N, S[0], S[1], S[2], cs.cout, splits)
-            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, c0 + c1, splits),
+            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", cs.code, c0 + c1, splits),
                  bias, a, None, cs.cout, None, cs.cout, N * S[0] * S[1] * S[2], RELU)
 
     # ------------------------------------------------------------------ buffers
@@ -504,7 +521,7 @@ class UNetEngine:
         for blk, l in [(bk, i) for i, bk in enumerate(self.enc)] + [(bk, 3 - i) for i, bk in enumerate(self.dec)]:
             for cs, c1 in ((blk.c0, C[l] if blk in self.dec else 0), (blk.c1, 0)):
                 c0 = cs.cin_store - c1
-                ws.append(query("pcms_conv3_wgrad_ws_floats", self.code, N, *S[l], c0, c1, cs.cout,
+                ws.append(query("pcms_conv3_wgrad_ws_floats", cs.code, N, *S[l], c0, c1, cs.cout,
                                 self.wgrad_target))
         b["dwt"] = torch.empty(max(ws), dtype=torch.float32, device=dev)
         # split-K slabs [splits][nvox][Cout] for every conv (fwd and dgrad) that splits
@@ -513,9 +530,9 @@ class UNetEngine:
             for cs in (blk.c0, blk.c1):
                 dirs = [(cs.cin_store, cs.cout)] + ([(cs.cout, cs.cin)] if cs is not self.convs[0] else [])
                 for cin, cout in dirs:  # forward, dgrad (the stem has none)
-                    sp = self._splits(N, S[l], cin, cout)
+                    sp = self._splits(N, S[l], cin, cout, cs.code)
                     if sp > 1:
-                        yacc = max(yacc, query("pcms_conv3_splits", self.code, cin, sp) * nv[l] * cout)
+                        yacc = max(yacc, query("pcms_conv3_splits", cs.code, cin, sp) * nv[l] * cout)
         b["yacc"] = torch.empty(yacc, dtype=torch.float32, device=dev)
         # partial rows of the head / ConvT-bias gradient reductions (summed in a fixed order)
         red = [query("pcms_head_bwd_ws_floats", D * H * W, N, self.ncls)]
@@ -535,10 +552,10 @@ class UNetEngine:
         self.buf_key = key
 
     # ------------------------------------------------------------------ primitives
-    def _splits(self, N, S, cin, cout):
+    def _splits(self, N, S, cin, cout, code):
         mb = query("pcms_conv3_mblocks", N, *S)
         wgs = mb * (cout // 64)
-        nch = -(-cin // query("pcms_conv3_chunk", self.code))
+        nch = -(-cin // query("pcms_conv3_chunk", code))
         if wgs >= 192 or nch == 1 or wgs == 0:
             return 1
         return max(1, min(nch, -(-384 // wgs)))
@@ -549,21 +566,21 @@ class UNetEngine:
         the conv alone (checkpointed decoder: the forward's BN coefficients are reused)."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
-        splits = self._splits(N, S, c0 + c1, cs.cout)
+        splits = self._splits(N, S, c0 + c1, cs.cout, cs.code)
         st = b["stats"] if training and not recompute else None
         if cs is self.convs[0] and self.stem_sup & 1:
             with self._timed("stem_fwd"):
                 call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2], 0)
             rows = query("pcms_stem_fwd_rows", N, *S)
         elif splits == 1:
-            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
+            call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
-            rows = query("pcms_conv3_fwd_rows", self.code, N, *S, c0, c1, cs.cout)
+            rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, c1, cs.cout)
         else:
             acc = b["yacc"]
-            call("pcms_conv3_fwd", self.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
+            call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  acc, None, 0, N, S[0], S[1], S[2], cs.cout, splits)
-            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, c0 + c1, splits),
+            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", cs.code, c0 + c1, splits),
                  cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox, 0)
             rows = query("pcms_split_epilogue_rows", nvox)
         if recompute:
@@ -694,7 +711,7 @@ class UNetEngine:
         elif ga2 is not None:
             self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         with self._side():
-            call("pcms_conv3_wgrad", self.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
+            call("pcms_conv3_wgrad", blk.c1.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
                  b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target, int(self._gstore))
         # dgrad conv1 -> grad of a1
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
@@ -715,7 +732,7 @@ class UNetEngine:
                 with self._timed("stem_wgrad"):
                     call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
             else:
-                call("pcms_conv3_wgrad", self.code, x0, c0, x1, c1, gZ, blk.c0.mod.weight.grad, b["dwt"], N,
+                call("pcms_conv3_wgrad", blk.c0.code, x0, c0, x1, c1, gZ, blk.c0.mod.weight.grad, b["dwt"], N,
                      *S, blk.c0.cout, blk.c0.cin, self.wgrad_target, int(self._gstore))
         if gx_out0 is not None:
             self._dgrad(blk.c0, gZ, gx_out0, gx_out1, cy0, N, S)
@@ -729,15 +746,15 @@ class UNetEngine:
     def _dgrad(self, cs: ConvSpec, gy, out0, out1, cy0, N, S):
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
-        splits = self._splits(N, S, cs.cout, cs.cin)
+        splits = self._splits(N, S, cs.cout, cs.cin, cs.code)
         if splits == 1:
-            call("pcms_conv3_fwd", self.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
+            call("pcms_conv3_fwd", cs.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  None, None, 0, N, *S, cs.cin, 1)
         else:
             acc = b["yacc"]
-            call("pcms_conv3_fwd", self.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
+            call("pcms_conv3_fwd", cs.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  acc, None, 0, N, *S, cs.cin, splits)
-            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", self.code, cs.cout, splits),
+            call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", cs.code, cs.cout, splits),
                  None, out0, out1, cy0, None, cs.cin, nvox, 0)
 
     def backward(self, dlogits: torch.Tensor):

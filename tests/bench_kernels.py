@@ -58,9 +58,8 @@ def main():
         ys = [torch.empty(nvox * cout, dtype=T, device="cuda") for _ in range(3)]
         dys = [torch.randn(nvox * cout, device="cuda").to(T) for _ in range(3)]
         w = torch.randn(cout, cin, 27, device="cuda") / math.sqrt(27 * cin)
-        ck = L.query("pcms_conv3_chunk", code)
-        wf = torch.empty(-(-cin // ck) * 27 * cout * ck, dtype=T, device="cuda")
-        wd = torch.empty(-(-cout // ck) * 27 * cin * ck, dtype=T, device="cuda")
+        wf = torch.empty(L.query("pcms_conv3_pack_elems", code, cout, cin), dtype=T, device="cuda")
+        wd = torch.empty(L.query("pcms_conv3_pack_elems", code, cin, cout), dtype=T, device="cuda")
         L.call("pcms_conv3_pack", code, w, wf, cout, cin, 0)
         L.call("pcms_conv3_pack", code, w, wd, cout, cin, 1)
         rows = L.query("pcms_conv3_mblocks", N, D, H, W)

@@ -18,8 +18,7 @@ def main():
         w = torch.randn(cout, cin, 3, 3, 3, generator=g) * math.sqrt(2.0 / (27 * cout))
         ref = F.conv3d(x.double(), w.double(), None, padding=1)
         cpu = F.conv3d(x, w, None, padding=1).double()
-        ck = L.query("pcms_conv3_chunk", 0)
-        wp = torch.empty(-(-cin // ck) * 27 * cout * ck, device="cuda")
+        wp = torch.empty(L.query("pcms_conv3_pack_elems", 0, cout, cin), device="cuda")
         L.call("pcms_conv3_pack", 0, w.cuda(), wp, cout, cin, 0)
         y = torch.empty(N, *S, cout, device="cuda")
         L.call("pcms_conv3_fwd", 0, x.permute(0, 2, 3, 4, 1).contiguous().cuda(), cin, None, 0, wp, None, y, None,

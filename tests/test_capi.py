@@ -45,6 +45,12 @@ def test_library_loads_and_exports_every_symbol():
 
 def test_host_queries_without_gpu():
     assert _lib.query("pcms_conv3_chunk", _lib.BF16) == 32
-    assert _lib.query("pcms_conv3_chunk", _lib.F32) == 16
+    assert _lib.query("pcms_conv3_chunk", _lib.F32) == 8      # bf16x6: 8 fp32 channels per chunk
+    assert _lib.query("pcms_conv3_chunk", _lib.F32X3) == 16
+    # pack elements (activation dtype): bf16 32 per (chunk, tap, row); fp32 x6: 48 bf16 per
+    # 8 channels = 24 floats; x3: 32 bf16 per 16 channels = 16 floats
+    assert _lib.query("pcms_conv3_pack_elems", _lib.BF16, 64, 64) == 2 * 27 * 64 * 32
+    assert _lib.query("pcms_conv3_pack_elems", _lib.F32, 64, 64) == 8 * 27 * 64 * 24
+    assert _lib.query("pcms_conv3_pack_elems", _lib.F32X3, 64, 5) == 1 * 27 * 64 * 16
     assert _lib.query("pcms_conv3_mblocks", 2, 128, 128, 64) == 2 * 16 * 16 * 8
     assert _lib.query("pcms_loss_rows", 1 << 20) > 0

@@ -31,7 +31,7 @@ def _batch(seed):
 def _uses_split_k(m):
     eng = m.engine()
     S, N = eng.bufs["S"], eng.buf_key[0]
-    return any(eng._splits(N, S[l], c.cin_store, c.cout) > 1 for l, blk in enumerate(eng.enc) for c in (blk.c0, blk.c1))
+    return any(eng._splits(N, S[l], c.cin_store, c.cout, c.code) > 1 for l, blk in enumerate(eng.enc) for c in (blk.c0, blk.c1))
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])

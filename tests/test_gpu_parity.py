@@ -236,7 +236,7 @@ def test_decoder_checkpointing_matches_plain_step(precision):
             losses.append(float(loss))
         eng = m.engine()
         S, N = eng.bufs["S"], eng.buf_key[0]
-        assert any(eng._splits(N, S[l], 64 << l, 64 << l) > 1 for l in range(5)), "no split-K level at this shape"
+        assert any(eng._splits(N, S[l], 64 << l, 64 << l, eng.convs[2 * l].code) > 1 for l in range(5)), "no split-K level at this shape"
         nbuf = sum(1 for k in eng.bufs if k.startswith("d") or k.startswith("ck_"))
         runs.append((losses, grads, {k: v.detach().clone() for k, v in m.state_dict().items()}, nbuf))
     (l0, g0, s0, n0), (l1, g1, s1, n1) = runs

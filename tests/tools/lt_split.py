@@ -12,10 +12,10 @@ from pcms_amd._lib import query  # noqa: E402
 THR, TGT = int(sys.argv[1]), int(sys.argv[2])
 
 
-def _splits(self, N, S, cin, cout):
+def _splits(self, N, S, cin, cout, code):
     mb = query("pcms_conv3_mblocks", N, *S)
     wgs = mb * (cout // 64)
-    nch = -(-cin // query("pcms_conv3_chunk", self.code))
+    nch = -(-cin // query("pcms_conv3_chunk", code))
     if wgs >= THR or nch == 1 or wgs == 0:
         return 1
     return max(1, min(nch, -(-TGT // wgs)))
