@@ -77,6 +77,9 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
  * dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (one partial row per voxel split,
  * summed in a fixed order: deterministic)                                               */
 int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout, int target_wgs);
+/* bf16 grids of at most v boxes split the taps over two workgroups (no partial rows) before
+ * splitting the voxels; 0 never, v < 0 queries; returns the previous value              */
+int pcms_conv3_wgrad_tg_maxbox(int v);
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, int flags, hipStream_t s);
@@ -163,6 +166,11 @@ int pcms_maxpool_bwd_bn(int dtype, const void* y, const float* scale, const floa
                         int C, hipStream_t s);
 
 /* ---- ConvTranspose3d(k=2, s=2) + F.pad: models/unet3d.py:120,139-151 --------------- */
+/* the persistent bf16 forward used at Cin 128 / Cout 64 (level-0 Up3D): on (1) / off (0),
+ * v < 0 queries; returns the previous setting (A/B and tests)                          */
+int pcms_convt_fwd_stream(int v);
+/* elements (activation dtype) of one pack: bf16 8 Cin Cout; fp32 (bf16x6 fragments) 3x that */
+int pcms_convt_pack_elems(int dtype, int Cin, int Cout);
 int pcms_convt_pack(int dtype, const float* w, void* out, int Cin, int Cout, int dgrad, hipStream_t s);
 int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bias, void* out,
                    int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);

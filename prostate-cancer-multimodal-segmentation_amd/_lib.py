@@ -29,6 +29,7 @@ SIGNATURES = {
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiiis",
+    "pcms_conv3_wgrad_tg_maxbox": "i",
     "pcms_stem_pack_elems": "",
     "pcms_stem_pack": "ppis",
     "pcms_stem_supported": "iiii",
@@ -53,6 +54,8 @@ SIGNATURES = {
     "pcms_maxpool_bwd_bn": "ippppppppiiiiis",
     "pcms_bn_relu_bwd_finish": "i" + "p" * 8 + "ippppilps",
     "pcms_convt_pack": "ippiiis",
+    "pcms_convt_pack_elems": "iii",
+    "pcms_convt_fwd_stream": "i",
     "pcms_convt_fwd": "ippppiiiiiiiiis",
     "pcms_convt_dgrad": "ipppiiiiiiiiis",
     "pcms_convt_dgrad_ws_floats": "iiiiii",

@@ -153,7 +153,7 @@ def up_forward(up, x1: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
         raise ValueError("Up3D: the skip tensor must be at least twice the upsampled input's size")
     x1p, _ = r.pack(x1)
     x2p, _ = r.pack(x2)
-    fpack = r.buf(8 * C1 * cout_t)
+    fpack = r.buf(query("pcms_convt_pack_elems", r.code, C1, cout_t))
     call("pcms_convt_pack", r.code, ct.weight.detach(), fpack, C1, cout_t, 0)
     u = r.buf(N * Do * Ho * Wo * cout_t)
     call("pcms_convt_fwd", r.code, x1p, fpack, ct.bias, u, N, Di, Hi, Wi, C1, cout_t, Do, Ho, Wo)

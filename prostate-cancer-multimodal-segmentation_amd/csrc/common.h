@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 typedef uint16_t bf16_t;  // raw bf16 bits (same bytes as torch.bfloat16)
 
@@ -39,6 +40,24 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   const f32x2_t f = {a, b};
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
+}
+
+// arithmetic tags of the fp32-data conv kernels (split-bf16: conv_common.h)
+struct x3_t {};
+struct x6_t {};
+
+// three bf16 parts of 8 floats (h, m, l: 8 packed bf16 each)
+__device__ __forceinline__ void split3x8(const float* f, u32x4_t& h, u32x4_t& m, u32x4_t& l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = f[2 * i], b = f[2 * i + 1];
+    const uint32_t hh = pack_bf16x2(a, b);
+    const float ra = a - __uint_as_float(hh << 16), rb = b - __uint_as_float(hh & 0xffff0000u);
+    const uint32_t mm = pack_bf16x2(ra, rb);
+    h[i] = hh;
+    m[i] = mm;
+    l[i] = pack_bf16x2(ra - __uint_as_float(mm << 16), rb - __uint_as_float(mm & 0xffff0000u));
+  }
 }
 
 template <typename T> struct Elem;

@@ -453,10 +453,13 @@ struct WgradParams {
   float* dw;             // direct (one split, bf16): dw [Cout][cw][27] += through an LDS transpose
   int cw, direct;
   int store;             // PCMS_GRAD_STORE: dw = (the first writer of a fresh gradient), not +=
+  int ntg;               // tap groups (TG kernels: 2, taps [0, 16) / [16, 27) per workgroup)
 };
 
 
-template <typename T, int LBD, int LBH, int LBW>
+// TG: the taps are split over two workgroups per (tile, split) -- for grids of few boxes,
+// where splitting the voxels instead would add partial rows and a reduction pass
+template <typename T, int LBD, int LBH, int LBW, bool TG = false>
 __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p) {
   const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   typedef WTraits<T> Tr;
@@ -474,13 +477,21 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // BUFBYTES apart
   constexpr bool kX3 = std::is_same<T, x3_t>::value, kX6 = std::is_same<T, x6_t>::value;
   typedef typename std::conditional<kX3 || kX6, float, bf16_t>::type M;
-  const int ntap2 = wave < 3 ? 4 : 3;
   // 1-D grid, logical id XCD-aware (dispatch is round-robin over 8 XCDs: consecutive logical
   // ids land on one XCD at about the same time), tile (co block, ci block) fastest: the
   // workgroups of one split that share its dy boxes (and its halos) share an L2
   const int G = gridDim.x, ntile = p.nco * p.nci;
   const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-  const int tile = lg % ntile, split = lg / ntile;
+  const int tile = lg % ntile, split = lg / ntile / (TG ? 2 : 1);
+  // the wave's taps: main taps tb + 8 j (j < NJ, accumulators j and 4 + j) and, where it
+  // exists, one more at tb + 8 NJ (accumulators 3 and 7).  TG group 0: taps w, w + 8;
+  // group 1: 16 + w, 24 + w (waves 0-2)
+  const int tgrp = TG ? (lg / ntile) & 1 : 0;
+  constexpr int NJ = TG ? 1 : 3;
+  const int tb = 16 * tgrp + wave;
+  const bool four = TG ? (tgrp == 0 || wave < 3) : wave < 3;
+  auto owned = [&](int j) __attribute__((always_inline)) { return j < NJ || (j == 3 && four); };
+  auto tapof = [&](int j) __attribute__((always_inline)) { return tb + 8 * (j < NJ ? j : NJ); };
   const int co_base = (tile % p.nco) * 64;
   const int ci_base = (tile / p.nco) * 32;
   const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
@@ -664,8 +675,8 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         const char* xb3 = xb + (hsel ? BUFBYTES : 2 * BUFBYTES);  // B3: l | m
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (j < ntap2) {
-            const int tap = wave + 8 * j;
+          if (owned(j)) {
+            const int tap = tapof(j);
             const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
             const int off = (kd * HH + kh) * HW + kw;
             const int o0 = (hr0 + off) * Tr::XROW + ci * 2, o1 = (hr1 + off) * Tr::XROW + ci * 2;
@@ -693,8 +704,8 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       const int ci = g * 16 + pp * 4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (j < ntap2) {
-          const int tap = wave + 8 * j;
+        if (owned(j)) {
+          const int tap = tapof(j);
           const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
           const int off = (kd * HH + kh) * HW + kw;
           const int o0 = (hr0 + off) * Tr::XROW + ci * 2, o1 = (hr1 + off) * Tr::XROW + ci * 2;
@@ -731,11 +742,10 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     const int vrow = (vl >> LW) * HWc + (vl & ((1 << LW) - 1));  // its halo row offset
     const char* ab0 = buf + dy_off_bf16(vl, g * 16 + pp * 4);
     const char* ab1 = buf + dy_off_bf16(vl, 32 + g * 16 + pp * 4);
-    const bool four = wave < 3;
     const char* bb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int tap = wave + 8 * j;
+      const int tap = tapof(j);
       const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
       bb[j] = buf + DYBYTES + (vrow + (kd * HHc + kh) * HWc + kw) * Tr::XROW + (g * 16 + pp * 4) * 2;
     }
@@ -751,7 +761,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       fa[set][0] = cat(tr_read(ab0, s * 2048), tr_read(ab0, s * 2048 + 512));
       fa[set][1] = cat(tr_read(ab1, s * 2048), tr_read(ab1, s * 2048 + 512));
 #pragma unroll
-      for (int j = 0; j < 3; ++j) fb[set][j] = cat(tr_read(bb[j], hro(s)), tr_read(bb[j], hro(s) + 4 * Tr::XROW));
+      for (int j = 0; j < NJ; ++j) fb[set][j] = cat(tr_read(bb[j], hro(s)), tr_read(bb[j], hro(s) + 4 * Tr::XROW));
     };
     auto load3 = [&](int s, int set) __attribute__((always_inline)) {
       f3[set] = cat(tr_read(bb[3], hro(s)), tr_read(bb[3], hro(s) + 4 * Tr::XROW));
@@ -762,7 +772,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       constexpr int s = decltype(sc)::value, cs = s & 1, ns = cs ^ 1;
       if constexpr (s + 1 < NK) load(s + 1, ns);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         acc[j] = mfma(fa[cs][0], fb[cs][j], acc[j]);
         acc[4 + j] = mfma(fa[cs][1], fb[cs][j], acc[4 + j]);
       }
@@ -872,8 +882,8 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (j >= ntap2) continue;
-          const int tap = wave + 8 * j;
+          if (!owned(j)) continue;
+          const int tap = tapof(j);
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int col = (e & 3) + 8 * (e >> 2) + 4 * hsel;
@@ -881,7 +891,17 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           }
         }
         __syncthreads();
-        if (nci == 32) {
+        if (TG) {
+          // this group's taps only (the other group's workgroup writes the rest of each run)
+          for (int i = tid; i < 32 * 32 * 27; i += kWThreads) {
+            const int col = i / 864, r = i % 864, tap = r % 27;
+            const int co = co_base + ct * 32 + col;
+            if (co < p.Cout && r < nci * 27 && (tap >= 16) == (tgrp == 1)) {
+              float* d = p.dw + ((long)co * p.cw + ci_base) * 27 + r;
+              *d = p.store ? tile[i] : *d + tile[i];
+            }
+          }
+        } else if (nci == 32) {
           // whole 32 x 864-float runs: 16-B read-modify-writes, all of a thread's loads in
           // flight before the first add (a dependent load -> add -> store chain per element
           // made the deep levels latency-bound)
@@ -916,8 +936,8 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (j >= ntap2) continue;
-      const int tap = wave + 8 * j;
+      if (!owned(j)) continue;
+      const int tap = tapof(j);
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -1662,7 +1682,10 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
 
 // Weight-gradient launch plan: box geometry, boxes per split, split count (shared by the
 // launch and its workspace query)
-struct WgradPlan { Box b; int nbd, nbh, nbw, nbox, bps, splits; };
+// bf16 grids of at most this many boxes split their taps over two workgroups (TG) before
+// splitting their voxels (partial rows + a reduction pass); 0 disables
+static int g_wgrad_tg_maxbox = 64;
+struct WgradPlan { Box b; int nbd, nbh, nbw, nbox, bps, splits, ntg; };
 static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int Cout, int target_wgs) {
   WgradPlan q;
   const int bv = dtype == PCMS_BF16 ? WTraits<bf16_t>::BV : dtype == PCMS_F32X3 ? WTraits<x3_t>::BV : WTraits<x6_t>::BV;
@@ -1672,13 +1695,22 @@ static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int 
   q.nbox = N * q.nbd * q.nbh * q.nbw;
   const int tiles = (Cout / 64) * cdiv(Cin, 32);
   if (target_wgs <= 0) target_wgs = 512;
-  const int splits = std::max(1, std::min(q.nbox, cdiv(target_wgs, tiles)));
+  q.ntg = dtype == PCMS_BF16 && q.nbox <= g_wgrad_tg_maxbox && tiles < target_wgs ? 2 : 1;
+  const int splits = std::max(1, std::min(q.nbox, cdiv(target_wgs, tiles * q.ntg)));
   q.bps = cdiv(q.nbox, splits);
   q.splits = cdiv(q.nbox, q.bps);
   return q;
 }
 
 // fp32 workspace floats pcms_conv3_wgrad needs: one [27][Cout][c0+c1] partial row per split
+// grids of at most v boxes split the taps of the bf16 weight gradient over two workgroups
+// before splitting the voxels (0: never); v < 0 queries.  Returns the previous value.
+int pcms_conv3_wgrad_tg_maxbox(int v) {
+  const int old = g_wgrad_tg_maxbox;
+  if (v >= 0) g_wgrad_tg_maxbox = v;
+  return old;
+}
+
 int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout, int target_wgs) {
   const int Cin = c0 + c1;
   return wgrad_plan(dtype, N, D, H, W, Cin, Cout, target_wgs).splits * 27 * Cout * Cin;
@@ -1716,12 +1748,16 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   p.cw = cin_w;
   p.direct = splits == 1;
   p.store = flags & PCMS_GRAD_STORE;
-  dim3 grid(splits * p.nco * p.nci);
+  p.ntg = q.ntg;
+  dim3 grid(splits * p.nco * p.nci * q.ntg);
   size_t lds;
   if (dtype == PCMS_BF16) {
     lds = (size_t)WTraits<bf16_t>::NBUF * (WTraits<bf16_t>::BV * WTraits<bf16_t>::DYROW + kWHaloMax * WTraits<bf16_t>::XROW);
     auto kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1>;
-    if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
+    if (q.ntg == 2) {
+      kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1, true>;
+      if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3, true>;
+    } else if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
     else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
     else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

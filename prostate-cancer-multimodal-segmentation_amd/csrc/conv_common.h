@@ -22,8 +22,7 @@ constexpr uint32_t kOOB = 0x80000000u;  // buffer voffset past num_records: read
 //  x3_t (dtype PCMS_F32X3): v = h + l (16 bits), hh + lh + hl in three MFMAs over 16
 //       channels: twice the rate, ~10x the fp32 rounding error (measured: misses the
 //       north-star 1e-3 logit bar by ~30 %; kept as an explicit faster mode).
-struct x3_t {};
-struct x6_t {};
+// (the tags x3_t / x6_t live in common.h)
 
 template <typename T> struct Traits;
 template <> struct Traits<bf16_t> {
@@ -50,19 +49,6 @@ template <> struct Traits<x6_t> {
   typedef s16x8_t Frag;
   typedef float Mem;
 };
-// three bf16 parts of 8 floats (h, m, l: 8 packed bf16 each)
-__device__ __forceinline__ void split3x8(const float* f, u32x4_t& h, u32x4_t& m, u32x4_t& l) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float a = f[2 * i], b = f[2 * i + 1];
-    const uint32_t hh = pack_bf16x2(a, b);
-    const float ra = a - __uint_as_float(hh << 16), rb = b - __uint_as_float(hh & 0xffff0000u);
-    const uint32_t mm = pack_bf16x2(ra, rb);
-    h[i] = hh;
-    m[i] = mm;
-    l[i] = pack_bf16x2(ra - __uint_as_float(mm << 16), rb - __uint_as_float(mm & 0xffff0000u));
-  }
-}
 
 __device__ __forceinline__ f32x16_t mfma(s16x8_t a, s16x8_t b, f32x16_t c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),

@@ -129,6 +129,204 @@ __global__ void __launch_bounds__(256) convt_dgrad_kernel(const T* dout, const T
   }
 }
 
+// bf16 forward at Cout = 64, Cin = 128 (Up3D up4, the level-0 upsample: 67 MB in, 268 MB
+// out -- a store stream).  PERSISTENT: one 8-wave workgroup per CU walks 64-voxel tiles
+// slot, slot + nslot, ...; wave t computes tap t (its 64 x 128 weights held in registers
+// for the whole launch: no weight traffic), so a tile's A rows (64 x 256 B, LDS, 16-B slots
+// XOR row & 15) are read from HBM exactly once and feed all 8 taps.  The next tile's rows are
+// register-prefetched while this one computes and stores; LDS is double-buffered with one raw
+// barrier per tile (no vmcnt(0): the output stores stay in flight across tiles).  Output:
+// each lane a channel pair (packed bf16x2), 32 lanes = one whole 128-B child row,
+// non-temporal.
+constexpr int kSTM = 64;                           // voxels per tile
+constexpr int kSTRow = 256;                        // 128 ci x 2 B
+__global__ void __launch_bounds__(512, 1) convt_fwd_stream_kernel(const bf16_t* x, const bf16_t* wpk,
+                                                                  const float* bias, bf16_t* out, UpGeom g,
+                                                                  int ntile) {
+  constexpr int Cin = 128, Cout = 64;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kSTM * kSTRow];
+  const int tid = threadIdx.x, lane = tid & 63, t = tid >> 6, r = lane & 31, h = lane >> 5;
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  // this wave's weights: B fragment (ks, nt) = row (t, co = 2 r + nt), K = 16 ks + 8 h
+  s16x8_t b[8][2];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      b[ks][nt] = *reinterpret_cast<const s16x8_t*>(wpk + ((long)t * Cout + 2 * r + nt) * Cin + ks * 16 + 8 * h);
+  // opaque: the compiler would otherwise re-load the weights inside the tile loop (cheap
+  // rematerialisation) and wait for them with vmcnt(0) -- draining the output stores
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) asm volatile("" : "+v"(b[ks][nt]));
+  const float b0 = bias[2 * r], b1 = bias[2 * r + 1];
+  const long dt = tap_delta(g, t) * Cout + 2 * r;
+  // staging: piece pc = tid + 512 j (j < 2) = row pc >> 4, slot pc & 15
+  u32x4_t stg[2];
+  auto load = [&](int tile) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pc = tid + 512 * j, row = pc >> 4, sl = pc & 15;
+      const long m = std::min<long>((long)tile * kSTM + row, M - 1);  // clamped tail rows: never stored
+      stg[j] = *reinterpret_cast<const u32x4_t*>(x + m * Cin + sl * 8);
+    }
+  };
+  auto put = [&](char* buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pc = tid + 512 * j, row = pc >> 4, sl = pc & 15;
+      *reinterpret_cast<u32x4_t*>(buf + row * kSTRow + ((sl ^ (row & 15)) << 4)) = stg[j];
+    }
+  };
+  int tile = blockIdx.x;
+  if (tile >= ntile) return;
+  load(tile);
+  put(lds);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int it = 0; tile < ntile; ++it, tile += gridDim.x) {
+    const char* buf = lds + (it & 1) * kSTM * kSTRow;
+    const int next = tile + gridDim.x;
+    if (next < ntile) load(next);
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mt][nt][e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int row = mt * 32 + r;
+        const s16x8_t a = *reinterpret_cast<const s16x8_t*>(buf + row * kSTRow + (((ks * 2 + h) ^ (row & 15)) << 4));
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a, b[ks][nt], acc[mt][nt]);
+      }
+    // a lane's rows come in runs of 4 consecutive voxels starting at a multiple of 4 (Win % 4
+    // == 0: a run never leaves its w-row), whose children are 2 voxels apart: one child_base
+    // per run.  All 32 values are packed before the first store: rewriting a register that an
+    // in-flight store still reads costs a vmcnt(0) per store (measured: 158 us with per-store
+    // packing; one wait per tile left: 70.5 us; alternating two register sets by tile: 73 us).
+    uint32_t pk[2][16];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) pk[mt][e] = pack_bf16x2(acc[mt][0][e] + b0, acc[mt][1][e] + b1);
+    const long mbase = (long)tile * kSTM + 4 * h;
+    if ((long)(tile + 1) * kSTM <= M) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int grp = 0; grp < 4; ++grp) {
+          uint32_t* base = reinterpret_cast<uint32_t*>(out + child_base(g, mbase + mt * 32 + 8 * grp) * Cout + dt);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(pk[mt][grp * 4 + i], base + i * Cout);
+        }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const long m = mbase + mt * 32 + (e & 3) + 8 * (e >> 2);
+          if (m < M) __builtin_nontemporal_store(pk[mt][e], reinterpret_cast<uint32_t*>(out + child_base(g, m) * Cout + dt));
+        }
+    }
+    if (next < ntile) put(lds + ((it + 1) & 1) * kSTM * kSTRow);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+// fp32 build (bf16x6, see conv_common.h): K steps of 8 channels; the A row (8 fp32) split
+// into h, m, l in registers, the weights pre-split in their pack (per 8 K-elements the three
+// B fragments [h|h] [m|h] [l|m], 48 bf16); three MFMAs per step and N-tile.
+__device__ __forceinline__ void afrag_x6(const float* p, int h, s16x8_t& a1, s16x8_t& a2) {
+  const f32x4_t u = *reinterpret_cast<const f32x4_t*>(p), v = *reinterpret_cast<const f32x4_t*>(p + 4);
+  const float f[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+  u32x4_t hh, mm, ll;
+  split3x8(f, hh, mm, ll);
+  a1 = __builtin_bit_cast(s16x8_t, h ? mm : hh);  // [h | m]
+  a2 = __builtin_bit_cast(s16x8_t, h ? ll : hh);  // [h | l]
+}
+__device__ __forceinline__ f32x16_t mfma_x6(s16x8_t a1, s16x8_t a2, const bf16_t* b, int h, f32x16_t c) {
+  c = mfma(a1, *reinterpret_cast<const s16x8_t*>(b + 8 * h), c);
+  c = mfma(a2, *reinterpret_cast<const s16x8_t*>(b + 16 + 8 * h), c);
+  return mfma(a1, *reinterpret_cast<const s16x8_t*>(b + 32 + 8 * h), c);
+}
+
+// forward, fp32 build: out[child(m, t)][co] = b[co] + sum_ci x[m][ci] W[ci][co][t]
+// (pack rows q = t Cout + co, Cin / 8 groups of 48 bf16)
+__global__ void __launch_bounds__(256) convt_fwd_x6_kernel(const float* x, const bf16_t* wt, const float* bias,
+                                                           float* out, UpGeom g, int Cin, int Cout) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  const long m0 = (long)blockIdx.x * 128 + wave * 32;
+  const int q0 = blockIdx.y * 64;
+  if (m0 >= M) return;
+  const long ma = std::min<long>(m0 + r, M - 1);
+  const float* arow = x + ma * Cin;
+  const bf16_t* b0 = wt + (long)(q0 + 2 * r) * Cin * 6;
+  const bf16_t* b1 = b0 + (long)Cin * 6;
+  f32x16_t acc0, acc1;
+  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  for (int k = 0; k < Cin; k += 8) {
+    s16x8_t a1, a2;
+    afrag_x6(arow + k, h, a1, a2);
+    acc0 = mfma_x6(a1, a2, b0 + k * 6, h, acc0);
+    acc1 = mfma_x6(a1, a2, b1 + k * 6, h, acc1);
+  }
+  const int q = q0 + 2 * r;
+  const int t = q / Cout, co = q % Cout;
+  const float bias0 = bias[co], bias1 = bias[co + 1];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (m >= M) continue;
+    float* dst = out + child_vox(g, m, t) * Cout + co;
+    dst[0] = acc0[e] + bias0;
+    dst[1] = acc1[e] + bias1;
+  }
+}
+
+// dgrad, fp32 build: dx[m][ci] = sum_{t, co} dout[child(m, t)][co] Wd[ci][t][co]
+// (pack rows ci, 8 Cout / 8 groups of 48 bf16)
+// ws != nullptr: blockIdx.z takes K groups [z G / Z, (z + 1) G / Z) of the G = Cout / 8 per tap
+// x 8 taps and stores its fp32 partial sums to ws[z][m][ci] (summed in z order afterwards)
+__global__ void __launch_bounds__(256) convt_dgrad_x6_kernel(const float* dout, const bf16_t* wd, float* dx,
+                                                             UpGeom g, int Cin, int Cout, float* ws) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const long M = (long)g.N * g.Din * g.Hin * g.Win;
+  const long m0 = (long)blockIdx.x * 128 + wave * 32;
+  const int q0 = blockIdx.y * 64;
+  if (m0 >= M) return;
+  const long ma = std::min<long>(m0 + r, M - 1);
+  const long K = 8L * Cout;
+  const bf16_t* b0 = wd + (long)(q0 + r) * K * 6;
+  const bf16_t* b1 = wd + (long)(q0 + 32 + r) * K * 6;
+  f32x16_t acc0, acc1;
+  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  const int G = Cout / 8 * 8, Z = gridDim.z;
+  const int g0 = (int)((long)blockIdx.z * G / Z), g1 = (int)((long)(blockIdx.z + 1) * G / Z);
+  for (int gi = g0; gi < g1; ++gi) {
+    const int t = gi / (Cout / 8), k = (gi % (Cout / 8)) * 8;
+    s16x8_t a1, a2;
+    afrag_x6(dout + child_vox(g, ma, t) * Cout + k, h, a1, a2);
+    acc0 = mfma_x6(a1, a2, b0 + ((long)t * Cout + k) * 6, h, acc0);
+    acc1 = mfma_x6(a1, a2, b1 + ((long)t * Cout + k) * 6, h, acc1);
+  }
+  float* dst = ws ? ws + (long)blockIdx.z * M * Cin : dx;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (m >= M) continue;
+    dst[m * Cin + q0 + r] = acc0[e];
+    dst[m * Cin + q0 + 32 + r] = acc1[e];
+  }
+}
+
 // bf16 forward and dgrad, LDS-staged (the hot path).  The direct kernels above read each A
 // row 32 B per lane pair and instruction (the 32x32 A layout): ~25 % of each 128-B line per
 // request, ~1/5 of the HBM roofline.  Here a 512-thread workgroup owns 256 input voxels x 128
@@ -297,8 +495,9 @@ __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, 
   }
 }
 
-// dx[m][ci] = bf16(sum over z = 0..S-1 of ws[z][m][ci]), z in order; 4 elements per thread
-__global__ void __launch_bounds__(256) convt_dgrad_reduce(const float* ws, int S, long E, bf16_t* dx) {
+// dx[m][ci] = T(sum over z = 0..S-1 of ws[z][m][ci]), z in order; 4 elements per thread
+template <typename T>
+__global__ void __launch_bounds__(256) convt_dgrad_reduce(const float* ws, int S, long E, T* dx) {
   const long i = (blockIdx.x * 256L + threadIdx.x) * 4;
   if (i >= E) return;
   f32x4_t v[16];
@@ -312,9 +511,13 @@ __global__ void __launch_bounds__(256) convt_dgrad_reduce(const float* ws, int S
     for (int j = 0; j < 16; ++j)
       if (j < nz) a += v[j];
   }
-  uint32_t* d = reinterpret_cast<uint32_t*>(dx + i);
-  d[0] = pack_bf16x2(a[0], a[1]);
-  d[1] = pack_bf16x2(a[2], a[3]);
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<f32x4_t*>(dx + i) = a;
+  } else {
+    uint32_t* d = reinterpret_cast<uint32_t*>(dx + i);
+    d[0] = pack_bf16x2(a[0], a[1]);
+    d[1] = pack_bf16x2(a[2], a[3]);
+  }
 }
 
 // ---- weight gradient: C[p = ci][q = (t, co)] over K = input voxels ----
@@ -546,6 +749,8 @@ __global__ void __launch_bounds__(256) convt_wgrad_reduce(const float* ws, int R
 }
 
 // master W[Cin][Cout][8] fp32 ->  fwd pack [8][Cout][Cin]  /  dgrad pack [Cin][8][Cout]
+// (x6: element i = (row, k) of that order becomes the three B fragments of its 8-group:
+// [row][k / 8][48] bf16, see afrag_x6)
 template <typename T>
 __global__ void convt_pack_kernel(const float* w, T* out, int Cin, int Cout, int dgrad) {
   const long total = (long)Cin * Cout * 8;
@@ -553,7 +758,17 @@ __global__ void convt_pack_kernel(const float* w, T* out, int Cin, int Cout, int
     int t, co, ci;
     if (!dgrad) { ci = i % Cin; long r = i / Cin; co = r % Cout; t = r / Cout; }
     else { co = i % Cout; long r = i / Cout; t = r % 8; ci = r / 8; }
-    out[i] = Elem<T>::cvt(w[((long)ci * Cout + co) * 8 + t]);
+    const float v = w[((long)ci * Cout + co) * 8 + t];
+    if constexpr (std::is_same<T, x6_t>::value) {
+      bf16_t* o = reinterpret_cast<bf16_t*>(out) + (i >> 3) * 48;
+      const int j = (int)(i & 7);
+      const bf16_t hh = f2bf(v);
+      const float rr = v - bf2f(hh);
+      const bf16_t mm = f2bf(rr), ll = f2bf(rr - bf2f(mm));
+      o[j] = hh; o[8 + j] = hh; o[16 + j] = mm; o[24 + j] = hh; o[32 + j] = ll; o[40 + j] = mm;
+    } else {
+      out[i] = Elem<T>::cvt(v);
+    }
   }
 }
 
@@ -618,6 +833,18 @@ __global__ void __launch_bounds__(256) adam_pack_convt_kernel(float* P, float* G
   }
 }
 
+static int g_convt_stream = 1;  // the persistent forward at Cin 128 / Cout 64 (A/B switch)
+
+inline int device_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
+
 UpGeom make_geom(int N, int Din, int Hin, int Win, int Do, int Ho, int Wo) {
   UpGeom g;
   g.N = N; g.Din = Din; g.Hin = Hin; g.Win = Win; g.Do = Do; g.Ho = Ho; g.Wo = Wo;
@@ -646,8 +873,21 @@ int pcms_convt_pack(int dtype, const float* w, void* out, int Cin, int Cout, int
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL(convt_pack_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, w, (bf16_t*)out, Cin, Cout, dgrad);
   else
-    hipLaunchKernelGGL(convt_pack_kernel<float>, dim3(grid), dim3(256), 0, s, w, (float*)out, Cin, Cout, dgrad);
+    hipLaunchKernelGGL(convt_pack_kernel<x6_t>, dim3(grid), dim3(256), 0, s, w, (x6_t*)out, Cin, Cout, dgrad);
   PCMS_CHECK_LAUNCH();
+}
+
+// the persistent bf16 forward for Cin 128 / Cout 64 on (v = 1) / off (0); v < 0 queries
+int pcms_convt_fwd_stream(int v) {
+  const int old = g_convt_stream;
+  if (v >= 0) g_convt_stream = v;
+  return old;
+}
+
+// elements (activation dtype) of one ConvTranspose3d pack: bf16 8 Cin Cout; fp32 build
+// (bf16x6) 48 bf16 per 8 weights = 3x the fp32 count
+int pcms_convt_pack_elems(int dtype, int Cin, int Cout) {
+  return dtype == PCMS_BF16 ? 8 * Cin * Cout : 3 * 8 * Cin * Cout;
 }
 
 // out: skip-sized (N, Do, Ho, Wo, Cout). If the grid is larger than 2x the input the pad
@@ -663,6 +903,12 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
     if (e != hipSuccess) return (int)e;
   }
   const long M = (long)N * Din * Hin * Win;
+  if (dtype == PCMS_BF16 && Cin == 128 && Cout == 64 && Win % 4 == 0 && g_convt_stream) {
+    const int ntile = cdiv(M, kSTM);
+    hipLaunchKernelGGL(convt_fwd_stream_kernel, dim3(std::min(ntile, device_cus())), dim3(512), 0, s,
+                       (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, ntile);
+    PCMS_CHECK_LAUNCH();
+  }
   if (dtype == PCMS_BF16 && Cin % 64 == 0 && (8 * Cout) % kCDN == 0) {
     const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;
     auto kern = nt ? convt_lds_kernel<true, true> : convt_lds_kernel<true, false>;
@@ -676,7 +922,7 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL(convt_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
   else
-    hipLaunchKernelGGL(convt_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (const float*)wpack, bias, (float*)out, g, Cin, Cout);
+    hipLaunchKernelGGL(convt_fwd_x6_kernel, grid, dim3(256), 0, s, (const float*)x, (const bf16_t*)wpack, bias, (float*)out, g, Cin, Cout);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -717,7 +963,7 @@ int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* 
       hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), Cin / kCDN, S), dim3(512), kCDStage, s,
                          (const bf16_t*)dout, (const bf16_t*)wpack_d, nullptr, (bf16_t*)dx, g, Cin, Cout, ws);
       const long E = M * Cin;
-      hipLaunchKernelGGL(convt_dgrad_reduce, dim3((unsigned)cdiv(E / 4, 256)), dim3(256), 0, s, (const float*)ws, S,
+      hipLaunchKernelGGL(convt_dgrad_reduce<bf16_t>, dim3((unsigned)cdiv(E / 4, 256)), dim3(256), 0, s, (const float*)ws, S,
                          E, (bf16_t*)dx);
       PCMS_CHECK_LAUNCH();
     }
@@ -728,10 +974,21 @@ int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* 
     PCMS_CHECK_LAUNCH();
   }
   dim3 grid(cdiv(M, 128), Cin / 64);
-  if (dtype == PCMS_BF16)
+  if (dtype == PCMS_BF16) {
     hipLaunchKernelGGL(convt_dgrad_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, (const bf16_t*)wpack_d, (bf16_t*)dx, g, Cin, Cout);
-  else
-    hipLaunchKernelGGL(convt_dgrad_kernel<float>, grid, dim3(256), 0, s, (const float*)dout, (const float*)wpack_d, (float*)dx, g, Cin, Cout);
+    PCMS_CHECK_LAUNCH();
+  }
+  // fp32 build: K split into the workspace's slabs where the grid is small (level 4: 16
+  // workgroups -> 256)
+  const int S = ws ? convt_dgrad_splits(M, Cin, Cout) : 1;
+  grid.z = S;
+  hipLaunchKernelGGL(convt_dgrad_x6_kernel, grid, dim3(256), 0, s, (const float*)dout, (const bf16_t*)wpack_d,
+                     (float*)dx, g, Cin, Cout, S > 1 ? ws : nullptr);
+  if (S > 1) {
+    const long E = M * Cin;
+    hipLaunchKernelGGL(convt_dgrad_reduce<float>, dim3((unsigned)cdiv(E / 4, 256)), dim3(256), 0, s, (const float*)ws,
+                       S, E, (float*)dx);
+  }
   PCMS_CHECK_LAUNCH();
 }
 

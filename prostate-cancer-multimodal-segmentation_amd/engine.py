@@ -399,8 +399,9 @@ class UNetEngine:
         for i, up in enumerate(self.ups):
             cin, cout = up.in_channels, up.out_channels
             if i not in self.convt_packs:
-                self.convt_packs[i] = (torch.empty(8 * cin * cout, dtype=self.tdtype, device=self.device),
-                                       torch.empty(8 * cin * cout, dtype=self.tdtype, device=self.device))
+                n = query("pcms_convt_pack_elems", self.code, cin, cout)
+                self.convt_packs[i] = (torch.empty(n, dtype=self.tdtype, device=self.device),
+                                       torch.empty(n, dtype=self.tdtype, device=self.device))
             f, d = self.convt_packs[i]
             call("pcms_convt_pack", self.code, up.weight, f, cin, cout, 0)
             call("pcms_convt_pack", self.code, up.weight, d, cin, cout, 1)

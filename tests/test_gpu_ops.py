@@ -252,12 +252,23 @@ def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S, wgs):
     (2, 128, 0, 128, (4, 4, 4)),
     (2, 256, 0, 64, (1, 2, 1)),
     (1, 64, 64, 128, (4, 8, 8)),        # one box: the unsplit direct flush (16-B RMW of dw)
+    (2, 128, 0, 128, (16, 16, 8)),      # level-3 geometry (compile-time 4x8x8 box), 16 boxes
 ])
 @pytest.mark.parametrize("store", [0, 1])
-def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S, store):
+@pytest.mark.parametrize("tg", [64, 0])
+def test_conv3_wgrad(dt, code, tol, N, c0, c1, cout, S, store, tg):
     """dw += (flags 0) or dw = (PCMS_GRAD_STORE: the first writer of a fresh gradient; the
-    buffer's old contents must not leak through) the weight gradient."""
+    buffer's old contents must not leak through) the weight gradient.  tg: bf16 grids of at
+    most tg boxes split their taps over two workgroups (tg 0: voxel splits only)."""
     L = _lib()
+    old_tg = L.query("pcms_conv3_wgrad_tg_maxbox", tg)
+    try:
+        _wgrad_case(L, dt, code, N, c0, c1, cout, S, store)
+    finally:
+        L.query("pcms_conv3_wgrad_tg_maxbox", old_tg)
+
+
+def _wgrad_case(L, dt, code, N, c0, c1, cout, S, store):
     g = torch.Generator().manual_seed(c0 + 3 * cout)
     cin = c0 + c1
     cin_real = 5 if cin == 8 else cin
@@ -447,8 +458,8 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     up = F.pad(u, [dxx // 2, dxx - dxx // 2, dyy // 2, dyy - dyy // 2, dz // 2, dz - dz // 2])
     gout = torch.randn(up.shape, generator=g).to(dt)
     up.backward(gout.double())
-    fp = torch.empty(8 * cin * cout, dtype=dt, device=DEV)
-    dp = torch.empty(8 * cin * cout, dtype=dt, device=DEV)
+    fp = torch.empty(L.query("pcms_convt_pack_elems", code, cin, cout), dtype=dt, device=DEV)
+    dp = torch.empty(L.query("pcms_convt_pack_elems", code, cin, cout), dtype=dt, device=DEV)
     wdev = w.float().to(DEV)
     L.call("pcms_convt_pack", code, wdev, fp, cin, cout, 0)
     L.call("pcms_convt_pack", code, wdev, dp, cin, cout, 1)
@@ -477,6 +488,38 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     close(ncdhw(dxs.cpu()), xr.grad, tol, "convT dgrad (K-split)")
     close(dw.cpu(), wr.grad, 1e-4 if code else 2e-5, "convT wgrad")
     close(db.cpu(), br.grad, 1e-4 if code else 1e-5, "convT bias grad")
+
+
+@pytest.mark.parametrize("Sin,Sout", [((32, 32, 24), (64, 64, 48)), ((24, 20, 12), (49, 41, 25))])
+def test_convt_fwd_stream(Sin, Sout):
+    """The persistent level-0 ConvTranspose forward (Cin 128, Cout 64; several 64-voxel tiles
+    per workgroup, a partial last tile, F.pad ring) is bit-identical to the LDS kernel and
+    matches fp64 on the bf16-rounded inputs."""
+    L = _lib()
+    g = torch.Generator().manual_seed(11)
+    N, cin, cout = 2, 128, 64
+    x = torch.randn(N, cin, *Sin, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cin, cout, 2, 2, 2, generator=g) / math.sqrt(cin)).to(torch.bfloat16)
+    b = torch.randn(cout, generator=g)
+    u = F.conv_transpose3d(x.double(), w.double(), b.double(), stride=2)
+    dz, dyy, dxx = (Sout[i] - u.shape[2 + i] for i in range(3))
+    ref = F.pad(u, [dxx // 2, dxx - dxx // 2, dyy // 2, dyy - dyy // 2, dz // 2, dz - dz // 2])
+    fp = torch.empty(L.query("pcms_convt_pack_elems", 1, cin, cout), dtype=torch.bfloat16, device=DEV)
+    L.call("pcms_convt_pack", 1, w.float().to(DEV), fp, cin, cout, 0)
+    xd = ndhwc(x).to(DEV)
+    outs = []
+    old = L.query("pcms_convt_fwd_stream", -1)
+    try:
+        for on in (1, 0):
+            L.query("pcms_convt_fwd_stream", on)
+            o = torch.full((N, *Sout, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+            L.call("pcms_convt_fwd", 1, xd, fp, b.to(DEV), o, N, *Sin, cin, cout, *Sout)
+            outs.append(o)
+    finally:
+        L.query("pcms_convt_fwd_stream", old)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    close(ncdhw(outs[0].cpu()), ref, 1e-2, "convT stream fwd")
 
 
 @pytest.mark.parametrize("dt,code,tol", DTS)

@@ -19,7 +19,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 KERNELS = {
     "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E"],
     "stem.hip": ["stem_fwd_direct_kernelILi2ELi3E", "stem_fwd_direct_kernelILi3ELi2E", "stem_wgrad_stream_kernel"],
-    "convt.hip": ["convt_lds_kernel"],
+    "convt.hip": ["convt_lds_kernel", "convt_fwd_stream_kernel"],
     # streaming fusions: a spill there would add scratch traffic to an HBM-bound pass
     "ops.hip": ["maxpool_bwd_bn_kernel", "head_bwd_kernel", "head_bn_apply_kernel", "bn_relu_pool_kernel"],
 }

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--size", default="128,128,64")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="fp32: the conv MFMA fraction counts the bf16x6 work (6 bf16 MFMA products per product)")
     ap.add_argument("--wgrad-target", type=int, default=0, help="engine.wgrad_target override")
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
@@ -57,7 +59,8 @@ def main():
     spatial = tuple(int(v) for v in a.size.split(","))
     torch.manual_seed(0)
     tr = Trainer({"device": "cuda", "learning_rate": 1e-4, "batch_size": a.batch, "num_epochs": 1,
-                  "loss": "bce_dice", "precision": "bf16"})
+                  "loss": "bce_dice", "precision": a.precision})
+    xf = 6 if a.precision == "fp32" else 1  # bf16 MFMA work per FLOP of the 3x3x3 convs
     if a.wgrad_target:
         tr.model.engine().wgrad_target = a.wgrad_target
     b = make_batch(a.batch, spatial, seed=1)
@@ -89,7 +92,7 @@ def main():
     rows = []
     for i, (n, ar, _) in enumerate(per[0]):
         us = statistics.median(p[i][2] for p in per)
-        f = flops(n, ar)
+        f = flops(n, ar) * (xf if n.startswith("pcms_conv3") else 1)
         rows.append({"i": i, "name": n, "desc": desc(n, ar), "us": round(us, 1), "gflop": round(f / 1e9, 2),
                      "mfma_frac": round(f / (us * 1e-6) / PEAK, 3) if f else None})
     tot = sum(r["us"] for r in rows)
