@@ -734,9 +734,13 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // for every wave; the fourth (waves 0-2: taps 24-26) in a uniform branch at the step's end,
   // its fragment also one step ahead (one code path: no per-variant register allocation).
   auto compute_fixed = [&](const char* buf) __attribute__((always_inline)) {
-    constexpr int LD = LBW >= 3 ? LBD : 0, LH = LBW >= 3 ? LBH : 0, LW = LBW >= 3 ? LBW : 4;
+    constexpr int LD = LBW >= 2 ? LBD : 0, LH = LBW >= 2 ? LBH : 0, LW = LBW >= 2 ? LBW : 4;
     constexpr int HHc = (1 << LH) + 2, HWc = (1 << LW) + 2;
     constexpr int NK = (1 << (LD + LH + LW)) / 16;
+    // halo rows between a lane's two voxels vl and vl + 4: the same w-row (w >= 8: vl % 8 < 4)
+    // or, at w = 4, the next h-row (LH >= 2: a 16-voxel step stays inside one d-plane)
+    static_assert(LW >= 3 || (LW == 2 && LH >= 2), "compile-time wgrad box");
+    constexpr int D4 = LW >= 3 ? 4 : HWc;
     const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
     const int vl = 8 * hsel + qq;  // the lane's first voxel inside a step
     const int vrow = (vl >> LW) * HWc + (vl & ((1 << LW) - 1));  // its halo row offset
@@ -761,10 +765,10 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       fa[set][0] = cat(tr_read(ab0, s * 2048), tr_read(ab0, s * 2048 + 512));
       fa[set][1] = cat(tr_read(ab1, s * 2048), tr_read(ab1, s * 2048 + 512));
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) fb[set][j] = cat(tr_read(bb[j], hro(s)), tr_read(bb[j], hro(s) + 4 * Tr::XROW));
+      for (int j = 0; j < NJ; ++j) fb[set][j] = cat(tr_read(bb[j], hro(s)), tr_read(bb[j], hro(s) + D4 * Tr::XROW));
     };
     auto load3 = [&](int s, int set) __attribute__((always_inline)) {
-      f3[set] = cat(tr_read(bb[3], hro(s)), tr_read(bb[3], hro(s) + 4 * Tr::XROW));
+      f3[set] = cat(tr_read(bb[3], hro(s)), tr_read(bb[3], hro(s) + D4 * Tr::XROW));
     };
     load(0, 0);
     if (four) load3(0, 0);
@@ -784,7 +788,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     });
   };
   auto compute_box = [&](const char* buf) __attribute__((always_inline)) {
-    if constexpr (!kX3 && !kX6 && LBW >= 3) compute_fixed(buf);
+    if constexpr (!kX3 && !kX6 && LBW >= 2) compute_fixed(buf);
     else compute(buf);
   };
 
@@ -1760,6 +1764,7 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
     } else if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
     else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
     else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3>;
+    else if (q.b.lbd == 3 && q.b.lbh == 3 && q.b.lbw == 2) kern = conv3_wgrad_kernel<bf16_t, 3, 3, 2>;  // level 4
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
   } else if (dtype == PCMS_F32X3) {

@@ -253,6 +253,7 @@ def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S, wgs):
     (2, 256, 0, 64, (1, 2, 1)),
     (1, 64, 64, 128, (4, 8, 8)),        # one box: the unsplit direct flush (16-B RMW of dw)
     (2, 128, 0, 128, (16, 16, 8)),      # level-3 geometry (compile-time 4x8x8 box), 16 boxes
+    (2, 64, 0, 64, (8, 8, 4)),          # level-4 geometry (compile-time 8x8x4 box, 4-wide steps)
 ])
 @pytest.mark.parametrize("store", [0, 1])
 @pytest.mark.parametrize("tg", [64, 0])
