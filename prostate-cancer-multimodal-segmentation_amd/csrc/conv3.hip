@@ -29,7 +29,9 @@ namespace {
 
 // LBD/LBH/LBW >= 0: compile-time box geometry (the hot (4, 8, 16) box: halo decode and tap
 // offsets become constant arithmetic); -1: runtime geometry from p.
-template <typename T, int MINW, int LBD, int LBH, int LBW>
+// MTW: M-tiles per wave (4: 512-voxel boxes; 2: boxes of <= 256 voxels -- level 4's 8x8x4 --
+// on all four waves instead of two)
+template <typename T, int MINW, int LBD, int LBH, int LBW, int MTW = 4>
 __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p) {
   const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   typedef Traits<T> Tr;
@@ -54,24 +56,24 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
 
   const bool w16 = lbw_ == 4;
   const int prow = w16 ? perm32(r_lane) : r_lane;
-  int hb[4];
+  int hb[MTW];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    int r = wave * 128 + mt * 32 + prow;
+  for (int mt = 0; mt < MTW; ++mt) {
+    int r = wave * (32 * MTW) + mt * 32 + prow;
     if (r >= boxvol) r = 0;
     int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
     hb[mt] = (rd * HH + rh) * HW + rw;
   }
-  const bool wave_active = wave * 128 < boxvol;
+  const bool wave_active = wave * (32 * MTW) < boxvol;
 
   // fp32 data (x3_t / x6_t): the fp32 halo split into bf16 parts in LDS, three MFMAs per
   // (M-tile, N-tile, tap) instead of two
   constexpr bool kX3 = std::is_same<T, x3_t>::value, kX6 = std::is_same<T, x6_t>::value;
   constexpr bool kSplit = kX3 || kX6;
   typedef typename Tr::Mem M;
-  f32x16_t acc[4][2];
+  f32x16_t acc[MTW][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MTW; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -169,13 +171,13 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
       if constexpr (kX6) return lds_slot(lds, row, 2 * hsel);
       else return lds_a(lds, row, 1, hsel);
     };
-    s16x8_t a[2][4];
+    s16x8_t a[2][MTW];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+    for (int mt = 0; mt < MTW; ++mt) {
       a[0][mt] = lds_a(lds, hb[mt], 0, hsel);
       a[1][mt] = frag1(hb[mt]);
     }
-    auto tap_step = [&](int tap, int set, const int (&hbk)[4]) {
+    auto tap_step = [&](int tap, int set, const int (&hbk)[MTW]) {
       load_b(bset[set ^ 1], min(tap + 1, 26));
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tap's MFMAs
       const int tn = tap + 1 < 27 ? tap + 1 : 0;
@@ -185,7 +187,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
         // x6: [h|m].[h|h] + [h|l].[m|h] + [h|m].[l|m] (a[0], a[1]; B ks 0, 1, 2)
         constexpr int b1 = kX6 ? 1 : 0, b2 = kX6 ? 2 : 1;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
+        for (int mt = 0; mt < MTW; ++mt) {
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[0][mt], bset[set][nt][0], acc[mt][nt]);
 #pragma unroll
@@ -196,7 +198,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
           a[0][mt] = lds_a(lds, hbk[mt] + offn, 0, hsel);
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < 2 * MTW; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // 3 MFMA
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
         }
@@ -204,14 +206,14 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) {
+          for (int mt = 0; mt < MTW; ++mt) {
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma(a[ks][mt], bset[set][nt][ks], acc[mt][nt]);
             a[ks][mt] = lds_a(lds, hbk[mt] + offn, ks, hsel);
           }
         // (the scheduler would otherwise sink all eight reads below the last MFMA)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < 2 * MTW; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
         }
@@ -220,16 +222,16 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     for (int kdh = 0; kdh < 8; kdh += 2) {
       // row bases from an opaque copy: the fragment addresses are recomputed per trip rather
       // than hoisted out of the loops (and spilled)
-      int hbk[4];
+      int hbk[MTW];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
+      for (int mt = 0; mt < MTW; ++mt) hbk[mt] = opaque(hb[mt]);
 #pragma unroll
       for (int j = 0; j < 6; ++j) tap_step(kdh * 3 + j, j & 1, hbk);
     }
     {
-      int hbk[4];
+      int hbk[MTW];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) hbk[mt] = opaque(hb[mt]);
+      for (int mt = 0; mt < MTW; ++mt) hbk[mt] = opaque(hb[mt]);
 #pragma unroll
       for (int j = 0; j < 3; ++j) tap_step(24 + j, j & 1, hbk);
     }
@@ -251,11 +253,11 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
   uint64_t vmask = 0;  // bit mt * 16 + e: row valid
   if (wave_active) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
-        const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
+        const int r = wave * (32 * MTW) + mt * 32 + (w16 ? perm32(rr) : rr);
         bool valid = r < boxvol;
         if (valid && !interior) {
           const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
@@ -274,11 +276,11 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     bf16_t* ct = reinterpret_cast<bf16_t*>(lds);
     if (wave_active) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < MTW; ++mt) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
-          const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
+          const int r = wave * (32 * MTW) + mt * 32 + (w16 ? perm32(rr) : rr);
           const bool valid = (vmask >> (mt * 16 + e)) & 1;
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
@@ -304,12 +306,12 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     }
   } else if (wave_active) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+    for (int mt = 0; mt < MTW; ++mt) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         if (!((vmask >> (mt * 16 + e)) & 1)) continue;
         const int rr = (e & 3) + 8 * (e >> 2) + 4 * hsel;
-        const int r = wave * 128 + mt * 32 + (w16 ? perm32(rr) : rr);
+        const int r = wave * (32 * MTW) + mt * 32 + (w16 ? perm32(rr) : rr);
         const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
         const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
         const long vox = ((long)n * p.D + gd) * plane + (long)gh * p.W + gw;
@@ -345,7 +347,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     float sd[2] = {0.f, 0.f};
     if (wave_active) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           if (!((vmask >> (mt * 16 + e)) & 1)) continue;
@@ -1516,6 +1518,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 // big-box forward: bf16, whole 8x8x16 boxes, 16-channel chunks of both sources, enough boxes
 // to give every CU one (pcms_conv3_big_min_boxes), every byte offset inside a 32-bit voffset
 static int g_big_min_boxes = 256;
+static int g_conv_mtw2 = 1;  // boxes of <= 256 voxels on 2 M-tiles per wave (A/B switch)
 static int g_big_max_wgs = 0;  // persistent grid cap (0: one workgroup per CU)
 static bool big_fwd_ok(int dtype, int N, int D, int H, int W, int c0, int c1) {
   if (dtype != PCMS_BF16 || D % kBgBD || H % 8 || W % 16 || c0 % 16 || c1 % 16 || c0 < 16) return false;
@@ -1561,6 +1564,14 @@ int pcms_conv3_big_min_boxes(int v) {
 int pcms_conv3_big_max_wgs(int v) {
   const int old = g_big_max_wgs;
   if (v >= 0) g_big_max_wgs = v;
+  return old;
+}
+
+// general-kernel boxes of <= 256 voxels on four waves of 2 M-tiles (1) or two of 4 (0);
+// v < 0 queries; returns the previous setting
+int pcms_conv3_small_box_mtw2(int v) {
+  const int old = g_conv_mtw2;
+  if (v >= 0) g_conv_mtw2 = v;
   return old;
 }
 
@@ -1669,14 +1680,17 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   }
   dim3 grid(N * p.nbd * p.nbh * p.nbw, Cout / 64, splits);
   const bool hot = b.lbd == 2 && b.lbh == 3 && b.lbw == 4;
+  const bool small = b.lbd + b.lbh + b.lbw <= 8 && g_conv_mtw2;  // <= 256 voxels: 2 M-tiles per wave
   if (dtype == PCMS_BF16) {
     if (hot) hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2, 2, 3, 4>), grid, dim3(kThreads), 0, s, p);
+    else if (small) hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2, -1, -1, -1, 2>), grid, dim3(kThreads), 0, s, p);
     else hipLaunchKernelGGL((conv3_fwd_kernel<bf16_t, 2, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
   } else if (dtype == PCMS_F32X3) {
     if (hot) hipLaunchKernelGGL((conv3_fwd_kernel<x3_t, 2, 2, 3, 4>), grid, dim3(kThreads), 0, s, p);
     else hipLaunchKernelGGL((conv3_fwd_kernel<x3_t, 2, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
   } else {
     if (hot) hipLaunchKernelGGL((conv3_fwd_kernel<x6_t, 2, 2, 3, 4>), grid, dim3(kThreads), 0, s, p);
+    else if (small) hipLaunchKernelGGL((conv3_fwd_kernel<x6_t, 2, -1, -1, -1, 2>), grid, dim3(kThreads), 0, s, p);
     else hipLaunchKernelGGL((conv3_fwd_kernel<x6_t, 2, -1, -1, -1>), grid, dim3(kThreads), 0, s, p);
   }
   PCMS_CHECK_LAUNCH();

@@ -160,6 +160,47 @@ def test_bn_stats_large_mean(N, S, split):
     close(mean, yref.mean(1), 1e-6, "mean")
 
 
+@pytest.mark.parametrize("code", [1, 0])
+def test_conv3_small_box_two_mtiles_per_wave(code):
+    """Level-4 boxes (8x8x4 = 256 voxels) on four waves of 2 M-tiles: outputs bit-identical to
+    two waves of 4 (the same MFMA sequence per output tile), unsplit and split-K; the BN
+    partials group their sums by wave, so they agree to fp32 rounding."""
+    L = _lib()
+    dt = torch.bfloat16 if code == 1 else torch.float32
+    g = torch.Generator().manual_seed(21)
+    N, S, cin, cout = 2, (8, 8, 4), 128, 128
+    x = torch.randn(N, cin, *S, generator=g).to(dt)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+    b = torch.randn(cout, generator=g)
+    wp = torch.empty(L.query("pcms_conv3_pack_elems", code, cout, cin), dtype=dt, device=DEV)
+    L.call("pcms_conv3_pack", code, w.to(DEV), wp, cout, cin, 0)
+    xd = ndhwc(x).to(DEV)
+    nvox = N * S[0] * S[1] * S[2]
+    rows = L.query("pcms_conv3_fwd_rows", code, N, *S, cin, 0, cout)
+    outs = []
+    old = L.query("pcms_conv3_small_box_mtw2", -1)
+    try:
+        for on in (1, 0):
+            L.query("pcms_conv3_small_box_mtw2", on)
+            y = torch.empty(N, *S, cout, dtype=dt, device=DEV)
+            st = torch.zeros(rows * (cout * 2 + 1), device=DEV)
+            L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wp, b.to(DEV), y, None, cout, None, st, 0, N, *S, cout, 1)
+            ns = L.query("pcms_conv3_splits", code, cin, 3)
+            acc = torch.full((ns * nvox * cout,), float("nan"), device=DEV)
+            ys = torch.empty_like(y)
+            L.call("pcms_conv3_fwd", code, xd, cin, None, 0, wp, b.to(DEV), ys, None, cout, acc, None, 0, N, *S, cout, 3)
+            L.call("pcms_split_epilogue", code, acc, ns, b.to(DEV), ys, None, cout, None, cout, nvox, 0)
+            outs.append((y, st, ys))
+    finally:
+        L.query("pcms_conv3_small_box_mtw2", old)
+    torch.cuda.synchronize()
+    for i in (0, 2):
+        assert torch.equal(outs[0][i].view(torch.uint8), outs[1][i].view(torch.uint8))
+    close(outs[0][1].cpu(), outs[1][1].cpu(), 1e-5, "BN partials")
+    ref = F.conv3d(x.double(), w.to(dt).double(), b.double(), padding=1)
+    close(ncdhw(outs[0][0].cpu()), ref, 1e-2 if code == 1 else 2e-5, "small-box conv")
+
+
 @pytest.mark.parametrize("dt,code,tol", CONV_DTS)
 def test_conv3_dual_source_and_dgrad_split_output(dt, code, tol):
     """Up3D: conv over cat([skip, up]) without materialising the cat, and the dgrad whose
