@@ -95,14 +95,10 @@ __device__ __forceinline__ void colsum_final(const double* ws, int C, int c, dou
 }
 
 // Stage 2: -> mean/invstd/scale/shift (+ running stats when training)
-__global__ void bn_finalize_kernel(const double* ws, int C, double count, const float* gamma, const float* beta,
-                                   float* rmean, float* rvar, long long* nbt, float momentum, float eps,
-                                   float* scale, float* shift, float* mean_out, float* invstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (nbt && c == 0) *nbt += 1;
-  if (c >= C) return;
-  double s1, s2;
-  colsum_final(ws, C, c, s1, s2);
+__device__ __forceinline__ void bn_finalize_one(int c, double s1, double s2, double count, const float* gamma,
+                                                const float* beta, float* rmean, float* rvar, float momentum,
+                                                float eps, float* scale, float* shift, float* mean_out,
+                                                float* invstd_out) {
   const double mean = s1 / count;
   double var = s2 / count - mean * mean;
   if (var < 0) var = 0;
@@ -116,6 +112,16 @@ __global__ void bn_finalize_kernel(const double* ws, int C, double count, const 
     rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mean);
     rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
   }
+}
+__global__ void bn_finalize_kernel(const double* ws, int C, double count, const float* gamma, const float* beta,
+                                   float* rmean, float* rvar, long long* nbt, float momentum, float eps,
+                                   float* scale, float* shift, float* mean_out, float* invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nbt && c == 0) *nbt += 1;
+  if (c >= C) return;
+  double s1, s2;
+  colsum_final(ws, C, c, s1, s2);
+  bn_finalize_one(c, s1, s2, count, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean_out, invstd_out);
 }
 
 // Eval-mode BatchNorm folded into the conv before it (UNet3D.predict / inference,
@@ -231,18 +237,75 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_reduce_kernel(
 
 // pass 2: fp64 column sums -> dgamma/dbeta (+=) and the apply coefficients
 //   dy = k1*g + k2*xhat + k3, k1 = gamma*invstd, k2 = -k1*sum(g xhat)/M, k3 = -k1*sum(g)/M
-__global__ void bn_bwd_finalize_kernel(const double* ws, int C, double count, const float* gamma,
-                                       const float* invstd, float* dgamma, float* dbeta, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1, s2;
-  colsum_final(ws, C, c, s1, s2);
+__device__ __forceinline__ void bn_bwd_finalize_one(int c, double s1, double s2, double count, const float* gamma,
+                                                    const float* invstd, float* dgamma, float* dbeta, float* coef) {
   dbeta[c] += (float)s1;
   dgamma[c] += (float)s2;
   const double k1 = (double)gamma[c] * (double)invstd[c];
   coef[c * 3 + 0] = (float)k1;
   coef[c * 3 + 1] = (float)(-k1 * s2 / count);
   coef[c * 3 + 2] = (float)(-k1 * s1 / count);
+}
+__global__ void bn_bwd_finalize_kernel(const double* ws, int C, double count, const float* gamma,
+                                       const float* invstd, float* dgamma, float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1, s2;
+  colsum_final(ws, C, c, s1, s2);
+  bn_bwd_finalize_one(c, s1, s2, count, gamma, invstd, dgamma, dbeta, coef);
+}
+
+// Few partial rows (<= kSmallRows): the column sums and the finalize in ONE launch, one block
+// per 64 channels (no cross-block dependency): 4 row lanes x 64 channels, lane rl adds rows
+// rl, rl + 4, ... in order (8 rows' loads in flight), the 4 lanes summed in a fixed order
+// (deterministic).  Saves the second launch of the two-stage path (~5 us each, 36 per step).
+constexpr int kSmallRows = 512;
+template <bool BWD>
+__global__ void __launch_bounds__(256) colsum_finalize_small_kernel(
+    const float* part, int rows, int C, const float* cnt, double count, const float* gamma, const float* beta,
+    float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* scale, float* shift,
+    float* mean_out, float* invstd, float* dgamma, float* dbeta, float* coef) {
+  __shared__ double red[4][64][2];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  if (!BWD && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    int r = rl;
+    for (; r + 28 < rows; r += 32) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(part + ((long)(r + 4 * u) * C + c) * 2);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s1 += (double)v[u].x;
+        if (cnt) {
+          const double n = (double)cnt[r + 4 * u];
+          s2 += (double)v[u].y + (n > 0.0 ? (double)v[u].x * (double)v[u].x / n : 0.0);
+        } else {
+          s2 += (double)v[u].y;
+        }
+      }
+    }
+    for (; r < rows; r += 4) {
+      const float2 v = *reinterpret_cast<const float2*>(part + ((long)r * C + c) * 2);
+      s1 += (double)v.x;
+      if (cnt) {
+        const double n = (double)cnt[r];
+        s2 += (double)v.y + (n > 0.0 ? (double)v.x * (double)v.x / n : 0.0);
+      } else {
+        s2 += (double)v.y;
+      }
+    }
+  }
+  red[rl][cl][0] = s1;
+  red[rl][cl][1] = s2;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    for (int g = 1; g < 4; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
+    if constexpr (BWD) bn_bwd_finalize_one(c, s1, s2, count, gamma, invstd, dgamma, dbeta, coef);
+    else bn_finalize_one(c, s1, s2, count, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean_out, invstd);
+  }
 }
 
 // NT: as bn_relu_kernel (level-0 apply: 805 MB in 118 us = 6.8 TB/s)
@@ -1157,6 +1220,12 @@ int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long 
 int pcms_bn_finalize(const float* part, int rows, int C, double count, const float* gamma, const float* beta,
                      float* rmean, float* rvar, long long* nbt, float momentum, float eps,
                      float* scale, float* shift, float* mean, float* invstd, double* ws, hipStream_t s) {
+  if (rows <= kSmallRows) {
+    hipLaunchKernelGGL(colsum_finalize_small_kernel<false>, dim3(cdiv(C, 64)), dim3(256), 0, s, part, rows, C,
+                       part + (long)rows * C * 2, count, gamma, beta, rmean, rvar, nbt, momentum, eps, scale, shift,
+                       mean, invstd, nullptr, nullptr, nullptr);
+    PCMS_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, part, rows, C,
                      part + (long)rows * C * 2, ws);
   hipError_t e = hipGetLastError();
@@ -1235,12 +1304,19 @@ int pcms_bn_relu_bwd_finish(int dtype, const void* da, const void* y, const floa
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || (TPB % (C / VEC)) != 0) return -1;
   const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
-  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C,
-                     (const float*)nullptr, ws);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, s, (const double*)ws, C, (double)nvox,
-                     gamma, invstd, dgamma, dbeta, coef);
+  hipError_t e;
+  if (rows <= kSmallRows) {
+    hipLaunchKernelGGL(colsum_finalize_small_kernel<true>, dim3(cdiv(C, 64)), dim3(256), 0, s, part, rows, C,
+                       (const float*)nullptr, (double)nvox, gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f,
+                       nullptr, nullptr, nullptr, const_cast<float*>(invstd), dgamma, dbeta, coef);
+  } else {
+    hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 64), kRB), dim3(256), 0, s, (const float*)part, rows, C,
+                       (const float*)nullptr, ws);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, s, (const double*)ws, C,
+                       (double)nvox, gamma, invstd, dgamma, dbeta, coef);
+  }
   e = hipGetLastError();
   if (e != hipSuccess || dy == nullptr) return (int)e;  // dy NULL: the consumer applies (coef)
   const int grid = ew_grid(dtype, C, nvox);
