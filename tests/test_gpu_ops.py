@@ -340,6 +340,27 @@ def _wgrad_case(L, dt, code, N, c0, c1, cout, S, store):
     close(got, wr.grad, 1e-4 if code else 2e-5, "wgrad")
 
 
+@pytest.mark.parametrize("c0,c1,S", [(64, 0, (32, 32, 32)), (32, 32, (24, 20, 40))])
+def test_conv3_wgrad_many_boxes(c0, c1, S):
+    """bf16 weight gradient over a grid of many boxes (the level-0..2 voxel-split plan, partial
+    last boxes, two sources) vs fp64."""
+    L = _lib()
+    g = torch.Generator().manual_seed(31)
+    N, cout = 2, 64
+    cin = c0 + c1
+    x = torch.randn(N, cin, *S, generator=g).to(torch.bfloat16)
+    dy = torch.randn(N, cout, *S, generator=g).to(torch.bfloat16)
+    wr = torch.zeros(cout, cin, 3, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv3d(x.double(), wr, None, padding=1).backward(dy.double())
+    ws = torch.empty(L.query("pcms_conv3_wgrad_ws_floats", 1, N, *S, c0, c1, cout, 256), device=DEV)
+    x0 = ndhwc(x[:, :c0]).to(DEV)
+    x1 = ndhwc(x[:, c0:]).to(DEV) if c1 else None
+    dw = torch.full((cout * cin * 27,), float("nan"), device=DEV)
+    L.call("pcms_conv3_wgrad", 1, x0, c0, x1, c1, ndhwc(dy).to(DEV), dw, ws, N, *S, cout, cin, 256, 1)
+    torch.cuda.synchronize()
+    close(dw.cpu().view(cout, cin, 3, 3, 3), wr.grad, 1e-4, "many-box wgrad vs fp64")
+
+
 @pytest.mark.parametrize("dt,code,tol", DTS)
 def test_bn_relu_fwd_bwd(dt, code, tol):
     L = _lib()
