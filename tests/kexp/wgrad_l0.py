@@ -1,5 +1,6 @@
-"""Level-0 bf16 weight gradient (64 -> 64 at 2 x 128x128x64, fresh-gradient store), 3 launches:
-the command the PMC passes of tests/kexp/pmc_wgrad.sh profile (test tooling)."""
+"""bf16 weight gradient at one level (fresh-gradient store), 3 launches: the command the PMC
+passes of tests/kexp/pmc_wgrad.sh profile (test tooling).  WGRAD_LEVEL=0 (64 -> 64 at
+2 x 128x128x64, default), 1 (128 -> 128 at 2 x 64x64x32), 3 (512 -> 512 at 2 x 16x16x8)."""
 import os
 import sys
 
@@ -9,7 +10,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import pcms_amd  # noqa: E402,F401
 from pcms_amd import _lib as L  # noqa: E402
 
-N, D, H, W, c0, co = 2, 128, 128, 64, 64, 64
+lev = int(os.environ.get("WGRAD_LEVEL", "0"))
+N, c0 = 2, 64 << lev
+D, H, W = 128 >> lev, 128 >> lev, 64 >> lev
+co = c0
 x0 = torch.relu(torch.randn(N * D * H * W * c0, device="cuda")).to(torch.bfloat16)
 dy = torch.randn(N * D * H * W * co, device="cuda").to(torch.bfloat16)
 dw = torch.zeros(co * c0 * 27, device="cuda")
