@@ -16,6 +16,7 @@
 //   256 no staging at all (the compute phase alone)
 //   512 the next box's pieces issued one per compute step (interleaved with the MFMAs)
 //   1024 MFMA operands all zero (lower power: tells clock effects from pipeline conflicts)
+//   2048 wave specialisation: the two waves of SIMD 3 issue every piece and run no MFMAs
 // Built by tests/kexp/Makefile (libdmaprobe.so), driven by tests/kexp/dma_probe.py.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,7 +37,7 @@ __global__ void __launch_bounds__(kT, 1) probe_kernel(const uint16_t* x, const u
                                                       uint32_t xbytes, uint32_t dybytes, float* sink) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr bool kDepth2 = F & 1, kReg = F & 2, kL2 = F & 4, kWide = F & 8, kDyOnly = F & 16, kXOnly = F & 32;
-  constexpr bool kMfma = F & 64, kLdsRd = F & 128, kNoStage = F & 256, kInter = F & 512, kZero = F & 1024;
+  constexpr bool kMfma = F & 64, kLdsRd = F & 128, kNoStage = F & 256, kInter = F & 512, kZero = F & 1024, kSpec = F & 2048;
   constexpr int XROWB = kWide ? 128 : 64;
   constexpr int XP = kHalo * XROWB / 16;
   constexpr int NP = (kXOnly ? 0 : kDyP) + (kDyOnly ? 0 : XP);
@@ -62,9 +63,13 @@ __global__ void __launch_bounds__(kT, 1) probe_kernel(const uint16_t* x, const u
     const int d0 = bdi * 4, h0 = bhi * 8, w0 = bwi * 8;
     (void)buf;
     const uint32_t lb = l0;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (kSpec && (wv & 3) != 3) return;
+    constexpr int NI = kSpec ? (NP + 127) / 128 : PER;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int pc0 = __builtin_amdgcn_readfirstlane((tid & ~63) + i * kT);
+    for (int i = 0; i < NI; ++i) {
+      const int pc0 = kSpec ? __builtin_amdgcn_readfirstlane((wv >> 2) * 64 + i * 128)
+                            : __builtin_amdgcn_readfirstlane((tid & ~63) + i * kT);
       if (pc0 >= NP) break;
       if (only >= 0 && i != only) continue;
       const int pc = pc0 + lane;
@@ -114,6 +119,7 @@ __global__ void __launch_bounds__(kT, 1) probe_kernel(const uint16_t* x, const u
   const char* rb = lds + lane * 8 + wave * 1024;
   auto compute = [&](int nb) __attribute__((always_inline)) {
     if constexpr (!kMfma && !kLdsRd) return;
+    if (kSpec && (wave & 3) == 3) return;
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       if constexpr (kInter) if (st < PER && nb >= 0) stage(nb, 0, st);
@@ -185,7 +191,7 @@ extern "C" int probe_run(int flags, const void* x, const void* dy, int N, int D,
     break;
   switch (flags) {
     PROBE(0) PROBE(1) PROBE(2) PROBE(3) PROBE(4) PROBE(5) PROBE(8) PROBE(9) PROBE(16) PROBE(17) PROBE(32) PROBE(33)
-    PROBE(20) PROBE(36) PROBE(64) PROBE(128) PROBE(192) PROBE(320) PROBE(384) PROBE(448) PROBE(576) PROBE(704) PROBE(66) PROBE(194) PROBE(1088) PROBE(1344) PROBE(1600)
+    PROBE(20) PROBE(36) PROBE(64) PROBE(128) PROBE(192) PROBE(320) PROBE(384) PROBE(448) PROBE(576) PROBE(704) PROBE(66) PROBE(194) PROBE(1088) PROBE(1344) PROBE(1600) PROBE(2048) PROBE(2112) PROBE(2240) PROBE(2368) PROBE(2496)
     default: return -1;
   }
 #undef PROBE

@@ -16,7 +16,9 @@ NAMES = {0: "product shape, 1 box in flight", 1: "2 boxes in flight", 2: "regist
          576: "interleaved staging + MFMA phase", 704: "interleaved staging + LDS-fed MFMAs",
          66: "register staging + MFMA phase", 194: "register staging + LDS-fed MFMAs",
          1344: "zero-operand MFMA phase alone", 1088: "staging + zero-operand MFMAs",
-         1600: "interleaved staging + zero-op MFMAs"}
+         1600: "interleaved staging + zero-op MFMAs",
+         2048: "SIMD-3 waves stage (no MFMAs)", 2112: "SIMD-3 stages, SIMDs 0-2 MFMA",
+         2368: "SIMDs 0-2 MFMA alone", 2496: "SIMDs 0-2 LDS-fed MFMA alone", 2240: "SIMD-3 stages, 0-2 LDS-fed MFMA"}
 
 
 def main():
