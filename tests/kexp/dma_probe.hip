@@ -17,6 +17,7 @@
 //   512 the next box's pieces issued one per compute step (interleaved with the MFMAs)
 //   1024 MFMA operands all zero (lower power: tells clock effects from pipeline conflicts)
 //   2048 wave specialisation: the two waves of SIMD 3 issue every piece and run no MFMAs
+//   4096 16 waves (1024 threads) share the pieces and the MFMAs (half the MFMAs per wave)
 // Built by tests/kexp/Makefile (libdmaprobe.so), driven by tests/kexp/dma_probe.py.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -33,10 +34,11 @@ constexpr int kBuf = 256 * 128 + kHalo * 128;  // room for the 128-B-row halo va
 // (every in-flight box lands in the same LDS region: nothing reads it, only the traffic counts)
 
 template <int F>
-__global__ void __launch_bounds__(kT, 1) probe_kernel(const uint16_t* x, const uint16_t* dy, int D, int H, int W,
+__global__ void __launch_bounds__((F & 4096) ? 1024 : 512, 1) probe_kernel(const uint16_t* x, const uint16_t* dy, int D, int H, int W,
                                                       uint32_t xbytes, uint32_t dybytes, float* sink) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr bool kDepth2 = F & 1, kReg = F & 2, kL2 = F & 4, kWide = F & 8, kDyOnly = F & 16, kXOnly = F & 32;
+  constexpr int kT = (F & 4096) ? 1024 : 512;
   constexpr bool kMfma = F & 64, kLdsRd = F & 128, kNoStage = F & 256, kInter = F & 512, kZero = F & 1024, kSpec = F & 2048;
   constexpr int XROWB = kWide ? 128 : 64;
   constexpr int XP = kHalo * XROWB / 16;
@@ -121,7 +123,7 @@ __global__ void __launch_bounds__(kT, 1) probe_kernel(const uint16_t* x, const u
     if constexpr (!kMfma && !kLdsRd) return;
     if (kSpec && (wave & 3) == 3) return;
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
+    for (int st = 0; st < (kT == 1024 ? 8 : 16); ++st) {
       if constexpr (kInter) if (st < PER && nb >= 0) stage(nb, 0, st);
       if constexpr (kInter) __builtin_amdgcn_sched_barrier(0);
       s16x8_t f[6];
@@ -138,7 +140,7 @@ __global__ void __launch_bounds__(kT, 1) probe_kernel(const uint16_t* x, const u
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = mfma(f[j & 1], f[2 + (j & 3)], acc[j]);
         if (kInter) __builtin_amdgcn_sched_barrier(0);
-        if (st == 15)
+        if (st == (kT == 1024 ? 7 : 15))
 #pragma unroll
           for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(acc[j]));
       } else {
@@ -187,11 +189,11 @@ extern "C" int probe_run(int flags, const void* x, const void* dy, int N, int D,
 #define PROBE(F)                                                                                               \
   case F:                                                                                                      \
     (void)hipFuncSetAttribute((const void*)probe_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
-    hipLaunchKernelGGL(probe_kernel<F>, grid, dim3(kT), lds, s, (const uint16_t*)x, (const uint16_t*)dy, D, H, W, xb, db, sink); \
+    hipLaunchKernelGGL(probe_kernel<F>, grid, dim3((F & 4096) ? 1024 : 512), lds, s, (const uint16_t*)x, (const uint16_t*)dy, D, H, W, xb, db, sink); \
     break;
   switch (flags) {
     PROBE(0) PROBE(1) PROBE(2) PROBE(3) PROBE(4) PROBE(5) PROBE(8) PROBE(9) PROBE(16) PROBE(17) PROBE(32) PROBE(33)
-    PROBE(20) PROBE(36) PROBE(64) PROBE(128) PROBE(192) PROBE(320) PROBE(384) PROBE(448) PROBE(576) PROBE(704) PROBE(66) PROBE(194) PROBE(1088) PROBE(1344) PROBE(1600) PROBE(2048) PROBE(2112) PROBE(2240) PROBE(2368) PROBE(2496)
+    PROBE(20) PROBE(36) PROBE(64) PROBE(128) PROBE(192) PROBE(320) PROBE(384) PROBE(448) PROBE(576) PROBE(704) PROBE(66) PROBE(194) PROBE(1088) PROBE(1344) PROBE(1600) PROBE(2048) PROBE(2112) PROBE(2240) PROBE(2368) PROBE(2496) PROBE(4096) PROBE(4160) PROBE(4416) PROBE(4544) PROBE(4288)
     default: return -1;
   }
 #undef PROBE

@@ -18,7 +18,9 @@ NAMES = {0: "product shape, 1 box in flight", 1: "2 boxes in flight", 2: "regist
          1344: "zero-operand MFMA phase alone", 1088: "staging + zero-operand MFMAs",
          1600: "interleaved staging + zero-op MFMAs",
          2048: "SIMD-3 waves stage (no MFMAs)", 2112: "SIMD-3 stages, SIMDs 0-2 MFMA",
-         2368: "SIMDs 0-2 MFMA alone", 2496: "SIMDs 0-2 LDS-fed MFMA alone", 2240: "SIMD-3 stages, 0-2 LDS-fed MFMA"}
+         2368: "SIMDs 0-2 MFMA alone", 2496: "SIMDs 0-2 LDS-fed MFMA alone", 2240: "SIMD-3 stages, 0-2 LDS-fed MFMA",
+         4096: "16 waves stage", 4160: "16 waves: staging + MFMA phase", 4416: "16 waves: MFMA phase alone",
+         4544: "16 waves: LDS-fed MFMA alone", 4288: "16 waves: staging + LDS-fed MFMA"}
 
 
 def main():
