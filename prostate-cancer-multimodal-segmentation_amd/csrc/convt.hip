@@ -258,73 +258,117 @@ __device__ __forceinline__ f32x16_t mfma_x6(s16x8_t a1, s16x8_t a2, const bf16_t
 }
 
 // forward, fp32 build: out[child(m, t)][co] = b[co] + sum_ci x[m][ci] W[ci][co][t]
-// (pack rows q = t Cout + co, Cin / 8 groups of 48 bf16)
-__global__ void __launch_bounds__(256) convt_fwd_x6_kernel(const float* x, const bf16_t* wt, const float* bias,
+// (pack rows q = t Cout + co, Cin / 8 groups of 48 bf16).  Each wave owns MT 32-row M-tiles,
+// so every B fragment (L2) feeds MT x 3 MFMAs: at MT = 1 the weight fragments were 3/4 of the
+// ~8.6 GB a level-0 launch pulled from L2.  The K loop order per accumulator is unchanged.
+template <int MT>
+__global__ void __launch_bounds__(256, 2) convt_fwd_x6_kernel(const float* x, const bf16_t* wt, const float* bias,
                                                            float* out, UpGeom g, int Cin, int Cout) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const long M = (long)g.N * g.Din * g.Hin * g.Win;
-  const long m0 = (long)blockIdx.x * 128 + wave * 32;
+  const long m0 = (long)blockIdx.x * (128 * MT) + wave * (32 * MT);
   const int q0 = blockIdx.y * 64;
   if (m0 >= M) return;
-  const long ma = std::min<long>(m0 + r, M - 1);
-  const float* arow = x + ma * Cin;
-  const bf16_t* b0 = wt + (long)(q0 + 2 * r) * Cin * 6;
-  const bf16_t* b1 = b0 + (long)Cin * 6;
-  f32x16_t acc0, acc1;
-  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  const float* arow[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) arow[i] = x + std::min<long>(m0 + 32 * i + r, M - 1) * Cin;
+  const bf16_t* bp[2];
+  bp[0] = wt + (long)(q0 + 2 * r) * Cin * 6;
+  bp[1] = bp[0] + (long)Cin * 6;
+  f32x16_t acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { acc[i][0][e] = 0.f; acc[i][1][e] = 0.f; }
   for (int k = 0; k < Cin; k += 8) {
-    s16x8_t a1, a2;
-    afrag_x6(arow + k, h, a1, a2);
-    acc0 = mfma_x6(a1, a2, b0 + k * 6, h, acc0);
-    acc1 = mfma_x6(a1, a2, b1 + k * 6, h, acc1);
+    s16x8_t bb[2][3];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) bb[n][j] = *reinterpret_cast<const s16x8_t*>(bp[n] + k * 6 + 16 * j + 8 * h);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      s16x8_t a1, a2;
+      afrag_x6(arow[i] + k, h, a1, a2);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        acc[i][n] = mfma(a1, bb[n][0], acc[i][n]);
+        acc[i][n] = mfma(a2, bb[n][1], acc[i][n]);
+        acc[i][n] = mfma(a1, bb[n][2], acc[i][n]);
+      }
+    }
   }
   const int q = q0 + 2 * r;
   const int t = q / Cout, co = q % Cout;
   const float bias0 = bias[co], bias1 = bias[co + 1];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-    if (m >= M) continue;
-    float* dst = out + child_vox(g, m, t) * Cout + co;
-    dst[0] = acc0[e] + bias0;
-    dst[1] = acc1[e] + bias1;
-  }
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const long m = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (m >= M) continue;
+      float* dst = out + child_vox(g, m, t) * Cout + co;
+      dst[0] = acc[i][0][e] + bias0;
+      dst[1] = acc[i][1][e] + bias1;
+    }
 }
 
 // dgrad, fp32 build: dx[m][ci] = sum_{t, co} dout[child(m, t)][co] Wd[ci][t][co]
-// (pack rows ci, 8 Cout / 8 groups of 48 bf16)
+// (pack rows ci, 8 Cout / 8 groups of 48 bf16); MT 32-row M-tiles per wave as the forward.
 // ws != nullptr: blockIdx.z takes K groups [z G / Z, (z + 1) G / Z) of the G = Cout / 8 per tap
 // x 8 taps and stores its fp32 partial sums to ws[z][m][ci] (summed in z order afterwards)
-__global__ void __launch_bounds__(256) convt_dgrad_x6_kernel(const float* dout, const bf16_t* wd, float* dx,
+template <int MT>
+__global__ void __launch_bounds__(256, 2) convt_dgrad_x6_kernel(const float* dout, const bf16_t* wd, float* dx,
                                                              UpGeom g, int Cin, int Cout, float* ws) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const long M = (long)g.N * g.Din * g.Hin * g.Win;
-  const long m0 = (long)blockIdx.x * 128 + wave * 32;
+  const long m0 = (long)blockIdx.x * (128 * MT) + wave * (32 * MT);
   const int q0 = blockIdx.y * 64;
   if (m0 >= M) return;
-  const long ma = std::min<long>(m0 + r, M - 1);
+  long ma[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) ma[i] = std::min<long>(m0 + 32 * i + r, M - 1);
   const long K = 8L * Cout;
-  const bf16_t* b0 = wd + (long)(q0 + r) * K * 6;
-  const bf16_t* b1 = wd + (long)(q0 + 32 + r) * K * 6;
-  f32x16_t acc0, acc1;
-  for (int e = 0; e < 16; ++e) { acc0[e] = 0.f; acc1[e] = 0.f; }
+  const bf16_t* bp[2];
+  bp[0] = wd + (long)(q0 + r) * K * 6;
+  bp[1] = wd + (long)(q0 + 32 + r) * K * 6;
+  f32x16_t acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { acc[i][0][e] = 0.f; acc[i][1][e] = 0.f; }
   const int G = Cout / 8 * 8, Z = gridDim.z;
   const int g0 = (int)((long)blockIdx.z * G / Z), g1 = (int)((long)(blockIdx.z + 1) * G / Z);
   for (int gi = g0; gi < g1; ++gi) {
     const int t = gi / (Cout / 8), k = (gi % (Cout / 8)) * 8;
-    s16x8_t a1, a2;
-    afrag_x6(dout + child_vox(g, ma, t) * Cout + k, h, a1, a2);
-    acc0 = mfma_x6(a1, a2, b0 + ((long)t * Cout + k) * 6, h, acc0);
-    acc1 = mfma_x6(a1, a2, b1 + ((long)t * Cout + k) * 6, h, acc1);
+    s16x8_t bb[2][3];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        bb[n][j] = *reinterpret_cast<const s16x8_t*>(bp[n] + ((long)t * Cout + k) * 6 + 16 * j + 8 * h);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      s16x8_t a1, a2;
+      afrag_x6(dout + child_vox(g, ma[i], t) * Cout + k, h, a1, a2);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        acc[i][n] = mfma(a1, bb[n][0], acc[i][n]);
+        acc[i][n] = mfma(a2, bb[n][1], acc[i][n]);
+        acc[i][n] = mfma(a1, bb[n][2], acc[i][n]);
+      }
+    }
   }
   float* dst = ws ? ws + (long)blockIdx.z * M * Cin : dx;
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const long m = m0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-    if (m >= M) continue;
-    dst[m * Cin + q0 + r] = acc0[e];
-    dst[m * Cin + q0 + 32 + r] = acc1[e];
-  }
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const long m = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (m >= M) continue;
+      dst[m * Cin + q0 + r] = acc[i][0][e];
+      dst[m * Cin + q0 + 32 + r] = acc[i][1][e];
+    }
 }
 
 // bf16 forward and dgrad, LDS-staged (the hot path).  The direct kernels above read each A
@@ -892,6 +936,11 @@ int pcms_convt_pack_elems(int dtype, int Cin, int Cout) {
 
 // out: skip-sized (N, Do, Ho, Wo, Cout). If the grid is larger than 2x the input the pad
 // ring is zero-filled here (F.pad semantics).
+// fp32 build: 4 M-tiles per wave where that still leaves >= 2 workgroups per CU (level-0
+// forward 1072 -> 683 us, dgrad 1172 -> 734 us; 2 M-tiles: 770 / 759 us)
+constexpr int kX6MT = 4;
+static bool x6_mt4(long M, long colblocks) { return cdiv(M, 128 * kX6MT) * colblocks >= 2L * device_cus(); }
+
 int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bias, void* out,
                    int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
   if (Cin % 16 || Cout % 64) return -1;
@@ -919,10 +968,14 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
     PCMS_CHECK_LAUNCH();
   }
   dim3 grid(cdiv(M, 128), 8 * Cout / 64);
-  if (dtype == PCMS_BF16)
+  if (dtype == PCMS_BF16) {
     hipLaunchKernelGGL(convt_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout);
-  else
-    hipLaunchKernelGGL(convt_fwd_x6_kernel, grid, dim3(256), 0, s, (const float*)x, (const bf16_t*)wpack, bias, (float*)out, g, Cin, Cout);
+  } else if (x6_mt4(M, 8 * Cout / 64)) {
+    grid.x = cdiv(M, 128 * kX6MT);
+    hipLaunchKernelGGL(convt_fwd_x6_kernel<kX6MT>, grid, dim3(256), 0, s, (const float*)x, (const bf16_t*)wpack, bias, (float*)out, g, Cin, Cout);
+  } else {
+    hipLaunchKernelGGL(convt_fwd_x6_kernel<1>, grid, dim3(256), 0, s, (const float*)x, (const bf16_t*)wpack, bias, (float*)out, g, Cin, Cout);
+  }
   PCMS_CHECK_LAUNCH();
 }
 
@@ -982,8 +1035,14 @@ int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* 
   // workgroups -> 256)
   const int S = ws ? convt_dgrad_splits(M, Cin, Cout) : 1;
   grid.z = S;
-  hipLaunchKernelGGL(convt_dgrad_x6_kernel, grid, dim3(256), 0, s, (const float*)dout, (const bf16_t*)wpack_d,
-                     (float*)dx, g, Cin, Cout, S > 1 ? ws : nullptr);
+  if (x6_mt4(M, Cin / 64 * S)) {
+    grid.x = cdiv(M, 128 * kX6MT);
+    hipLaunchKernelGGL(convt_dgrad_x6_kernel<kX6MT>, grid, dim3(256), 0, s, (const float*)dout, (const bf16_t*)wpack_d,
+                       (float*)dx, g, Cin, Cout, S > 1 ? ws : nullptr);
+  } else {
+    hipLaunchKernelGGL(convt_dgrad_x6_kernel<1>, grid, dim3(256), 0, s, (const float*)dout, (const bf16_t*)wpack_d,
+                       (float*)dx, g, Cin, Cout, S > 1 ? ws : nullptr);
+  }
   if (S > 1) {
     const long E = M * Cin;
     hipLaunchKernelGGL(convt_dgrad_reduce<float>, dim3((unsigned)cdiv(E / 4, 256)), dim3(256), 0, s, (const float*)ws,

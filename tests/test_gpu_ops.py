@@ -505,7 +505,8 @@ def test_bn_relu_pool_and_maxpool_bwd_bn(dt, code, tol, S, C):
 @pytest.mark.parametrize("dt,code,tol", DTS)
 @pytest.mark.parametrize("Sin,Sout,cin,cout",[((4, 4, 2), (8, 8, 4), 128, 64), ((2, 2, 3), (5, 4, 7), 128, 64),
                                                ((8, 8, 6), (16, 16, 12), 256, 128),  # > 1 tile, 2 co chunks
-                                               ((8, 8, 4), (16, 16, 8), 1024, 512)])  # level 4 (split dgrad)
+                                               ((8, 8, 4), (16, 16, 8), 1024, 512),  # level 4 (split dgrad)
+                                               ((31, 32, 17), (62, 64, 34), 128, 64)])  # fp32: 4 M-tiles per wave, ragged
 def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     L = _lib()
     g = torch.Generator().manual_seed(9)
