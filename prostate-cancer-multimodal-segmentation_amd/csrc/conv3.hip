@@ -1011,6 +1011,22 @@ __global__ void __launch_bounds__(256) pack_conv3_kernel(const float* w, T* out,
     tile[jj][k][t] = v;
   }
   __syncthreads();
+  if constexpr (std::is_same<T, x6_t>::value) {
+    // one thread per packed row (t, jj): its 8 k values split once, the 96-B row
+    // [h|h] [m|h] [l|m] written as six 16-B stores (consecutive threads: consecutive rows)
+    static_assert(CK == 8, "x6 pack rows hold 8 k");
+    const int jj = threadIdx.x % 8, t = threadIdx.x / 8;
+    if (t < 27 && j0 + jj < J) {
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = flip ? tile[jj][k][26 - t] : tile[jj][k][t];
+      u32x4_t h, m, l;
+      split3x8(f, h, m, l);
+      u32x4_t* o = reinterpret_cast<u32x4_t*>(reinterpret_cast<bf16_t*>(out) + (((long)chunk * 27 + t) * J + j0 + jj) * 48);
+      o[0] = h; o[1] = h; o[2] = m; o[3] = h; o[4] = l; o[5] = m;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < E; e += 256) {
     const int k = e % CK, jj = (e / CK) % 8, t = e / (CK * 8);
     if (j0 + jj >= J) continue;

@@ -884,3 +884,31 @@ def test_conv3_pack2_equals_two_packs(cout, cin):
     torch.cuda.synchronize()
     assert torch.equal(f1.view(torch.int16), f2.view(torch.int16))
     assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))
+
+
+@pytest.mark.parametrize("flip", [0, 1])
+@pytest.mark.parametrize("cout,cin", [(64, 24), (128, 64)])
+def test_conv3_pack_x6_layout(flip, cout, cin):
+    """fp32 build (bf16x6) weight pack, bit-exact against a torch emulation of the split:
+    rows [chunk][27][J][48 bf16] = [h | h] [m | h] [l | m] over 8 k, h = rne(v), m = rne(v - h),
+    l = rne(v - h - m); dgrad packs (flip) mirror the taps and swap Cin / Cout."""
+    L = _lib()
+    code = 0
+    w = torch.randn(cout, cin, 27, device=DEV) * 0.1
+    J, K = (cin, cout) if flip else (cout, cin)
+    n = L.query("pcms_conv3_pack_elems", code, J, K)
+    out = torch.full((n,), float("nan"), device=DEV)
+    L.call("pcms_conv3_pack", code, w, out, cout, cin, flip)
+    torch.cuda.synchronize()
+    nch = -(-K // 8)
+    got = out.view(torch.int16)[: nch * 27 * J * 48].view(nch, 27, J, 48).cpu()
+    wc = w.cpu()
+    src = wc.permute(1, 0, 2).flip(2) if flip else wc  # [J][K][27]
+    src = torch.nn.functional.pad(src, (0, 0, 0, nch * 8 - K))  # zero k padding
+    v = src.view(J, nch, 8, 27).permute(1, 3, 0, 2)  # [chunk][t][J][k]
+    h = v.to(torch.bfloat16)
+    r = v - h.float()
+    m = r.to(torch.bfloat16)
+    lo = (r - m.float()).to(torch.bfloat16)
+    exp = torch.cat([h, h, m, h, lo, m], dim=3).view(torch.int16)
+    assert torch.equal(got, exp)
