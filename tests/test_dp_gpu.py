@@ -32,7 +32,7 @@ def _port():
 def _run(tmp_path, world, clip=0.0):
     out = str(tmp_path / "dp.pt")
     port = str(_port())
-    env = dict(os.environ, CLIP=str(clip))
+    env = dict(os.environ, CLIP=str(clip), PCMS_DP_STEPS="1")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "tools", "dp_worker.py"), str(r), str(world), port,
                                out], env=env) for r in range(world)]
     rcs = [p.wait(timeout=240) for p in procs]

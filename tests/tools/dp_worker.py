@@ -28,7 +28,7 @@ def main():
     tr = Trainer(cfg)
     assert tr.distributed and tr.world_size == world
     losses = []
-    for s in range(int(os.environ.get("STEPS", "1"))):
+    for s in range(int(os.environ.get("PCMS_DP_STEPS", "1"))):
         b = make_batch(2, SPATIAL, seed=step_seed(rank, s), label="bernoulli")
         losses.append(tr.step(b))
     eng = tr.model.engine()
