@@ -936,10 +936,11 @@ int pcms_convt_pack_elems(int dtype, int Cin, int Cout) {
 
 // out: skip-sized (N, Do, Ho, Wo, Cout). If the grid is larger than 2x the input the pad
 // ring is zero-filled here (F.pad semantics).
-// fp32 build: 4 M-tiles per wave where that still leaves >= 2 workgroups per CU (level-0
-// forward 1072 -> 683 us, dgrad 1172 -> 734 us; 2 M-tiles: 770 / 759 us)
+// fp32 build: 4 M-tiles per wave where that still leaves a workgroup per CU (level-0 forward
+// 1072 -> 657 us, dgrad 1172 -> 744 us, level-1 dgrad 515 -> 363 us; 2 M-tiles, or a
+// 2-workgroups-per-CU threshold, measured slower)
 constexpr int kX6MT = 4;
-static bool x6_mt4(long M, long colblocks) { return cdiv(M, 128 * kX6MT) * colblocks >= 2L * device_cus(); }
+static bool x6_mt4(long M, long colblocks) { return cdiv(M, 128 * kX6MT) * colblocks >= device_cus(); }
 
 int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bias, void* out,
                    int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
