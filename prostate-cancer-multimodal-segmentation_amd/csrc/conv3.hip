@@ -461,7 +461,7 @@ struct WgradParams {
 
 // TG: the taps are split over two workgroups per (tile, split) -- for grids of few boxes,
 // where splitting the voxels instead would add partial rows and a reduction pass
-template <typename T, int LBD, int LBH, int LBW, bool TG = false>
+template <typename T, int LBD, int LBH, int LBW, bool TG = false, bool P4 = false>
 __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p) {
   const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   typedef WTraits<T> Tr;
@@ -496,6 +496,10 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   auto tapof = [&](int j) __attribute__((always_inline)) { return tb + 8 * (j < NJ ? j : NJ); };
   const int co_base = (tile % p.nco) * 64;
   const int ci_base = (tile / p.nco) * 32;
+  // fp32 build, <= 8 input channels (the stem): the 32 MFMA columns hold 4 taps x 8 channels
+  // (column n = tap 4 wave + n / 8, channel n % 8; waves 0-6 own the 7 tap groups) instead of
+  // one tap x 32 channels of which 24 are padding -- 3.9x fewer MFMAs per box
+  constexpr bool pack4 = kX6 && P4;  // the host launches P4 for Cin <= 8 only
   const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
   const int HH = bh + 2, HW = bw + 2;
   const int HV = (bd + 2) * HH * HW;
@@ -672,6 +676,26 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         }
         const int hr0 = halo_row(v_a), hr1 = halo_row(v_a + 4);
         const int ci = g * 16 + pp * 4;
+        if constexpr (pack4) {
+          if (wave < 7) {
+            // the lane's 4 columns g 16 + pp 4 .. + 3 = tap 2 g + pp / 2 of the group, channels
+            // (pp & 1) 4 .. + 3 (tap 27 of the last group reads tap 26; its column is dropped)
+            const int tap = min(4 * wave + 2 * g + (pp >> 1), 26);
+            const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+            const int off = (kd * HH + kh) * HW + kw;
+            const int o0 = (hr0 + off) * Tr::XROW + (pp & 1) * 8, o1 = (hr1 + off) * Tr::XROW + (pp & 1) * 8;
+            const s16x8_t b1 = frag(xb, o0, o1);
+            const s16x8_t b2 = frag(xb + (hsel ? 0 : BUFBYTES), o0, o1);
+            const s16x8_t b3 = frag(xb + (hsel ? BUFBYTES : 2 * BUFBYTES), o0, o1);
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+              acc[4 * ct] = mfma(a1[ct], b1, acc[4 * ct]);
+              acc[4 * ct] = mfma(a2[ct], b2, acc[4 * ct]);
+              acc[4 * ct] = mfma(a1[ct], b3, acc[4 * ct]);
+            }
+          }
+          continue;
+        }
         const char* xb1 = xb;                                     // B1: h | h
         const char* xb2 = xb + (hsel ? 0 : BUFBYTES);            // B2: m | h
         const char* xb3 = xb + (hsel ? BUFBYTES : 2 * BUFBYTES);  // B3: l | m
@@ -886,14 +910,24 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       const int nci = min(32, p.cw - ci_base);
       for (int ct = 0; ct < 2; ++ct) {
         __syncthreads();
+        if constexpr (pack4) {
+          const int tap = 4 * wave + ((lane & 31) >> 3);
+          if (wave < 7 && tap < 27)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (!owned(j)) continue;
-          const int tap = tapof(j);
+            for (int e = 0; e < 16; ++e) {
+              const int col = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+              tile[(col * 32 + (lane & 7)) * 27 + tap] = acc[ct * 4][e];
+            }
+        } else {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int col = (e & 3) + 8 * (e >> 2) + 4 * hsel;
-            tile[(col * 32 + (lane & 31)) * 27 + tap] = acc[ct * 4 + j][e];
+          for (int j = 0; j < 4; ++j) {
+            if (!owned(j)) continue;
+            const int tap = tapof(j);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int col = (e & 3) + 8 * (e >> 2) + 4 * hsel;
+              tile[(col * 32 + (lane & 31)) * 27 + tap] = acc[ct * 4 + j][e];
+            }
           }
         }
         __syncthreads();
@@ -938,6 +972,18 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           }
         }
       }
+      return;
+    }
+    if constexpr (pack4) {
+      const int tap = 4 * wave + ((lane & 31) >> 3), ci = ci_base + (lane & 7);
+      if (wave < 7 && tap < 27 && ci < p.Cin)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int co = co_base + ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+            if (co < p.Cout) prow[((long)tap * p.Cout + co) * p.Cin + ci] = acc[ct * 4][e];
+          }
       return;
     }
 #pragma unroll
@@ -1805,8 +1851,9 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   } else {
     typedef WTraits<x6_t> X;
     lds = (size_t)X::NPART * (X::BV * X::DYROW + X::HALO * X::XROW);
-    (void)hipFuncSetAttribute((const void*)conv3_wgrad_kernel<x6_t, -1, -1, -1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((conv3_wgrad_kernel<x6_t, -1, -1, -1>), grid, dim3(kWThreads), lds, s, p);
+    auto kern = Cin <= 8 ? conv3_wgrad_kernel<x6_t, -1, -1, -1, false, true> : conv3_wgrad_kernel<x6_t, -1, -1, -1>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;

@@ -288,6 +288,7 @@ def test_conv3_fwd_big_box(N, c0, c1, cout, cy0, S, wgs):
 @pytest.mark.parametrize("dt,code,tol", CONV_DTS)
 @pytest.mark.parametrize("N,c0,c1,cout,S", [
     (2, 8, 0, 64, (16, 16, 16)),
+    (1, 8, 0, 64, (4, 4, 8)),           # stem channels, one box: the unsplit direct flush
     (1, 64, 0, 64, (9, 10, 11)),
     (2, 64, 64, 64, (8, 8, 8)),
     (2, 128, 0, 128, (4, 4, 4)),
