@@ -162,6 +162,10 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
     wg_bytes = xb + (2 if fused else 1) * yb + 64 * 5 * 27 * 4
     t = res["fwd"] + res["wgrad"]
     achieved = (fwd_bytes + wg_bytes) / t
+    # SURVEY §8(d)'s own accounting (the conv alone: X + W + Y / X + dY + dW = 578.9 MB at
+    # N=2), over the same measured time: the fused kernel reads Y as well, so this is the
+    # lower of the two fractions
+    s8d_bytes = fwd_bytes + xb + yb + 64 * 5 * 27 * 4
     # HBM bytes per fwd+wgrad pair from the PMC counters (FETCH_SIZE / WRITE_SIZE in separate
     # rocprofv3 passes, gfx950 FETCH correction: tests/kexp/pmc_stem_traffic.sh), committed
     # for the shape they were measured on; null for any other shape
@@ -178,7 +182,9 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
     return {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
             "kernel": kernel,
-            "algorithmic_bytes": fwd_bytes + wg_bytes, "t_fwd_us": round(res["fwd"] * 1e6, 1),
+            "algorithmic_bytes": fwd_bytes + wg_bytes,
+            "frac_s8d": round(s8d_bytes / t / HBM_PEAK, 4), "algorithmic_bytes_s8d": s8d_bytes,
+            "t_fwd_us": round(res["fwd"] * 1e6, 1),
             "t_wgrad_us": round(res["wgrad"] * 1e6, 1),
             "timing": "HIP events around each launch inside the timed steps" if in_step else
                       f"{reps} back-to-back launches, median of 3"}
@@ -281,9 +287,29 @@ def main():
     tr = Trainer(cfg)
     host = _pinned_batches(a.batch, spatial, rank, 2, a.zero_fill)
     tr.model.engine().kernel_timer = {}
+    dp_info = None
+    if world > 1:
+        sync = tr._grad_sync()[1]
+        sync.exposed_events = []
     ts, wall, last = timed_steps(tr, host, a.warmup, a.steps, world)
     timer = tr.model.engine().kernel_timer
     tr.model.engine().kernel_timer = None
+    if world > 1:
+        # the all-reduce time the backward did not hide: HIP events on the compute stream
+        # around GradSync.finish()'s waits, the timed steps only (the last `steps` pairs)
+        if tr._grad_sync()[1] is not sync:  # re-flattened during the warm-up: no record
+            sync.exposed_events = []
+        evs = sync.exposed_events[-a.steps:]
+        sync.exposed_events = None
+        exp = [e0.elapsed_time(e1) for e0, e1 in evs]
+        et = torch.tensor([statistics.mean(exp) if exp else 0.0, max(exp) if exp else 0.0],
+                          device="cuda", dtype=torch.float64)
+        dist.all_reduce(et, op=dist.ReduceOp.MAX)
+        dp_info = {"allreduce_ms_exposed": round(float(et[0]), 3), "allreduce_ms_exposed_max": round(float(et[1]), 3),
+                   "buckets_mb": [round((hi - lo) * 4 / 2**20, 1) for lo, hi in sync.launched],
+                   "bucket_order": "backward order (decoder first, stem last); each launched async as the backward "
+                                   "finishes its modules, the rest waited for before Adam",
+                   "grad_mb": round(tr.model.engine().flat_g.numel() * 4 / 2**20, 1)}
     in_step = {}
     for key, name in (("fwd", "stem_fwd"), ("wgrad", "stem_wgrad")):
         evs = timer.get(name, [])
@@ -331,6 +357,8 @@ def main():
                                   "back to back between a barrier + synchronize on both sides"},
             "fp32_parity_build_value": fp32,
         }
+        if dp_info is not None:
+            out["dp"] = dp_info
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

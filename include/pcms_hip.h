@@ -249,6 +249,15 @@ int pcms_adam_pack_conv3(float* p, float* g, float* m, float* v, const long long
 int pcms_adam_pack_convt(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
                          float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
                          const float* gmul, hipStream_t s);
+/* fp32 build: the same with the bf16x6 packs (pcms_conv3_pack / pcms_convt_pack dtype 0
+ * layouts); conv tiles are 32 co x 16 ci (ntiles = sum Cout / 32 x Cin / 16), ConvT tiles
+ * 32 x 32 as above.  Replaces the per-step repack of the fp32 build's weights.             */
+int pcms_adam_pack_conv3_x6(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                            float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                            const float* gmul, hipStream_t s);
+int pcms_adam_pack_convt_x6(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                            float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                            const float* gmul, hipStream_t s);
 int pcms_adam_ranges(float* p, float* g, float* m, float* v, const long long* ranges, int nranges, long max_len,
                      float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
                      const float* gmul, hipStream_t s);

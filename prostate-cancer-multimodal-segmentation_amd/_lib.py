@@ -77,6 +77,8 @@ SIGNATURES = {
     "pcms_adam": "pppplfffffffps",
     "pcms_adam_pack_conv3": "pppppiifffffffps",
     "pcms_adam_pack_convt": "pppppiifffffffps",
+    "pcms_adam_pack_conv3_x6": "pppppiifffffffps",
+    "pcms_adam_pack_convt_x6": "pppppiifffffffps",
     "pcms_adam_ranges": "pppppilfffffffps",
     "pcms_grad_clip_ws_doubles": "",
     "pcms_fill_ranges": "ppilfs",

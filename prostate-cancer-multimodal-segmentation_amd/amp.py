@@ -72,6 +72,10 @@ class GradScaler:
     def step(self, optimizer, *args, **kwargs):
         if not self.enabled:
             return optimizer.step(*args, **kwargs)
+        if all(p.grad is None for p in optimizer.model.parameters()):
+            # no backward since zero_grad(set_to_none=True): flat_g holds a previous step's
+            # values; torch's GradScaler raises here as well
+            raise AssertionError("No inf checks were recorded for this optimizer.")
         self._unscale(optimizer)
         self._found_inf = not math.isfinite(float(self._norm))  # host sync, as torch's scaler
         if self._found_inf:

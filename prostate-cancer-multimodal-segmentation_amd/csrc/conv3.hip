@@ -1242,6 +1242,70 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
   }
 }
 
+// fp32 build (bf16x6 packs): Adam + both three-part packs in one pass.  One block per (conv,
+// 32 co x 16 ci) tile (the fp32 tile, 54 KiB, fits LDS where the 32 x 32 one would not): the
+// 32 contiguous 432-float runs w[co][ci0..ci0+16][27] are updated in place as in
+// adam_pack_conv3_kernel, the new fp32 weights kept in LDS, and each packed row -- 8 k
+// values -> the B fragments [h|h] [m|h] [l|m] (split3x8, pack_conv3_kernel<x6_t>'s
+// arithmetic) -- written as six 16-B stores:
+//   fwd   [ci/8][t][co][48]   (k = ci)
+//   dgrad [co/8][t][ci][48]   (k = co, tap mirrored)
+__global__ void __launch_bounds__(256) adam_pack_conv3_x6_kernel(float* P, float* Gr, float* Mo, float* Vo,
+                                                                 const long long* tab, int ntab, AdamCoef c,
+                                                                 const float* gmul) {
+  __shared__ float tf[32][16 * 27 + 1];  // [co][ci * 27 + t], rows padded by one float
+  int ei = 0;
+  while (ei + 1 < ntab && tab[8 * (ei + 1) + 5] <= (long long)blockIdx.x) ++ei;
+  const long long* e = tab + 8 * ei;
+  const long off = (long)e[0];
+  const int Cout = (int)e[1], Cin = (int)e[2];
+  bf16_t* fwd = reinterpret_cast<bf16_t*>(e[3]);
+  bf16_t* dgr = reinterpret_cast<bf16_t*>(e[4]);
+  const int local = blockIdx.x - (int)e[5];
+  const int j0 = (local % (Cout / 32)) * 32, ci0 = (local / (Cout / 32)) * 16;
+  const float s = gmul ? c.gscale * gmul[0] : c.gscale;
+  for (int q4 = threadIdx.x; q4 < 32 * 108; q4 += 256) {  // 32 runs of 108 f32x4
+    const int run = q4 / 108, q = q4 % 108;
+    const long idx = off + ((long)(j0 + run) * Cin + ci0) * 27 + 4 * q;
+    f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(P + idx));
+    f32x4_t gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Gr + idx));
+    f32x4_t mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Mo + idx));
+    f32x4_t vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Vo + idx));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float pk = pv[k], gk = gv[k], mk = mv[k], vk = vv[k];
+      adam_update(pk, gk, mk, vk, c, s);
+      pv[k] = pk; gv[k] = gk; mv[k] = mk; vv[k] = vk;
+      tf[run][4 * q + k] = pk;
+    }
+    __builtin_nontemporal_store(pv, reinterpret_cast<f32x4_t*>(P + idx));
+    __builtin_nontemporal_store(mv, reinterpret_cast<f32x4_t*>(Mo + idx));
+    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4_t*>(Vo + idx));
+    if (s != 1.f) __builtin_nontemporal_store(gv, reinterpret_cast<f32x4_t*>(Gr + idx));
+  }
+  __syncthreads();
+  auto put = [](bf16_t* row, const float (&f)[8]) {
+    u32x4_t h, m, l;
+    split3x8(f, h, m, l);
+    u32x4_t* o = reinterpret_cast<u32x4_t*>(row);
+    o[0] = h; o[1] = h; o[2] = m; o[3] = h; o[4] = l; o[5] = m;
+  };
+  for (int r = threadIdx.x; r < 27 * 32 * 2; r += 256) {  // fwd rows (t, co, ci-chunk of 8)
+    const int cc = r & 1, co = (r >> 1) & 31, t = r >> 6;
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = tf[co][(cc * 8 + k) * 27 + t];
+    put(fwd + ((((long)(ci0 / 8 + cc)) * 27 + t) * Cout + j0 + co) * 48, f);
+  }
+  for (int r = threadIdx.x; r < 27 * 16 * 4; r += 256) {  // dgrad rows (t, ci, co-chunk of 8)
+    const int cc = r & 3, ci = (r >> 2) & 15, t = r >> 6;
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = tf[cc * 8 + k][ci * 27 + 26 - t];
+    put(dgr + ((((long)(j0 / 8 + cc)) * 27 + t) * Cin + ci0 + ci) * 48, f);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Big-box forward / dgrad (bf16; the level-0/1 hot case: D % 8 == H % 8 == 0, W % 16 == 0,
 // input channels in 16-channel chunks), PERSISTENT: one 8-wave workgroup per CU, one grid of
@@ -1669,6 +1733,17 @@ int pcms_adam_pack_conv3(float* p, float* g, float* m, float* v, const long long
   if (ntab <= 0 || ntiles <= 0) return 0;
   const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
   hipLaunchKernelGGL(adam_pack_conv3_kernel, dim3(ntiles), dim3(256), 0, s, p, g, m, v, table, ntab, c, gmul);
+  PCMS_CHECK_LAUNCH();
+}
+
+// the same for the fp32 build: both bf16x6 packs (pcms_conv3_pack dtype 0 layouts); one tile
+// per 32 co x 16 ci (ntiles = sum of Cout / 32 x Cin / 16)
+int pcms_adam_pack_conv3_x6(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                            float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                            const float* gmul, hipStream_t s) {
+  if (ntab <= 0 || ntiles <= 0) return 0;
+  const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
+  hipLaunchKernelGGL(adam_pack_conv3_x6_kernel, dim3(ntiles), dim3(256), 0, s, p, g, m, v, table, ntab, c, gmul);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -877,6 +877,63 @@ __global__ void __launch_bounds__(256) adam_pack_convt_kernel(float* P, float* G
   }
 }
 
+// fp32 build: Adam + both bf16x6 ConvTranspose3d packs (convt_pack_kernel<x6_t> layouts:
+// fwd [t][co][ci / 8][48], dgrad [ci][t][co / 8][48]).  One block per (32 ci x 32 co) tile,
+// the updated fp32 tile [ci][co][t] kept in LDS (32 KiB).
+__global__ void __launch_bounds__(256) adam_pack_convt_x6_kernel(float* P, float* Gr, float* Mo, float* Vo,
+                                                                 const long long* tab, int ntab, AdamCoef c,
+                                                                 const float* gmul) {
+  __shared__ float tf[32][257];  // [ci][co * 8 + t], rows padded by one float
+  int ei = 0;
+  while (ei + 1 < ntab && tab[8 * (ei + 1) + 5] <= (long long)blockIdx.x) ++ei;
+  const long long* e = tab + 8 * ei;
+  const long off = (long)e[0];
+  const int Cin = (int)e[1], Cout = (int)e[2];
+  bf16_t* fwd = reinterpret_cast<bf16_t*>(e[3]);
+  bf16_t* dgr = reinterpret_cast<bf16_t*>(e[4]);
+  const int local = blockIdx.x - (int)e[5];
+  const int co0 = (local % (Cout / 32)) * 32, ci0 = (local / (Cout / 32)) * 32;
+  const float s = gmul ? c.gscale * gmul[0] : c.gscale;
+  for (int i = 0; i < 8; ++i) {
+    const int q4 = threadIdx.x + i * 256, run = q4 >> 6, q = q4 & 63;
+    const long idx = off + ((long)(ci0 + run) * Cout + co0) * 8 + 4 * q;
+    f32x4_t pv = *reinterpret_cast<const f32x4_t*>(P + idx), gv = *reinterpret_cast<const f32x4_t*>(Gr + idx);
+    f32x4_t mv = *reinterpret_cast<const f32x4_t*>(Mo + idx), vv = *reinterpret_cast<const f32x4_t*>(Vo + idx);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float pk = pv[k], gk = gv[k], mk = mv[k], vk = vv[k];
+      adam_update(pk, gk, mk, vk, c, s);
+      pv[k] = pk; gv[k] = gk; mv[k] = mk; vv[k] = vk;
+      tf[run][4 * q + k] = pk;
+    }
+    *reinterpret_cast<f32x4_t*>(P + idx) = pv;
+    *reinterpret_cast<f32x4_t*>(Mo + idx) = mv;
+    *reinterpret_cast<f32x4_t*>(Vo + idx) = vv;
+    if (s != 1.f) *reinterpret_cast<f32x4_t*>(Gr + idx) = gv;
+  }
+  __syncthreads();
+  auto put = [](bf16_t* row, const float (&f)[8]) {
+    u32x4_t h, m, l;
+    split3x8(f, h, m, l);
+    u32x4_t* o = reinterpret_cast<u32x4_t*>(row);
+    o[0] = h; o[1] = h; o[2] = m; o[3] = h; o[4] = l; o[5] = m;
+  };
+  for (int k = threadIdx.x; k < 8 * 32 * 4; k += 256) {  // fwd rows (t, co, 8-ci group)
+    const int grp = k & 3, co = (k >> 2) & 31, t = k >> 7;
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = tf[grp * 8 + i][co * 8 + t];
+    put(fwd + (((long)t * Cout + co0 + co) * Cin + ci0 + grp * 8) * 6, f);
+  }
+  for (int k = threadIdx.x; k < 32 * 8 * 4; k += 256) {  // dgrad rows (ci, t, 8-co group)
+    const int grp = k & 3, t = (k >> 2) & 7, ci = k >> 5;
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = tf[ci][(grp * 8 + i) * 8 + t];
+    put(dgr + (((long)(ci0 + ci) * 8 + t) * Cout + co0 + grp * 8) * 6, f);
+  }
+}
+
 static int g_convt_stream = 1;  // the persistent forward at Cin 128 / Cout 64 (A/B switch)
 
 inline int device_cus() {
@@ -908,6 +965,16 @@ int pcms_adam_pack_convt(float* p, float* g, float* m, float* v, const long long
   if (ntab <= 0 || ntiles <= 0) return 0;
   const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
   hipLaunchKernelGGL(adam_pack_convt_kernel, dim3(ntiles), dim3(256), 0, s, p, g, m, v, table, ntab, c, gmul);
+  PCMS_CHECK_LAUNCH();
+}
+
+// the same for the fp32 build: both bf16x6 packs (pcms_convt_pack dtype 0 layouts)
+int pcms_adam_pack_convt_x6(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,
+                            float step_size, float b1, float b2, float eps, float wd, float bc2_sqrt, float gscale,
+                            const float* gmul, hipStream_t s) {
+  if (ntab <= 0 || ntiles <= 0) return 0;
+  const AdamCoef c{step_size, b1, b2, eps, wd, bc2_sqrt, gscale};
+  hipLaunchKernelGGL(adam_pack_convt_x6_kernel, dim3(ntiles), dim3(256), 0, s, p, g, m, v, table, ntab, c, gmul);
   PCMS_CHECK_LAUNCH();
 }
 

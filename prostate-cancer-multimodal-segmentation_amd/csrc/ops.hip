@@ -850,22 +850,23 @@ __global__ void __launch_bounds__(TPB, (BN && NC > 2) ? 2 : 3) head_bwd_kernel(c
 // head_bwd_kernel would have stored it) instead of being written and read back:
 // dy = k1 g + k2 xhat + k3, g = da [y sc + sh > 0] (bn_relu_bwd_apply_kernel's arithmetic).
 template <typename T, bool NT, int NC>
-__global__ void __launch_bounds__(TPB, NC > 2 ? 2 : 3) head_bn_apply_kernel(const T* y, const float* dlogits, const float* w,
+__global__ void __launch_bounds__(TPB, 2) head_bn_apply_kernel(const T* y, const float* dlogits, const float* w,
                                                             const float* scale, const float* shift,
                                                             const float* mean, const float* invstd,
                                                             const float* coef, T* dy, long nvox_per_n, int N) {
   const long total = (long)N * nvox_per_n;
   const int sub = threadIdx.x & 7;
-  // dy = k1 g + A y + B with A = k2 invstd, B = k3 - k2 invstd mean (five per-channel values
-  // held instead of seven: the seven-value form spilled at three waves per SIMD)
-  float sc[8], sh[8], k1[8], A[8], B[8], wk[NC][8];
+  // dy = k1 g + A (y - mean) + k3 with A = k2 invstd: the centred form (A y + (k3 - A mean)
+  // loses ~eps |mean| / std to cancellation when |mean| >> std); six per-channel values held
+  float sc[8], sh[8], k1[8], A[8], mu[8], k3[8], wk[NC][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = sub * 8 + j;
     sc[j] = scale[c]; sh[j] = shift[c];
     k1[j] = coef[c * 3];
     A[j] = coef[c * 3 + 1] * invstd[c];
-    B[j] = coef[c * 3 + 2] - A[j] * mean[c];
+    mu[j] = mean[c];
+    k3[j] = coef[c * 3 + 2];
 #pragma unroll
     for (int k = 0; k < NC; ++k) wk[k][j] = w[k * 64 + c];
   }
@@ -885,7 +886,7 @@ __global__ void __launch_bounds__(TPB, NC > 2 ? 2 : 3) head_bn_apply_kernel(cons
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float g = (x[j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
-      o[j] = k1[j] * g + (A[j] * x[j] + B[j]);
+      o[j] = k1[j] * g + (A[j] * (x[j] - mu[j]) + k3[j]);
     }
     head_st<T, NT>(dy + v * 64 + sub * 8, o);
   };

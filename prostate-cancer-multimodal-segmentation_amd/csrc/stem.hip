@@ -68,6 +68,46 @@ constexpr int kSDRed = kSDW + kStemSteps * 64 * 32;
 constexpr int kSDLds = kSDRed + 8 * 64 * 3 * 4;               // + stats reduction
 constexpr int kSDThr = 512;                                   // one 8-wave workgroup per CU
 
+// Output stores.  PCMS_STEM_WIDE 1 (the product): 16-B stores of whole 128-B voxel rows.  A
+// lane holds channels (2 j', 2 j' + 1) of 16 voxels per M-tile (j' = its MFMA column), so the
+// four lanes of a quad hold channels 8 k .. 8 k + 7 (k = column >> 2) of the same four
+// w-consecutive voxels of a group g; a 4 x 4 transpose inside the quad (two DPP quad_perm
+// stages, each lane selecting between its own and its partner's register) leaves lane j of
+// the quad with voxel 4 g + j's channels 8 k .. 8 k + 7: one buffer_store_dwordx4 per group
+// writes 8 whole voxel rows (1 KiB).  8 store instructions per wave and box instead of 32
+// dword stores; the same bytes to the same addresses.  0: the dword stores (A/B builds).
+#ifndef PCMS_STEM_WIDE
+#define PCMS_STEM_WIDE 1
+#endif
+
+// DPP quad_perm controls: lane j reads lane j ^ 1 / j ^ 2 of its quad
+constexpr int kDppXor1 = 0xB1;  // quad_perm [1, 0, 3, 2]
+constexpr int kDppXor2 = 0x4E;  // quad_perm [2, 3, 0, 1]
+template <int CTRL> __device__ __forceinline__ uint32_t quad_xchg(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
+}
+// d[m] of quad lane j = element (j, m) -> element (m, j): lane j ends with d[c] = old d[j] of
+// lane c.  Stage s (xor 1, then xor 2) swaps (j, m) with (j ^ s, m ^ s) where bit s of j and
+// m differ: for the register pair (m0, m1 = m0 | s), a lane with the bit clear keeps d[m0]
+// and takes its partner's d[m0] as d[m1]; with the bit set it keeps d[m1] and takes the
+// partner's d[m1] as d[m0].
+__device__ __forceinline__ void quad_transpose4(uint32_t (&d)[4], bool b0, bool b1) {
+  {
+    const uint32_t x0 = quad_xchg<kDppXor1>(d[0]), x1 = quad_xchg<kDppXor1>(d[1]);
+    const uint32_t x2 = quad_xchg<kDppXor1>(d[2]), x3 = quad_xchg<kDppXor1>(d[3]);
+    const uint32_t n0 = b0 ? x1 : d[0], n1 = b0 ? d[1] : x0;
+    const uint32_t n2 = b0 ? x3 : d[2], n3 = b0 ? d[3] : x2;
+    d[0] = n0; d[1] = n1; d[2] = n2; d[3] = n3;
+  }
+  {
+    const uint32_t x0 = quad_xchg<kDppXor2>(d[0]), x1 = quad_xchg<kDppXor2>(d[1]);
+    const uint32_t x2 = quad_xchg<kDppXor2>(d[2]), x3 = quad_xchg<kDppXor2>(d[3]);
+    const uint32_t n0 = b1 ? x2 : d[0], n2 = b1 ? d[2] : x0;
+    const uint32_t n1 = b1 ? x3 : d[1], n3 = b1 ? d[3] : x1;
+    d[0] = n0; d[1] = n1; d[2] = n2; d[3] = n3;
+  }
+}
+
 // RELU: eval mode with the BatchNorm folded into the weights / bias (the output is the ReLU
 // activation; no statistics)
 template <int LBD, int LBH, bool RELU>
@@ -123,6 +163,11 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   const uint32_t vb0 = r_lane * 4, vb1 = r_lane * 4 + (uint32_t)W * 128;
   const uint32_t vA = hsel ? vb1 : vb0;  // g = 0, 3
   const uint32_t vB = hsel ? vb0 : vb1;  // g = 1, 2
+  // wide stores: quad lane j writes voxel 4 g + j (w), channels 8 k .. (k = r_lane >> 2)
+  const uint32_t wb0 = (r_lane & 3) * 128 + (r_lane >> 2) * 16, wb1 = wb0 + (uint32_t)W * 128;
+  const uint32_t wA = hsel ? wb1 : wb0, wB = hsel ? wb0 : wb1;
+  const bool qb0 = r_lane & 1, qb1 = (r_lane >> 1) & 1;
+  uint32_t qd[4];  // the packed channel pairs of the group being assembled
 
   auto origin = [&](int b, int& n, int& d0, int& h0, int& w0) {
     const int nbw = p.nbw, nbh = p.nbh, nbd = p.nbd;
@@ -176,8 +221,17 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   auto item_full = [&](f32x16_t (&acc)[2][2], int mt, int e, const uint32_t (&so)[2]) {
     const int g = e >> 2, rw = 4 * g + (e & 3);
     const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
-    __builtin_amdgcn_raw_buffer_store_b32(RELU ? pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f)) : pack_bf16x2(v0, v1), yr,
-                                          (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 2);
+    const uint32_t pk = RELU ? pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f)) : pack_bf16x2(v0, v1);
+    if constexpr (PCMS_STEM_WIDE) {
+      qd[e & 3] = pk;
+      if ((e & 3) == 3) {  // the group's four voxels are packed: transpose, one 16-B store
+        quad_transpose4(qd, qb0, qb1);
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4_t){qd[0], qd[1], qd[2], qd[3]}, yr,
+                                               (g == 1 || g == 2) ? wB : wA, so[mt] + 4 * g * 128, 2);
+      }
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(pk, yr, (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 2);
+    }
     const float e0 = v0 - K[0], e1 = v1 - K[1];
     s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
     s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
@@ -216,7 +270,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
     }
   };
 
-  // Every wave defers a box's epilogue to the next box: its 32 stores and BN sums are spread
+  // Every wave defers a box's epilogue to the next box: its 8 (wide) / 32 stores and BN sums are spread
   // over that box's 14 MFMA steps (3 items per step for steps 0-3, 2 after), so each SIMD's
   // store stream runs under the MFMAs instead of in bursts between them.
   f32x16_t prev[2][2];
@@ -289,8 +343,17 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
 #pragma unroll
           for (int q = qa; q < qb; ++q) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);  // pack + BN sums
-            __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // 1 store
+            if constexpr (PCMS_STEM_WIDE) {
+              if ((q & 3) == 3) {
+                __builtin_amdgcn_sched_group_barrier(0x002, 7 + 16, 0);  // pack + BN sums + transpose
+                __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);       // 1 store (8 rows)
+              } else {
+                __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);       // pack + BN sums
+              }
+            } else {
+              __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);  // pack + BN sums
+              __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // 1 store
+            }
           }
           if (st < 4) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 4 - 3 items
           else __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         // 4 - 2 items
@@ -320,6 +383,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
     // the next halo's DMA was issued before the 32 stores of the owed epilogue (none in the
     // first iteration)
     if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (PCMS_STEM_WIDE) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     STEM_STAMP(5);
   }

@@ -71,6 +71,9 @@ class GradSync:
         self._hi: Optional[int] = None
         self._next_hi = flat_g.numel()   # the next ready range must end here
         self.launched: List[Tuple[int, int]] = []   # buckets of the current step (tests / logs)
+        # bench.py under world > 1: HIP events on the compute stream around finish()'s waits
+        # (the all-reduce time the backward did not hide), one (start, end) pair per step
+        self.exposed_events: Optional[List] = None
 
     def reset(self):
         """Drop the state of a step whose backward stopped part-way (an exception between
@@ -120,8 +123,15 @@ class GradSync:
             self._lo = 0
             self._next_hi = 0
         self._launch()
+        ev = None
+        if self.exposed_events is not None and self.flat_g.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for w in self._works:
             w.wait()
+        if ev is not None:
+            ev[1].record()
+            self.exposed_events.append(ev)
         self._works = []
         self._next_hi = self.flat_g.numel()
         return 1.0 / self.world

@@ -137,6 +137,10 @@ class UNetEngine:
         self._eval = None      # {conv index: (fwd pack, folded bias)}, "stem": stem pack
         self._eval_key = None
         self._bn_epoch = 0     # training forwards so far (each moves the running statistics)
+        # weight generation: bumped by every change of the master weights the storage version
+        # counter does not see (the fused Adam writes flat_p through the C-ABI), by
+        # re-flattening and by a change of conv arithmetic; part of the eval-pack key
+        self._wgen = 0
         self._store_ranges = None  # (stem_sup, fill plan) of _store_plan
         self._gstore = False       # this backward writes conv weight gradients (PCMS_GRAD_STORE)
         self._flatten()
@@ -155,6 +159,8 @@ class UNetEngine:
                 cs.code = code
                 cs.fwd = cs.dgrad = None
         self._dirty = True
+        self._wgen += 1
+        self._adam_plan = None  # its table holds the old packs' pointers
         self._eval = None
         self.buf_key = None
 
@@ -192,7 +198,9 @@ class UNetEngine:
         self.flat_p, self.flat_g, self.flat_bn = flat, gflat, bflat
         self._flat_ptrs = [p.data_ptr() for p in params]
         self._dirty = True
+        self._wgen = getattr(self, "_wgen", 0) + 1
         self._adam_plan = None
+        self._store_ranges = None  # offsets into the new flat buffer
         self.grad_ranges = module_grad_ranges(self.model)
 
     @contextlib.contextmanager
@@ -301,17 +309,18 @@ class UNetEngine:
         """The master weights changed.  ``packs_fresh``: the fused Adam (adam_plan) already
         wrote the conv and ConvT packs from the new weights; only the stem's remain."""
         self._dirty = True
+        self._wgen += 1
         self._packs_fresh = packs_fresh and self._packed_version == self.flat_p._version
 
     def adam_plan(self):
-        """Fused Adam + weight-pack plan of the bf16 build (FlatAdam.step): device tables of
-        the conv / ConvT weights whose packs the Adam kernels write (int64 rows, see
-        include/pcms_hip.h pcms_adam_pack_conv3) and the [begin, end) ranges of every other
-        parameter.  None for the fp32 build."""
-        if self.code != BF16:
-            return None
+        """Fused Adam + weight-pack plan (FlatAdam.step): device tables of the conv / ConvT
+        weights whose packs the Adam kernels write (int64 rows, see include/pcms_hip.h
+        pcms_adam_pack_conv3) and the [begin, end) ranges of every other parameter.  The bf16
+        build writes bf16 packs; the fp32 build (``"x6"``: True) its bf16x6 packs, for the
+        convs in bf16x6 mode (a conv switched to bf16x3 is repacked as before)."""
         if self._adam_plan is not None:
             return self._adam_plan
+        x6 = self.code != BF16
         self._ensure_packs()
         base = self.flat_p.data_ptr()
 
@@ -325,11 +334,11 @@ class UNetEngine:
             w = cs.mod.weight
             if i == 0:
                 continue
-            if cs.cin % 32 or cs.cout % 32 or offset(w) % 4:
+            if cs.cin % 32 or cs.cout % 32 or offset(w) % 4 or (x6 and cs.code != F32):
                 skipped += 1
                 continue
             conv_rows.append([offset(w), cs.cout, cs.cin, cs.fwd.data_ptr(), cs.dgrad.data_ptr(), tiles, 0, 0])
-            tiles += (cs.cout // 32) * (cs.cin // 32)
+            tiles += (cs.cout // 32) * (cs.cin // (16 if x6 else 32))
             fused.append((offset(w), w.numel()))
         ct_rows, ct_tiles = [], 0
         for i, up in enumerate(self.ups):
@@ -361,6 +370,7 @@ class UNetEngine:
             # every conv / ConvT pack but the stem's comes out of the Adam pass (else the step
             # must not mark the packs fresh: a skipped layer would train on stale packs)
             "complete": skipped == 0,
+            "x6": x6,
         }
         return self._adam_plan
 
@@ -414,7 +424,7 @@ class UNetEngine:
         per conv (pcms_bn_fold, then the forward pack of w'); rebuilt when the parameters or
         the running statistics changed."""
         self._ensure_packs()
-        key = (self.flat_p._version, self._packed_version, self.flat_bn._version, self._bn_epoch)
+        key = (self._wgen, self.flat_p._version, self.flat_bn._version, self._bn_epoch)
         if self._eval is not None and self._eval_key == key:
             return
         if self._eval is None:

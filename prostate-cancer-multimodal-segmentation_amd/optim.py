@@ -30,7 +30,7 @@ class FlatAdam(torch.optim.Optimizer):
         # clip coefficient / AMP unscale), both folded into the single Adam pass
         self.grad_scale = 1.0
         self.grad_mul = None
-        self.fused_packs = True  # bf16 build: Adam writes the conv / ConvT packs (engine.adam_plan)
+        self.fused_packs = True  # Adam writes the conv / ConvT packs (engine.adam_plan; both builds)
         self._m = None
         self._v = None
 
@@ -63,8 +63,10 @@ class FlatAdam(torch.optim.Optimizer):
         if plan is not None:
             # bf16 build: the conv / ConvT weight packs come out of the Adam pass itself
             P = (eng.flat_p, eng.flat_g, m, v)
-            call("pcms_adam_pack_conv3", *P, plan["conv"], plan["nconv"], plan["conv_tiles"], *coef, self.grad_mul)
-            call("pcms_adam_pack_convt", *P, plan["convt"], plan["nconvt"], plan["convt_tiles"], *coef,
+            sfx = "_x6" if plan["x6"] else ""  # fp32 build: the bf16x6 packs
+            call("pcms_adam_pack_conv3" + sfx, *P, plan["conv"], plan["nconv"], plan["conv_tiles"], *coef,
+                 self.grad_mul)
+            call("pcms_adam_pack_convt" + sfx, *P, plan["convt"], plan["nconvt"], plan["convt_tiles"], *coef,
                  self.grad_mul)
             call("pcms_adam_ranges", *P, plan["ranges"], plan["nranges"], plan["max_len"], *coef, self.grad_mul)
         else:

@@ -237,9 +237,13 @@ class BaseTrainer:
             total, n = float(t[0]), int(t[1])
         return total / max(n, 1)
 
-    def save_checkpoint(self, epoch, loss, is_best=False, best_loss=None, patience=None):
+    def save_checkpoint(self, epoch, loss, is_best=False, best_loss=None, patience=None,
+                        filename="latest_checkpoint.pth"):
         """utils/trainer.py:236-278 (same dict keys and file names; ``best_loss`` /
-        ``patience`` are extra keys so a resumed ``train`` continues its early stopping)."""
+        ``patience`` are extra keys so a resumed ``train`` continues its early stopping).
+        ``train`` writes ``latest_checkpoint.pth`` on improvement only, as the reference
+        (:325-334), so that file always holds the best model and loss; the per-epoch resume
+        state goes to ``filename="resume_checkpoint.pth"``."""
         if self.rank != 0:
             return
         ckpt = {"epoch": epoch, "model_state_dict": self.model.state_dict(),
@@ -249,7 +253,7 @@ class BaseTrainer:
             ckpt["best_loss"], ckpt["patience"] = float(best_loss), int(patience or 0)
         if self.scaler is not None:
             ckpt["scaler_state_dict"] = self.scaler.state_dict()
-        torch.save(ckpt, os.path.join(self.config["save_dir"], "latest_checkpoint.pth"))
+        torch.save(ckpt, os.path.join(self.config["save_dir"], filename))
         if is_best:
             torch.save(self.model.state_dict(),
                        os.path.join(self.config["save_dir"], f"best_model_epoch_{epoch}.pth"))
@@ -300,16 +304,17 @@ class BaseTrainer:
             val_loss = self.validate_epoch()  # already the full-set value on every rank
             cur = val_loss if val_loss is not None else train_loss
             self.scheduler.step(cur)
-            if cur < best:
+            improved = cur < best
+            if improved:
                 best, patience = cur, 0
-                if self.config.get("save_dir"):
-                    self.save_checkpoint(epoch + 1, cur, is_best=True, best_loss=best, patience=patience)
             else:
                 patience += 1
-                if self.config.get("save_dir"):
-                    # latest_checkpoint.pth every epoch (the reference writes it on improvement
-                    # only): a resumed train() continues from this epoch with this patience
-                    self.save_checkpoint(epoch + 1, cur, best_loss=best, patience=patience)
+            if self.config.get("save_dir"):
+                if improved:  # the reference's latest_checkpoint.pth (best model) + best_model_epoch_{e}.pth
+                    self.save_checkpoint(epoch + 1, cur, is_best=True, best_loss=best, patience=patience)
+                # every epoch: the state a resumed train() continues from (this epoch, this patience)
+                self.save_checkpoint(epoch + 1, cur, best_loss=best, patience=patience,
+                                     filename="resume_checkpoint.pth")
             if patience >= 20:
                 break
         self._resume = (best, patience)

@@ -18,6 +18,9 @@
 //   1024 MFMA operands all zero (lower power: tells clock effects from pipeline conflicts)
 //   2048 wave specialisation: the two waves of SIMD 3 issue every piece and run no MFMAs
 //   4096 16 waves (1024 threads) share the pieces and the MFMAs (half the MFMAs per wave)
+//   8192 channel-blocked x: the halo read from a [N][C/32][D][H][W][32] layout (the same
+//        bytes; a halo W-row of 10 voxels is one contiguous 640-B run = 5 whole lines,
+//        instead of 10 half lines of 128-B voxel rows)
 // Built by tests/kexp/Makefile (libdmaprobe.so), driven by tests/kexp/dma_probe.py.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -40,6 +43,7 @@ __global__ void __launch_bounds__((F & 4096) ? 1024 : 512, 1) probe_kernel(const
   constexpr bool kDepth2 = F & 1, kReg = F & 2, kL2 = F & 4, kWide = F & 8, kDyOnly = F & 16, kXOnly = F & 32;
   constexpr int kT = (F & 4096) ? 1024 : 512;
   constexpr bool kMfma = F & 64, kLdsRd = F & 128, kNoStage = F & 256, kInter = F & 512, kZero = F & 1024, kSpec = F & 2048;
+  constexpr bool kBlocked = F & 8192;
   constexpr int XROWB = kWide ? 128 : 64;
   constexpr int XP = kHalo * XROWB / 16;
   constexpr int NP = (kXOnly ? 0 : kDyP) + (kDyOnly ? 0 : XP);
@@ -86,8 +90,12 @@ __global__ void __launch_bounds__((F & 4096) ? 1024 : 512, 1) probe_kernel(const
         const int hv = hp / (XROWB / 16), qq = hp % (XROWB / 16);
         const int hw_ = hv % 10, t_ = hv / 10, hh_ = t_ % 10, hd_ = t_ / 10;
         const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
-        if (hv < kHalo && gd >= 0 && gd < D && gh >= 0 && gh < H && gw >= 0 && gw < W)
-          voff = (uint32_t)(((((n * D + gd) * H + gh) * W + gw) * 64 + (kWide ? 0 : half * 32) + qq * 8) * 2);
+        if (hv < kHalo && gd >= 0 && gd < D && gh >= 0 && gh < H && gw >= 0 && gw < W) {
+          if constexpr (kBlocked)
+            voff = (uint32_t)((((((n * 2 + half) * D + gd) * H + gh) * W + gw) * 32 + qq * 8) * 2);
+          else
+            voff = (uint32_t)(((((n * D + gd) * H + gh) * W + gw) * 64 + (kWide ? 0 : half * 32) + qq * 8) * 2);
+        }
       }
       if constexpr (kReg) {
         v[i] = (isdy ? __builtin_amdgcn_raw_buffer_load_b128(dr2, voff, 0, 0) : __builtin_amdgcn_raw_buffer_load_b128(xr2, voff, 0, 0));
@@ -194,6 +202,7 @@ extern "C" int probe_run(int flags, const void* x, const void* dy, int N, int D,
   switch (flags) {
     PROBE(0) PROBE(1) PROBE(2) PROBE(3) PROBE(4) PROBE(5) PROBE(8) PROBE(9) PROBE(16) PROBE(17) PROBE(32) PROBE(33)
     PROBE(20) PROBE(36) PROBE(64) PROBE(128) PROBE(192) PROBE(320) PROBE(384) PROBE(448) PROBE(576) PROBE(704) PROBE(66) PROBE(194) PROBE(1088) PROBE(1344) PROBE(1600) PROBE(2048) PROBE(2112) PROBE(2240) PROBE(2368) PROBE(2496) PROBE(4096) PROBE(4160) PROBE(4416) PROBE(4544) PROBE(4288)
+    PROBE(8192) PROBE(8193) PROBE(8224) PROBE(8228) PROBE(8256) PROBE(8384)
     default: return -1;
   }
 #undef PROBE

@@ -20,7 +20,10 @@ NAMES = {0: "product shape, 1 box in flight", 1: "2 boxes in flight", 2: "regist
          2048: "SIMD-3 waves stage (no MFMAs)", 2112: "SIMD-3 stages, SIMDs 0-2 MFMA",
          2368: "SIMDs 0-2 MFMA alone", 2496: "SIMDs 0-2 LDS-fed MFMA alone", 2240: "SIMD-3 stages, 0-2 LDS-fed MFMA",
          4096: "16 waves stage", 4160: "16 waves: staging + MFMA phase", 4416: "16 waves: MFMA phase alone",
-         4544: "16 waves: LDS-fed MFMA alone", 4288: "16 waves: staging + LDS-fed MFMA"}
+         4544: "16 waves: LDS-fed MFMA alone", 4288: "16 waves: staging + LDS-fed MFMA",
+         8192: "blocked x: staging", 8193: "blocked x: 2 in flight", 8224: "blocked x: halo only",
+         8228: "blocked x: halo only, L2-resident", 8256: "blocked x: staging + MFMA phase",
+         8384: "blocked x: staging + LDS-fed MFMAs"}
 
 
 def main():

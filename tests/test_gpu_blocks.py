@@ -175,6 +175,43 @@ def test_eval_bn_folding(precision):
             assert e_f <= 2 * e_u + 1e-2, (step, e_f, e_u)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_eval_packs_follow_optimizer_step(precision):
+    """train forward -> backward -> eval -> opt.step() -> eval: the second eval must see the
+    stepped weights (the fused Adam writes the master weights through the C-ABI, so the
+    storage version counter alone cannot key the folded eval packs)."""
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    torch.manual_seed(5)
+    m = UNet3D(n_modalities=5, n_classes=1, precision=precision).cuda()
+    x = torch.rand(2, 5, 32, 32, 16)
+    y = (torch.rand(2, 1, 32, 32, 16) < 0.4).float()
+    opt = FlatAdam(m, lr=1e-2, weight_decay=1e-5)
+    m.train()
+    opt.zero_grad()
+    BCEDiceLoss()(m(x.cuda()), y.cuda()).backward()
+    m.eval()
+    with torch.no_grad():
+        before = m(x.cuda()).cpu()
+    opt.step()
+    eng = m.engine()
+    with torch.no_grad():
+        after = m(x.cuda()).cpu()
+        eng.fold_bn_eval = False
+        unfolded = m(x.cuda()).cpu()
+        eng.fold_bn_eval = True
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    lr = ref.forward(sd, x, training=False)
+    assert float((after - before).abs().max()) > 0, "eval reused the pre-step folded weights"
+    if precision == "fp32":
+        assert float((after - lr).abs().max()) <= ATOL
+    else:
+        e_f, e_u = float((after - lr).abs().max()), float((unfolded - lr).abs().max())
+        assert e_f <= 2 * e_u + 1e-2, (e_f, e_u)
+
+
 def test_predictor_pipeline(tmp_path):
     from pcms_amd.data import read_nifti, read_nifti_header, write_nifti
     from pcms_amd.predict import MODALITIES, ModelPredictor, load_multimodal_images, preprocess_image

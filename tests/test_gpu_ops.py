@@ -628,20 +628,21 @@ def test_head(dt, code, tol, ncls):
     close(db.cpu(), br.grad, 1e-5, "head bias grad")
 
 
-@pytest.mark.parametrize("dt,code,tol", DTS)
+@pytest.mark.parametrize("dt,code,tol,shift", [d + (0.3,) for d in DTS] + [DTS[0] + (100.0,)])
 @pytest.mark.parametrize("ncls", [1, 2])
-def test_head_bn_fused(dt, code, tol, ncls):
+def test_head_bn_fused(dt, code, tol, shift, ncls):
     """The last decoder block's BN + ReLU fused into the head (pcms_head_bn_fwd / _bwd) vs
     the unfused sequence (pcms_bn_relu -> pcms_head_fwd; pcms_head_bwd -> pcms_bn_relu_bwd):
     bit-identical logits and head weight / bias gradients, the BatchNorm gradients and dy
     equal up to the BN partial sums' order; and both against fp64 autograd of
-    relu(batch_norm(y)) -> conv1x1."""
+    relu(batch_norm(y)) -> conv1x1.  ``shift`` 100 (fp32): |mean| / std = 50, where an
+    uncentred apply (A y + B) loses ~eps |mean| / std to cancellation."""
     L = _lib()
     g = torch.Generator().manual_seed(4)
     N, S, C = 2, (6, 5, 8), 64
     V = S[0] * S[1] * S[2]
     nvox = N * V
-    y = (torch.randn(N, C, *S, generator=g) * 2 + 0.3).to(dt)
+    y = (torch.randn(N, C, *S, generator=g) * 2 + shift).to(dt)
     gamma = torch.rand(C, generator=g) + 0.5
     beta = torch.randn(C, generator=g) * 0.1
     w = torch.randn(ncls, 64, 1, 1, 1, generator=g) * 0.1

@@ -154,11 +154,13 @@ def test_grad_scaler_step_skip_and_scale_update():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("gscale", [1.0, 0.5])
-def test_fused_adam_packs_match_flat_adam(gscale):
-    """bf16 build: the fused Adam (pcms_adam_pack_conv3 / _convt / _ranges, engine.adam_plan)
-    matches the flat Adam kernel (same per-element arithmetic; the compiler may contract it
-    differently, so to 1e-6 relative), and the conv / ConvT weight packs it writes are
-    bit-identical to the pack kernels run on the updated master."""
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_fused_adam_packs_match_flat_adam(gscale, precision):
+    """The fused Adam (pcms_adam_pack_conv3 / _convt / _ranges, engine.adam_plan; the fp32
+    build's _x6 forms write the bf16x6 packs) matches the flat Adam kernel (same per-element
+    arithmetic; the compiler may contract it differently, so to 1e-6 relative), and the conv /
+    ConvT weight packs it writes are bit-identical to the pack kernels run on the updated
+    master."""
     from pcms_amd.models.unet3d import UNet3D
     from pcms_amd.optim import FlatAdam
     from pcms_amd.utils.losses import BCEDiceLoss
@@ -168,7 +170,7 @@ def test_fused_adam_packs_match_flat_adam(gscale):
     runs = []
     for fused in (False, True):
         torch.manual_seed(0)
-        m = UNet3D(n_modalities=5, n_classes=1).cuda()
+        m = UNet3D(n_modalities=5, n_classes=1, precision=precision).cuda()
         opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
         opt.fused_packs = fused
         opt.zero_grad()
@@ -181,7 +183,8 @@ def test_fused_adam_packs_match_flat_adam(gscale):
         runs.append((eng, opt))
     (e0, o0), (e1, o1) = runs
     plan = e1.adam_plan()
-    assert plan["nconv"] == 17 and plan["nconvt"] == 4
+    assert plan["nconv"] == 17 and plan["nconvt"] == 4 and plan["complete"]
+    assert plan["x6"] == (precision == "fp32")
     for a, b in ((e0.flat_p, e1.flat_p), (e0.flat_g, e1.flat_g), (o0._m, o1._m), (o0._v, o1._v)):
         torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-12)
     packs = [t.clone() for cs in e1.convs for t in (cs.fwd, cs.dgrad) if t is not None]
