@@ -119,7 +119,7 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
 
     def fwd(s):
         if sup & 1:
-            L.call("pcms_stem_fwd", s[0], eng.stem_pack, cs.mod.bias, s[1], stats, N, D, H, W, 0)
+            L.call("pcms_stem_fwd", s[0], eng.stem_pack, cs.mod.bias, s[1], stats, N, D, H, W, eng.stem_dense)
         else:
             L.call("pcms_conv3_fwd", code, s[0], eng.cp, None, 0, cs.fwd, cs.mod.bias, s[1], None, 64, None,
                    stats, 0, N, D, H, W, 64, 1)
@@ -170,10 +170,11 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
     # rocprofv3 passes, gfx950 FETCH correction: tests/kexp/pmc_stem_traffic.sh), committed
     # for the shape they were measured on; null for any other shape
     traffic = None
-    kernel = ("stem conv3d 5->64 fwd + wgrad with the BN0 backward apply fused in (stem_fwd_direct_kernel + "
+    fk = "stem_fwd_direct_kernel<DENSE>" if eng.stem_dense else "stem_fwd_direct_kernel"
+    kernel = (f"stem conv3d 5->64 fwd + wgrad with the BN0 backward apply fused in ({fk} + "
               "stem_wgrad_stream_kernel<BN>)" if fused else
-              "stem conv3d 5->64 fwd + wgrad (stem_fwd_direct_kernel + stem_wgrad_stream_kernel)")
-    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3_stem_traffic.json")
+              f"stem conv3d 5->64 fwd + wgrad ({fk} + stem_wgrad_stream_kernel)")
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r4_stem_traffic.json")
     if os.path.exists(tf):
         with open(tf) as f:
             rec = json.load(f)

@@ -31,6 +31,9 @@ extern "C" {
 /* gradient writer flags (pcms_conv3_wgrad): STORE writes dw instead of adding into it -- the
  * first writer after zero_grad(set_to_none=True), so the gradient needs no zero fill       */
 #define PCMS_GRAD_STORE 1
+/* pcms_stem_fwd flag: the K-dense kernel (9 tap rows x 16 instead of 14 tap pairs x 16; the
+ * pack's second form, valid for weights with cin_w <= 5)                                   */
+#define PCMS_STEM_DENSE 16
 
 /* ---- layout ---------------------------------------------------------------------- */
 /* batch['image'] (N, Cin, D, H, W) fp32 NCDHW -> NDHWC, channels zero-padded to Cp.
@@ -75,6 +78,14 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
                    float* yacc, float* stats, int flags,
                    int N, int D, int H, int W, int Cout, int splits, hipStream_t s);
+/* The conv of relu(x * isc + ish) (per input channel): the BatchNorm + ReLU of the layer
+ * below (models/unet3d.py:31-35, bn -> relu -> conv) applied to the staged halo in LDS
+ * instead of a separate HBM pass.  bf16, one source of <= 128 channels, the big-box shapes
+ * (-5 otherwise); no split, no flags.  Measured against pcms_bn_relu + pcms_conv3_fwd in
+ * DESIGN.md §0b (tests/tools/bnin_ab.py).                                                 */
+int pcms_conv3_fwd_bnin(int dtype, const void* x, int cin, const float* isc, const float* ish, const void* wpack,
+                        const float* bias, void* y, float* stats, int N, int D, int H, int W, int Cout,
+                        hipStream_t s);
 /* dw [Cout][cin_w][27] fp32 += sum_v dy[v, co] * x[v + tap, ci] (ci < cin_w <= c0 + c1;
  * flags PCMS_GRAD_STORE: dw = ...);
  * dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (one partial row per voxel split,
@@ -87,7 +98,9 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, int flags, hipStream_t s);
 /* Stem (inc.conv.0, bf16 build): input stored with 8 channels (n_modalities <= 8).
- * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32).
+ * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32), or, with
+ * PCMS_STEM_DENSE (cin_w <= 5), one (kd, kh) tap row of 3 kw x 5 channels per k-step (9 x 16);
+ * pcms_stem_pack writes both forms.
  * pcms_stem_supported: bit 0 = pcms_stem_fwd runs this shape, bit 1 = pcms_stem_wgrad
  * does (other shapes: the general pcms_conv3_fwd / pcms_conv3_wgrad).                   */
 int pcms_stem_supported(int N, int D, int H, int W);

@@ -28,6 +28,7 @@ SIGNATURES = {
     "pcms_conv3_pack2": "ipppiis",
     "pcms_conv3_splits": "iii",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
+    "pcms_conv3_fwd_bnin": "ipippppppiiiiiis",
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiiis",
     "pcms_conv3_wgrad_tg_maxbox": "i",

@@ -24,6 +24,8 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 enum { PCMS_F32 = 0, PCMS_BF16 = 1, PCMS_F32X3 = 2 };
 // conv epilogue flags (pcms_conv3_fwd, pcms_split_epilogue, pcms_stem_fwd)
 enum { PCMS_CONV_ACCUMULATE = 1, PCMS_CONV_RELU = 2 };
+// pcms_stem_fwd: the K-dense kernel (the pack's second form; weights with <= 5 input channels)
+enum { PCMS_STEM_DENSE = 16 };
 // gradient writer flags (pcms_conv3_wgrad): store instead of accumulating
 enum { PCMS_GRAD_STORE = 1 };
 

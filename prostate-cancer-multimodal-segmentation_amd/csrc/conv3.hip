@@ -1371,6 +1371,13 @@ template <int P, int Dist> constexpr int bg_wait(int t) {
 }
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// BNIN (pcms_conv3_fwd_bnin, single-source inputs of <= kBgBnMax channels): the input is
+// relu(x * isc + ish) -- the previous BatchNorm + ReLU applied in the staging path instead of
+// a separate HBM pass.  At a chunk's end each thread rewrites the pieces it staged for the
+// next chunk in LDS (their DMA has landed by the chunk-end vmcnt wait; out-of-range pieces,
+// the zero padding, are left zero), before the barrier that publishes the buffer.
+constexpr int kBgBnMax = 128;
+template <bool BNIN = false>
 __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Params p, uint32_t x0bytes,
                                                                      uint32_t x1bytes) {
   constexpr int MT = kBgMT;
@@ -1422,7 +1429,35 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     const uint32_t lb = __builtin_amdgcn_readfirstlane(
         dummy ? lds0 + 2 * kBgBuf : lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
     dma16(first ? xr0 : xr1, lb, dummy ? kOOB : voff, 0);
+    // BNIN: bit j = a real piece; bit 8 + j = its logical channel half
+    return (!dummy && voff != kOOB ? 1u << j : 0u) | ((uint32_t)((pc & 1) ^ ((hw_ >> 3) & 1)) << (8 + j));
   };
+  // BNIN: the staged pieces of buffer `buf` (chunk `chunk`) -> relu(x sc + sh) in place
+  float* bnt = reinterpret_cast<float*>(lds + 2 * kBgBuf + kBgDummy + 4 * kBgStage + 4 * 64 * 3 * 4 + 64 * 4);
+  auto bn_apply = [&](int buf, int chunk, uint32_t pm) {
+#pragma unroll
+    for (int j = 0; j < kBgPieces; ++j) {
+      if (!((pm >> j) & 1)) continue;
+      const int pc = tid + j * kBgThreads;
+      u32x4_t* q = reinterpret_cast<u32x4_t*>(lds + buf * kBgBuf + pc * 16);
+      const int c = chunk * 16 + ((pm >> (8 + j)) & 1) * 8;
+      const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(bnt + c), s1 = *reinterpret_cast<const f32x4_t*>(bnt + c + 4);
+      const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(bnt + kBgBnMax + c);
+      const f32x4_t h1 = *reinterpret_cast<const f32x4_t*>(bnt + kBgBnMax + c + 4);
+      const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      u32x4_t v = *q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        v[i] = pack_bf16x2(bn_relu1(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]),
+                           bn_relu1(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]));
+      *q = v;
+    }
+  };
+  if constexpr (BNIN) {
+    if (tid < p.Cin) { bnt[tid] = p.isc[tid]; bnt[kBgBnMax + tid] = p.ish[tid]; }
+    __syncthreads();
+  }
 
   // A fragment byte offsets in a halo buffer: MFMA row r = 256 wave + 32 mt + perm32(lane)
   // is box voxel (2 wave + mt / 4, 2 (mt % 4) + prow / 16, prow % 16).  The half swizzle
@@ -1471,11 +1506,13 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   // 64 -> 64; no effect with 8+ chunks, so not applied there).
   if (nchunk <= 4)
     for (int i = 0; i < 2 * (slot & 3); ++i) __builtin_amdgcn_s_sleep(127);
+  uint32_t pmask = 0;  // BNIN: the pieces staged for the next chunk (stage_piece bits)
 #pragma unroll
-  for (int j = 0; j < kBgPieces; ++j) stage_piece(n, d0, h0, w0, 0, 0, j, true);
+  for (int j = 0; j < kBgPieces; ++j) pmask |= stage_piece(n, d0, h0, w0, 0, 0, j, true);
 #pragma unroll
   for (int t = 0; t < kBgDist; ++t) load_b(bset[t], 0, t, (uint32_t)((co_base + 2 * r_lane + nt) * 64 + hsel * 16));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (BNIN) bn_apply(0, 0, pmask);
   __syncthreads();
   int buf = 0;
   while (true) {
@@ -1521,7 +1558,10 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
         constexpr int tn = tap + kBgDist;
         if constexpr (tn < 27) load_b(bset[tn % (kBgDist + 1)], chunk, tn, boff);
         else load_b(bset[tn % (kBgDist + 1)], schunk, tn - 27, boff);
-        if constexpr (tap < kBgPieces) stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, tap, live);
+        if constexpr (tap < kBgPieces) {
+          const uint32_t bits = stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, tap, live);
+          if constexpr (BNIN) pmask = (tap == 0 ? 0u : pmask) | bits;
+        }
         s16x8_t& b = bset[tap % (kBgDist + 1)];
         constexpr int extra = (Slack && tap < kBgDist) ? kBgEpiStores : 0;
         vm_wait1<bg_wait<kBgPieces, kBgDist>(tap) + extra>(b);
@@ -1538,6 +1578,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
       // must hold landed data by then (costs one L2 round trip per box).
       if (!last) vm_wait<27 - kBgPieces>();
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (BNIN) bn_apply(buf ^ 1, schunk, pmask);
       __syncthreads();
       buf ^= 1;
     };
@@ -1775,10 +1816,35 @@ int pcms_conv3_splits(int dtype, int Cin, int splits) {
 // partial sums into its own slab of yacc [splits][N*D*H*W][Cout] (plain stores, no zeroing
 // needed); pcms_split_epilogue then sums the slabs in split order (deterministic), adds the
 // bias, converts, and forms the BN statistics.
+static int conv3_fwd_any(int dtype, const void* x0, int c0, const void* x1, int c1, const float* isc,
+                         const float* ish, const void* wpack, const float* bias, void* y0, void* y1, int cy0,
+                         float* yacc, float* stats, int flags, int N, int D, int H, int W, int Cout, int splits,
+                         hipStream_t s);
+
 int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
                    const void* wpack, const float* bias, void* y0, void* y1, int cy0,
                    float* yacc, float* stats, int flags,
                    int N, int D, int H, int W, int Cout, int splits, hipStream_t s) {
+  return conv3_fwd_any(dtype, x0, c0, x1, c1, nullptr, nullptr, wpack, bias, y0, y1, cy0, yacc, stats, flags, N, D,
+                       H, W, Cout, splits, s);
+}
+
+// the same with the input's BatchNorm + ReLU applied in the staging path: the conv of
+// relu(x * isc + ish) (bf16, one source of <= 128 channels, the big-box shapes; -5 otherwise)
+int pcms_conv3_fwd_bnin(int dtype, const void* x, int cin, const float* isc, const float* ish, const void* wpack,
+                        const float* bias, void* y, float* stats, int N, int D, int H, int W, int Cout,
+                        hipStream_t s) {
+  if (!isc || !ish || cin > kBgBnMax || dtype != PCMS_BF16) return -1;
+  return conv3_fwd_any(dtype, x, cin, nullptr, 0, isc, ish, wpack, bias, y, nullptr, Cout, nullptr, stats, 0, N, D,
+                       H, W, Cout, 1, s);
+}
+
+}  // extern "C"
+
+static int conv3_fwd_any(int dtype, const void* x0, int c0, const void* x1, int c1, const float* isc,
+                         const float* ish, const void* wpack, const float* bias, void* y0, void* y1, int cy0,
+                         float* yacc, float* stats, int flags, int N, int D, int H, int W, int Cout, int splits,
+                         hipStream_t s) {
   const int accumulate = flags & PCMS_CONV_ACCUMULATE;
   const int Cin = c0 + c1;
   const int CK = pcms_conv3_chunk(dtype);
@@ -1791,6 +1857,7 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   Box b = fwd_box(D, H, W);
   Conv3Params p;
   p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1;
+  p.isc = isc; p.ish = ish;
   p.w = wpack; p.bias = bias; p.y0 = y0; p.y1 = y1; p.cy0 = cy0;
   p.yacc = splits > 1 ? yacc : nullptr;
   p.stats = stats; p.accumulate = flags;
@@ -1810,11 +1877,13 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
     p.nbd = D / kBgBD; p.nbh = H / 8; p.nbw = W / 16;
     const long nvox = (long)N * D * H * W;
     const int nslot = big_slots(N, D, H, W, Cout);
-    (void)hipFuncSetAttribute((const void*)conv3_fwd_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kBgLds);
-    hipLaunchKernelGGL(conv3_fwd_big_kernel, dim3(nslot * (Cout / 64)), dim3(kBgThreads), kBgLds, s, p,
+    auto kern = p.isc ? conv3_fwd_big_kernel<true> : conv3_fwd_big_kernel<false>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kBgLds);
+    hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64)), dim3(kBgThreads), kBgLds, s, p,
                        (uint32_t)(nvox * c0 * 2), (uint32_t)(nvox * c1 * 2));
     PCMS_CHECK_LAUNCH();
   }
+  if (p.isc) return -5;  // the input BatchNorm + ReLU runs on the big-box path only
   dim3 grid(N * p.nbd * p.nbh * p.nbw, Cout / 64, splits);
   const bool hot = b.lbd == 2 && b.lbh == 3 && b.lbw == 4;
   const bool small = b.lbd + b.lbh + b.lbw <= 8 && g_conv_mtw2;  // <= 256 voxels: 2 M-tiles per wave
@@ -1832,6 +1901,8 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
   }
   PCMS_CHECK_LAUNCH();
 }
+
+extern "C" {
 
 
 

@@ -100,6 +100,9 @@ struct Conv3Params {
   int nchunk, chunks_per_split;
   long nvox;             // N * D * H * W (split-K slab stride, in voxels)
   int lbd, lbh, lbw, nbd, nbh, nbw;
+  // conv3_fwd_big_kernel<true> (pcms_conv3_fwd_bnin): the input is relu(x * isc + ish) per
+  // input channel, applied to the staged halo in LDS (the BatchNorm + ReLU of the layer below)
+  const float* isc = nullptr; const float* ish = nullptr;
 };
 
 // dy tile: 128-B (bf16) rows, 64-B halves swizzled by row bit 1 (conflict-free tr reads).

@@ -35,6 +35,32 @@ __global__ void pack_input_kernel(const float* in, T* out, int N, int Cin, long 
   }
 }
 
+// the same with 4 voxels per thread (V % 4 == 0, Cin <= Cp == 8): one 16-B load per input
+// channel, one 16-B (bf16) / two 16-B (fp32) stores per voxel
+template <typename T>
+__global__ void __launch_bounds__(256) pack_input4_kernel(const float* in, T* out, int N, int Cin, long V) {
+  const long quads = (long)N * V / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < quads; i += (long)gridDim.x * blockDim.x) {
+    const long n = (4 * i) / V, v = (4 * i) % V;
+    f32x4_t x[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      x[c] = c < Cin ? __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(in + (n * Cin + c) * V + v))
+                     : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (sizeof(T) == 2) {
+        const u32x4_t o = {pack_bf16x2(x[0][k], x[1][k]), pack_bf16x2(x[2][k], x[3][k]),
+                           pack_bf16x2(x[4][k], x[5][k]), pack_bf16x2(x[6][k], x[7][k])};
+        *reinterpret_cast<u32x4_t*>(out + (4 * i + k) * 8) = o;
+      } else {
+        *reinterpret_cast<f32x4_t*>(out + (4 * i + k) * 8) = (f32x4_t){x[0][k], x[1][k], x[2][k], x[3][k]};
+        *reinterpret_cast<f32x4_t*>(out + (4 * i + k) * 8 + 4) = (f32x4_t){x[4][k], x[5][k], x[6][k], x[7][k]};
+      }
+    }
+  }
+}
+
 // ---------------- BatchNorm statistics ----------------
 // Stage 1: fp32 partial rows [rows][C][2] -> fp64 column sums [RB][C][2] (RB row groups).
 // block = 256 threads = 4 row lanes x 64 channels; grid = (ceil(C / 64), RB).
@@ -1212,6 +1238,12 @@ int launch_head_apply(bool nt, int grid, hipStream_t s, const void* y, const flo
 extern "C" {
 
 int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long V, int Cp, hipStream_t s) {
+  if (Cp == 8 && Cin <= 8 && V % 4 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+    const int grid = grid_for((long)N * V / 4, TPB, 4 * 256);
+    if (dtype == PCMS_BF16) hipLaunchKernelGGL(pack_input4_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, in, (bf16_t*)out, N, Cin, V);
+    else hipLaunchKernelGGL(pack_input4_kernel<float>, dim3(grid), dim3(TPB), 0, s, in, (float*)out, N, Cin, V);
+    PCMS_CHECK_LAUNCH();
+  }
   const int grid = grid_for((long)N * V, TPB);
   if (dtype == PCMS_BF16) hipLaunchKernelGGL(pack_input_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, in, (bf16_t*)out, N, Cin, V, Cp);
   else hipLaunchKernelGGL(pack_input_kernel<float>, dim3(grid), dim3(TPB), 0, s, in, (float*)out, N, Cin, V, Cp);

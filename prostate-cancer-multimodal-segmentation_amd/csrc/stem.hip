@@ -12,6 +12,10 @@ namespace {
 // so K = 14 x 16 = 224 (135 real).  HBM-bound: 16 B in + 128 B out per voxel.
 // ------------------------------------------------------------------------------------
 constexpr int kStemSteps = 14;                    // 28 taps (27 + 1 zero) / 2
+// K-dense form (<= 5 input channels): one k-step per (kd, kh) tap row, k = the three kw taps'
+// 5 channels (15 + 1 zero): K = 9 x 16 = 144 (135 real) instead of 224
+constexpr int kStemDSteps = 9;
+constexpr int kStemPackElems = (kStemSteps + kStemDSteps) * 64 * 16;  // both forms, tap-pair first
 
 // timeline instrumentation hook for tests/kexp (empty in the product library)
 #ifndef STEM_STAMP
@@ -22,14 +26,22 @@ constexpr int kStemSteps = 14;                    // 28 taps (27 + 1 zero) / 2
 // master W[64][cin_w][27] fp32 -> [14][64][16] bf16, k = h * 8 + c <-> (tap 2s + h, c);
 // the 64 output columns are ordered (nt, j) -> channel 2 j + nt so that a lane's two MFMA
 // tiles hold an adjacent channel pair (one packed bf16x2 LDS write per row)
+// followed by the K-dense form [9][64][16]: step s = tap row (kd, kh) = (s / 3, s % 3), k =
+// 5 kw + c for kw < 3, c < 5 (k = 15: zero) -- the order of the R1 | R2 halo windows of
+// stem_fwd_direct_kernel<.., DENSE>; zero unless cin_w <= 5
 __global__ void stem_pack_kernel(const float* w, bf16_t* out, int cin_w) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= kStemSteps * 64 * 16) return;
+  if (i >= kStemPackElems) return;
   const int k = i & 15, col = (i >> 4) & 63, s = i >> 10;
   const int co = 2 * (col & 31) + (col >> 5);  // MFMA column (nt, j) <-> channel 2 j + nt
-  const int tap = 2 * s + (k >> 3), c = k & 7;
   float v = 0.f;
-  if (tap < 27 && c < cin_w) v = w[((long)co * cin_w + c) * 27 + tap];
+  if (s < kStemSteps) {
+    const int tap = 2 * s + (k >> 3), c = k & 7;
+    if (tap < 27 && c < cin_w) v = w[((long)co * cin_w + c) * 27 + tap];
+  } else {
+    const int sd = s - kStemSteps, kw = k / 5, c = k % 5;
+    if (k < 15 && c < cin_w && cin_w <= 5) v = w[((long)co * cin_w + c) * 27 + sd * 3 + kw];
+  }
   out[i] = f2bf(v);
 }
 
@@ -66,18 +78,28 @@ constexpr int kSDHaloBytes = kSDHaloRows * 16;
 constexpr int kSDW = 2 * kSDHaloBytes;                        // weights [14][64][32 B]
 constexpr int kSDRed = kSDW + kStemSteps * 64 * 32;
 constexpr int kSDLds = kSDRed + 8 * 64 * 3 * 4;               // + stats reduction
+// K-dense form: the two raw halo buffers, then the repacked windows R (960 rows x 32 B: the
+// box's (bd + 2)(bh + 2) tap rows x 16 output w), weights [9][64][32 B], stats reduction
+constexpr int kSDRRows = 6 * 10 * 16;
+constexpr int kSD2R = 2 * kSDHaloBytes;
+constexpr int kSD2W = kSD2R + kSDRRows * 32;
+constexpr int kSD2Red = kSD2W + kStemDSteps * 64 * 32;
+constexpr int kSD2Lds = kSD2Red + 8 * 64 * 3 * 4;
+static_assert(kSD2Lds <= 160 * 1024, "LDS");
 constexpr int kSDThr = 512;                                   // one 8-wave workgroup per CU
 
-// Output stores.  PCMS_STEM_WIDE 1 (the product): 16-B stores of whole 128-B voxel rows.  A
+// Output stores.  PCMS_STEM_WIDE 1: 16-B stores of whole 128-B voxel rows.  A
 // lane holds channels (2 j', 2 j' + 1) of 16 voxels per M-tile (j' = its MFMA column), so the
 // four lanes of a quad hold channels 8 k .. 8 k + 7 (k = column >> 2) of the same four
 // w-consecutive voxels of a group g; a 4 x 4 transpose inside the quad (two DPP quad_perm
 // stages, each lane selecting between its own and its partner's register) leaves lane j of
 // the quad with voxel 4 g + j's channels 8 k .. 8 k + 7: one buffer_store_dwordx4 per group
 // writes 8 whole voxel rows (1 KiB).  8 store instructions per wave and box instead of 32
-// dword stores; the same bytes to the same addresses.  0: the dword stores (A/B builds).
+// dword stores; the same bytes to the same addresses.  0 (the product): the dword stores --
+// A/B on one box, standalone launches: wide 84.4 / 82.9 us vs dword 80.5 / 78.8 us, the
+// 16 DPP + select VALU per group cost more than the 24 store instructions they save.
 #ifndef PCMS_STEM_WIDE
-#define PCMS_STEM_WIDE 1
+#define PCMS_STEM_WIDE 0
 #endif
 
 // DPP quad_perm controls: lane j reads lane j ^ 1 / j ^ 2 of its quad
@@ -109,10 +131,22 @@ __device__ __forceinline__ void quad_transpose4(uint32_t (&d)[4], bool b0, bool 
 }
 
 // RELU: eval mode with the BatchNorm folded into the weights / bias (the output is the ReLU
-// activation; no statistics)
-template <int LBD, int LBH, bool RELU>
+// activation; no statistics).
+// DENSE (<= 5 input channels, the product): K = 9 tap rows x 16 instead of 14 tap pairs x 16.
+// After a box's halo has landed every thread repacks two of its 960 (tap row, w) windows:
+// R1 = [x(w) c0-4, x(w + 1) c0-2], R2 = [x(w + 1) c3-4, x(w + 2) c0-4, 0] (halo w), one 32-B
+// LDS row per window with the 16-B halves swapped on w bit 3 (a 16-lane read group covers
+// all 16 slots of a 256-B bank row); the A fragment of (M-tile, tap row) is then one
+// ds_read_b128 of R1 (k-half 0) or R2 (k-half 1), and a box takes 36 MFMAs per wave instead
+// of 56.  One more raw barrier per box (repack -> MFMAs).  Measured why it pays: the stem
+// forward's MFMA phase does not hide under its store stream (standalone launches, same box:
+// 14 MFMA steps 81.3-81.8 us, the first 9 steps only 64.8-67.2 us, none 55.4 us:
+// tests/tools/ab_stem_multi.sh with -DSTEM_MFMA_STEPS).
+template <int LBD, int LBH, bool RELU, bool DENSE = false>
 __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params p, int nbox, int mrows,
                                                                     uint32_t xbytes, uint32_t ybytes) {
+  constexpr int KS = DENSE ? kStemDSteps : kStemSteps;  // MFMA k-steps per box
+  constexpr int WOFF = DENSE ? kSD2W : kSDW;
   constexpr int NWV = kSDThr / 64;
   static_assert((1 << (LBD + LBH + 4)) == NWV * 64, "box = 64 voxels per wave");
   constexpr int bd = 1 << LBD, bh = 1 << LBH, bw = 16;
@@ -120,7 +154,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   constexpr int NP = (HV + kSDThr - 1) / kSDThr;  // halo pieces per thread
   static_assert((HV + 63) / 64 * 64 <= kSDHaloRows, "halo (whole DMA pieces) fits");
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* red = reinterpret_cast<float*>(lds + kSDRed);
+  float* red = reinterpret_cast<float*>(lds + (DENSE ? kSD2Red : kSDRed));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR math)
   const int r_lane = lane & 31, hsel = lane >> 5;
@@ -132,13 +166,13 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   // 16-B k-halves swapped when column bit 3 is set (a 16-lane group then reads 16 distinct
   // 16-B slots of the bank row)
   {
-    const u32x4_t* wg = reinterpret_cast<const u32x4_t*>(p.w);
-    for (int i = tid; i < kStemSteps * 64 * 2; i += kSDThr) {
+    const u32x4_t* wg = reinterpret_cast<const u32x4_t*>(p.w) + (DENSE ? kStemSteps * 64 * 2 : 0);
+    for (int i = tid; i < KS * 64 * 2; i += kSDThr) {
       const int row = i >> 1, half = i & 1, col = row & 63;
-      *reinterpret_cast<u32x4_t*>(lds + kSDW + row * 32 + ((half ^ ((col >> 3) & 1)) * 16)) = wg[i];
+      *reinterpret_cast<u32x4_t*>(lds + WOFF + row * 32 + ((half ^ ((col >> 3) & 1)) * 16)) = wg[i];
     }
   }
-  const char* wl = lds + kSDW + r_lane * 32 + ((hsel ^ ((r_lane >> 3) & 1)) * 16);
+  const char* wl = lds + WOFF + r_lane * 32 + ((hsel ^ ((r_lane >> 3) & 1)) * 16);
   float bias_l[2] = {0.f, 0.f};
   if (p.bias) { bias_l[0] = p.bias[2 * r_lane]; bias_l[1] = p.bias[2 * r_lane + 1]; }
   // halo rows of the two 32-row MFMA tiles (perm32 layout)
@@ -147,8 +181,12 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   for (int mt = 0; mt < 2; ++mt) {
     const int r = wave * 64 + mt * 32 + perm32(r_lane);
     const int rd = r >> (LBH + 4), rh = (r >> 4) & (bh - 1), rw = r & 15;
-    hb16[mt] = ((rd * HH + rh) * HW + rw) * 16;
+    if constexpr (DENSE)  // window row (rd, rh, rw) of R, k-half hsel
+      hb16[mt] = kSD2R + ((rd * HH + rh) * 16 + rw) * 32 + ((((rw >> 3) & 1) ^ hsel) * 16);
+    else
+      hb16[mt] = ((rd * HH + rh) * HW + rw) * 16;
   }
+  static_assert(!DENSE || (bd + 2) * HH * 16 <= kSDRRows, "windows fit R");
   // halo pieces of this thread: relative source offset (bytes) and packed coordinates
   int prel[NP], pco[NP];
 #pragma unroll
@@ -226,8 +264,13 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
       qd[e & 3] = pk;
       if ((e & 3) == 3) {  // the group's four voxels are packed: transpose, one 16-B store
         quad_transpose4(qd, qb0, qb1);
+        // soffset 0, the wave-uniform tile offset folded into voffset: a 16-B buffer store
+        // with an SGPR soffset gets no wait state before a VALU rewrites its data VGPRs (the
+        // compiler models that hazard only without a register soffset), and the store then
+        // read partly rewritten data (measured: the second dword of the last quad of every
+        // 16-lane row wrong in ~1 % of the stores); with soffset 0 hipcc pads it
         __builtin_amdgcn_raw_buffer_store_b128((u32x4_t){qd[0], qd[1], qd[2], qd[3]}, yr,
-                                               (g == 1 || g == 2) ? wB : wA, so[mt] + 4 * g * 128, 2);
+                                               ((g == 1 || g == 2) ? wB : wA) + so[mt] + 4 * g * 128, 0, 2);
       }
     } else {
       __builtin_amdgcn_raw_buffer_store_b32(pk, yr, (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 2);
@@ -289,6 +332,28 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
     STEM_STAMP(0);
     const int bn = b + gridDim.x;
     if (bn < nbox) stage(bn, (it + 1) & 1);
+    if constexpr (DENSE) {
+      // this box's halo -> the R1 | R2 windows (every wave is done with R: the barrier above)
+      const char* raw = lds + (it & 1) * kSDHaloBytes;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int j = tid + k * kSDThr;
+        if (j < (bd + 2) * HH * 16) {
+          const int row = j >> 4, w = j & 15;
+          const u32x4_t* src = reinterpret_cast<const u32x4_t*>(raw + (row * HW + w) * 16);
+          const u32x4_t a = src[0], bb = src[1], c = src[2];
+          const u32x4_t r1 = {a[0], a[1], __builtin_amdgcn_perm(bb[0], a[2], 0x05040100u),
+                              __builtin_amdgcn_perm(bb[1], bb[0], 0x05040302u)};
+          const u32x4_t r2 = {__builtin_amdgcn_perm(bb[2], bb[1], 0x05040302u), c[0], c[1], c[2] & 0xffffu};
+          char* dst = lds + kSD2R + j * 32;
+          const int sw = ((w >> 3) & 1) * 16;
+          *reinterpret_cast<u32x4_t*>(dst + sw) = r1;
+          *reinterpret_cast<u32x4_t*>(dst + (16 - sw)) = r2;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     STEM_STAMP(1);
     const bool interleave = pb >= 0 && is_full(pb);
     if (pb >= 0 && !interleave) epilogue(prev, pb);
@@ -308,6 +373,12 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
       int hs16 = hsel * 16;
       asm volatile("" : "+v"(hs16));
       auto load_a = [&](int st, s16x8_t (&a)[2]) {
+        if constexpr (DENSE) {  // tap row (kd, kh) = (st / 3, st % 3): a whole-row offset in R
+          const int off = ((st / 3) * HH + st % 3) * 16 * 32;
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(lds + hb16[mt] + off);
+          return;
+        }
         const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
         const int off16 = o0 * 16 + hs16 * (o1 - o0);
 #pragma unroll
@@ -321,23 +392,30 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
       load_a(0, abuf[0]);
       load_b(0, bbuf[0]);
 #pragma unroll
-      for (int st = 0; st < kStemSteps; ++st) {
-        if (st + 1 < kStemSteps) {
+      for (int st = 0; st < KS; ++st) {
+        if (st + 1 < KS) {
           load_a(st + 1, abuf[(st + 1) & 1]);
           load_b(st + 1, bbuf[(st + 1) & 1]);
         }
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-          acc[mt][0] = mfma(abuf[st & 1][mt], bbuf[st & 1][0], acc[mt][0]);
-          acc[mt][1] = mfma(abuf[st & 1][mt], bbuf[st & 1][1], acc[mt][1]);
+#ifdef STEM_MFMA_STEPS  // ablation builds (tests/tools/ab_build.sh): MFMAs of the first N steps only
+          if (st < STEM_MFMA_STEPS)
+#endif
+          {
+            acc[mt][0] = mfma(abuf[st & 1][mt], bbuf[st & 1][0], acc[mt][0]);
+            acc[mt][1] = mfma(abuf[st & 1][mt], bbuf[st & 1][1], acc[mt][1]);
+          }
         }
         // the next step's four fragment reads go out ahead of this step's MFMAs (left to
         // itself the scheduler sank them below three of the MFMAs, exposing the LDS
         // latency); the owed epilogue items go between the MFMAs
-        if (st + 1 < kStemSteps) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        if (st + 1 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
         if constexpr (IL) {
-          constexpr int q0[15] = {0, 3, 6, 9, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30, 32};
-          const int qa = q0[st], qb = q0[st + 1];
+          // the 32 owed items over the KS steps (<= 4 per step: one per MFMA)
+          constexpr int q14[15] = {0, 3, 6, 9, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30, 32};
+          constexpr int q9[10] = {0, 4, 8, 12, 16, 20, 24, 27, 30, 32};
+          const int qa = DENSE ? q9[st] : q14[st], qb = DENSE ? q9[st + 1] : q14[st + 1];
 #pragma unroll
           for (int q = qa; q < qb; ++q) item_full(prev, q >> 4, q & 15, pso);
 #pragma unroll
@@ -355,8 +433,10 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
               __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // 1 store
             }
           }
-          if (st < 4) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 4 - 3 items
-          else __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         // 4 - 2 items
+          const int rest = 4 - (qb - qa);  // the step's other MFMAs (a constant once unrolled)
+          if (rest == 1) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          else if (rest == 2) __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          else if (rest == 3) __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
         } else {
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         }
@@ -642,8 +722,11 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
 #pragma unroll
     for (int i = 0; i < BD; ++i) {
       if (i + 1 < BD) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
+#ifndef STEM_WG_TILES  // ablation builds: MFMAs of the first N column tiles only
+#define STEM_WG_TILES 7
+#endif
 #pragma unroll
-      for (int j = 0; j < 7; ++j) acc[j] = mfma(a[i & 1], bq[i & 1][j], acc[j]);
+      for (int j = 0; j < STEM_WG_TILES; ++j) acc[j] = mfma(a[i & 1], bq[i & 1][j], acc[j]);
     }
   };
 
@@ -774,10 +857,10 @@ extern "C" {
 
 int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s) {
   if (cin_w > 8) return -1;
-  hipLaunchKernelGGL(stem_pack_kernel, dim3(cdiv(kStemSteps * 64 * 16, 256)), dim3(256), 0, s, w, (bf16_t*)out, cin_w);
+  hipLaunchKernelGGL(stem_pack_kernel, dim3(cdiv(kStemPackElems, 256)), dim3(256), 0, s, w, (bf16_t*)out, cin_w);
   PCMS_CHECK_LAUNCH();
 }
-int pcms_stem_pack_elems(void) { return kStemSteps * 64 * 16; }
+int pcms_stem_pack_elems(void) { return kStemPackElems; }
 
 // bit 0: pcms_stem_fwd runs this shape; bit 1: pcms_stem_wgrad runs it
 int pcms_stem_supported(int N, int D, int H, int W) {
@@ -794,8 +877,8 @@ int pcms_stem_fwd_rows(int N, int D, int H, int W) {
 int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, float* stats,
                   int N, int D, int H, int W, int flags, hipStream_t s) {
   if (!stem_fwd_direct_shape(N, D, H, W)) return -5;
-  if (flags & ~PCMS_CONV_RELU || (stats && flags)) return -8;
-  const bool relu = flags & PCMS_CONV_RELU;
+  if (flags & ~(PCMS_CONV_RELU | PCMS_STEM_DENSE) || (stats && (flags & PCMS_CONV_RELU))) return -8;
+  const bool relu = flags & PCMS_CONV_RELU, dense = flags & PCMS_STEM_DENSE;
   const Box b = fwd_box(D, H, W);
   Conv3Params p;
   p.x0 = x; p.x1 = nullptr; p.c0 = 8; p.c1 = 0;
@@ -809,10 +892,13 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
   const int nbox = N * p.nbd * p.nbh * p.nbw;
   const long xbytes = p.nvox * 16, ybytes = p.nvox * 128;
   const int grid = std::min(nbox, device_cus());
-  auto kern = b.lbd == 2 ? (relu ? stem_fwd_direct_kernel<2, 3, true> : stem_fwd_direct_kernel<2, 3, false>)
-                         : (relu ? stem_fwd_direct_kernel<3, 2, true> : stem_fwd_direct_kernel<3, 2, false>);
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSDLds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThr), kSDLds, s, p, nbox, nbox, (uint32_t)xbytes, (uint32_t)ybytes);
+  auto kern = dense ? (b.lbd == 2 ? (relu ? stem_fwd_direct_kernel<2, 3, true, true> : stem_fwd_direct_kernel<2, 3, false, true>)
+                                  : (relu ? stem_fwd_direct_kernel<3, 2, true, true> : stem_fwd_direct_kernel<3, 2, false, true>))
+                    : (b.lbd == 2 ? (relu ? stem_fwd_direct_kernel<2, 3, true> : stem_fwd_direct_kernel<2, 3, false>)
+                                  : (relu ? stem_fwd_direct_kernel<3, 2, true> : stem_fwd_direct_kernel<3, 2, false>));
+  const int lds = dense ? kSD2Lds : kSDLds;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThr), lds, s, p, nbox, nbox, (uint32_t)xbytes, (uint32_t)ybytes);
   PCMS_CHECK_LAUNCH();
 }
 

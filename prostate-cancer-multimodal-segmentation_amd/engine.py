@@ -106,6 +106,9 @@ class UNetEngine:
         # bf16 build: the stem runs on dedicated tap-packed kernels (HBM-bound)
         self.stem_fast = self.code == BF16 and self.cp == 8
         self.stem_sup = 0  # pcms_stem_supported bits for the allocated shape (set by _alloc)
+        # PCMS_STEM_DENSE: the K-dense stem forward (9 tap rows of 3 kw x 5 channels) when the
+        # weight has <= 5 input channels; 0 selects the 14-tap-pair kernel (A/B)
+        self.stem_dense = 16 if self.nmod <= 5 else 0
         self.stem_pack = None
         self._flat_ptrs = None
         self._packed_version = -1
@@ -456,7 +459,7 @@ class UNetEngine:
         RELU = 2  # PCMS_CONV_RELU
         splits = self._splits(N, S, c0 + c1, cs.cout, cs.code)
         if i == 0 and self.stem_sup & 1:
-            call("pcms_stem_fwd", x0, self._eval["stem"], bias, a, None, N, S[0], S[1], S[2], RELU)
+            call("pcms_stem_fwd", x0, self._eval["stem"], bias, a, None, N, S[0], S[1], S[2], RELU | self.stem_dense)
         elif splits == 1:
             call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, pack, bias, a, None, cs.cout, None, None, RELU,
                  N, S[0], S[1], S[2], cs.cout, 1)
@@ -581,7 +584,7 @@ class UNetEngine:
         st = b["stats"] if training and not recompute else None
         if cs is self.convs[0] and self.stem_sup & 1:
             with self._timed("stem_fwd"):
-                call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2], 0)
+                call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2], self.stem_dense)
             rows = query("pcms_stem_fwd_rows", N, *S)
         elif splits == 1:
             call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,

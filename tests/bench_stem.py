@@ -36,7 +36,7 @@ def main():
             if name == "calib":
                 y.copy_(dy)          # 268 MB read + 268 MB write (torch copy kernel)
             elif name == "fwd":
-                L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W, 0)
+                L.call("pcms_stem_fwd", x, wp, bias, y, stats, N, D, H, W, 16)  # the product: K-dense
             elif name == "wgrad0":  # the plain weight gradient over a stored dy (unfused path)
                 L.call("pcms_stem_wgrad", x, dy, dw, ws, 5, N, D, H, W)
             else:

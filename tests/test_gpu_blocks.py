@@ -188,7 +188,7 @@ def test_eval_packs_follow_optimizer_step(precision):
     m = UNet3D(n_modalities=5, n_classes=1, precision=precision).cuda()
     x = torch.rand(2, 5, 32, 32, 16)
     y = (torch.rand(2, 1, 32, 32, 16) < 0.4).float()
-    opt = FlatAdam(m, lr=1e-2, weight_decay=1e-5)
+    opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
     m.train()
     opt.zero_grad()
     BCEDiceLoss()(m(x.cuda()), y.cuda()).backward()
@@ -205,8 +205,8 @@ def test_eval_packs_follow_optimizer_step(precision):
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     lr = ref.forward(sd, x, training=False)
     assert float((after - before).abs().max()) > 0, "eval reused the pre-step folded weights"
-    if precision == "fp32":
-        assert float((after - lr).abs().max()) <= ATOL
+    if precision == "fp32":  # (test_eval_bn_folding's bars)
+        assert float((after - lr).abs().max()) <= ATOL * max(float(lr.abs().max()), 1.0)
     else:
         e_f, e_u = float((after - lr).abs().max()), float((unfolded - lr).abs().max())
         assert e_f <= 2 * e_u + 1e-2, (e_f, e_u)

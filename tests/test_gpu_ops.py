@@ -748,13 +748,16 @@ def test_adam_matches_torch():
 
 
 @pytest.mark.parametrize("dt,code", [(torch.float32, 0), (torch.bfloat16, 1)])
-def test_pack_input(dt, code):
+@pytest.mark.parametrize("S", [(3, 4, 5), (3, 3, 5), (16, 16, 8)])
+def test_pack_input(dt, code, S):
+    """NCDHW fp32 -> NDHWC 8-channel (4-voxel vector path when V % 4 == 0, else scalar)."""
     L = _lib()
-    x = torch.rand(2, 5, 3, 4, 5)
-    out = torch.empty(2, 3, 4, 5, 8, dtype=dt, device=DEV)
-    L.call("pcms_pack_input", code, x.to(DEV), out, 2, 5, 60, 8)
+    V = S[0] * S[1] * S[2]
+    x = torch.rand(2, 5, *S)
+    out = torch.full((2, *S, 8), float("nan"), dtype=dt, device=DEV)
+    L.call("pcms_pack_input", code, x.to(DEV), out, 2, 5, V, 8)
     torch.cuda.synchronize()
-    exp = torch.zeros(2, 3, 4, 5, 8)
+    exp = torch.zeros(2, *S, 8)
     exp[..., :5] = ndhwc(x)
     close(out.cpu(), exp.to(dt), 0, "pack input")
 
@@ -762,10 +765,13 @@ def test_pack_input(dt, code):
 @pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (1, (9, 10, 11)), (2, (8, 8, 4)), (1, (6, 20, 33)),
                                  (1, (8, 12, 48)), (3, (4, 4, 16)), (1, (32, 32, 32)), (1, (48, 64, 64)),
                                  (2, (32, 64, 64)), (1, (12, 16, 16)), (4, (8, 64, 128))])
-def test_stem_fwd_wgrad_bf16(N, S):
-    """Dedicated stem kernels (tap-pair packed K) vs torch conv3d on the bf16-rounded input,
-    on the shapes they support (pcms_stem_supported; others refuse and the engine takes the
-    general kernels)."""
+@pytest.mark.parametrize("cin,dense", [(5, 16), (5, 0), (3, 16)])
+def test_stem_fwd_wgrad_bf16(N, S, cin, dense):
+    """Dedicated stem kernels vs torch conv3d on the bf16-rounded input, on the shapes they
+    support (pcms_stem_supported; others refuse and the engine takes the general kernels).
+    Forward: the K-dense kernel (PCMS_STEM_DENSE, 9 tap rows x 16: the product for <= 5
+    channels; also at 3 channels) and the 14-tap-pair kernel; both against fp64, and against
+    each other to the fp32 summation-order noise (same bf16 products)."""
     L = _lib()
     sup = L.query("pcms_stem_supported", N, *S)
     # (4, (8, 64, 128)): 4096 boxes, 16 per persistent workgroup of each kernel
@@ -777,11 +783,11 @@ def test_stem_fwd_wgrad_bf16(N, S):
             L.call("pcms_stem_fwd", None, None, None, None, None, N, *S, 0)
         return
     g = torch.Generator().manual_seed(sum(S))
-    x = torch.rand(N, 5, *S, generator=g).to(torch.bfloat16)
-    w = (torch.randn(64, 5, 3, 3, 3, generator=g) * 0.2)
+    x = torch.rand(N, cin, *S, generator=g).to(torch.bfloat16)
+    w = (torch.randn(64, cin, 3, 3, 3, generator=g) * 0.2)
     b = torch.randn(64, generator=g)
     xs = torch.zeros(N, 8, *S, dtype=torch.bfloat16)
-    xs[:, :5] = x
+    xs[:, :cin] = x
     xd = ndhwc(xs).to(DEV)
     xr = x.double()
     wr = w.to(torch.bfloat16).double().requires_grad_(True)
@@ -790,25 +796,29 @@ def test_stem_fwd_wgrad_bf16(N, S):
     ref.backward(dy.double())
     if sup & 1:
         wp = torch.empty(L.query("pcms_stem_pack_elems"), dtype=torch.bfloat16, device=DEV)
-        L.call("pcms_stem_pack", w.to(DEV), wp, 5)
+        L.call("pcms_stem_pack", w.to(DEV), wp, cin)
         y = torch.empty(N, *S, 64, dtype=torch.bfloat16, device=DEV)
         rows = L.query("pcms_stem_fwd_rows", N, *S)
         stats = torch.zeros(rows * (64 * 2 + 1), device=DEV)
-        L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y, stats, N, *S, 0)
+        L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y, stats, N, *S, dense)
+        y_other = torch.empty_like(y)
+        L.call("pcms_stem_fwd", xd, wp, b.to(DEV), y_other, None, N, *S, 16 - dense)
         torch.cuda.synchronize()
         close(ncdhw(y.cpu()), ref.detach(), 1e-2, "stem fwd")
+        # the two K orders round differently only where an fp32 sum lands on a bf16 tie
+        assert (y.float() - y_other.float()).abs().max().item() <= 2 ** -6 * ref.abs().max().item()
         mean, var = bn_moments(stats, rows, 64, N * S[0] * S[1] * S[2])
         yr = ref.detach().transpose(0, 1).reshape(64, -1)
         close(mean, yr.mean(1), 1e-3, "stem stats mean")
         close(var, yr.var(1, unbiased=False), 1e-3, "stem stats var")
     if sup & 2:
         guard = 4096
-        dw = torch.zeros(64 * 5 * 27 + guard, device=DEV)
-        ws = torch.empty(L.query("pcms_stem_wgrad_ws_floats", N, *S, 5), device=DEV)
-        L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, ws, 5, N, *S)
+        dw = torch.zeros(64 * cin * 27 + guard, device=DEV)
+        ws = torch.empty(L.query("pcms_stem_wgrad_ws_floats", N, *S, cin), device=DEV)
+        L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, ws, cin, N, *S)
         torch.cuda.synchronize()
-        assert dw[-guard:].abs().max().item() == 0.0
-        close(dw[:-guard].cpu().view(64, 5, 3, 3, 3), wr.grad, 1e-4, "stem wgrad")
+        assert dw[64 * cin * 27:].abs().max().item() == 0.0
+        close(dw[:64 * cin * 27].cpu().view(64, cin, 3, 3, 3), wr.grad, 1e-4, "stem wgrad")
 
 
 @pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (3, (4, 4, 16)), (1, (12, 16, 32)), (2, (32, 64, 64))])

@@ -21,10 +21,14 @@ def main():
     L.call("pcms_stem_pack", w, wp, 5)
     bias = torch.randn(64, device="cuda")
     stats = torch.empty(L.query("pcms_stem_fwd_rows", N, D, H, W) * 129, device="cuda")
+    bnv = [torch.rand(64, device="cuda") + 0.5 for _ in range(4)]  # scale, shift, mean, invstd
+    coef = torch.randn(3 * 64, device="cuda") * 0.01
     dw = torch.zeros(64 * 5 * 27, device="cuda")
     ws = torch.empty(L.query("pcms_stem_wgrad_ws_floats", N, D, H, W, 5), device="cuda")
-    fns = {"fwd": lambda s: L.call("pcms_stem_fwd", s[0], wp, bias, s[1], stats, N, D, H, W, 0),
-           "wgrad": lambda s: L.call("pcms_stem_wgrad", s[0], s[2], dw, ws, 5, N, D, H, W)}
+    fns = {"fwd": lambda s: L.call("pcms_stem_fwd", s[0], wp, bias, s[1], stats, N, D, H, W, 16),
+           "fwd14": lambda s: L.call("pcms_stem_fwd", s[0], wp, bias, s[1], stats, N, D, H, W, 0),
+           "wgrad": lambda s: L.call("pcms_stem_wgrad", s[0], s[2], dw, ws, 5, N, D, H, W),
+           "wgrad_bn": lambda s: L.call("pcms_stem_wgrad_bn", s[0], s[2], s[1], *bnv, coef, dw, ws, 5, N, D, H, W)}
     res = {}
     for rep in range(3):
         for name, fn in fns.items():
@@ -39,7 +43,8 @@ def main():
             e1.synchronize()
             res.setdefault(name, []).append(e0.elapsed_time(e1) / 30 * 1e3)
     t = {k: min(v) for k, v in res.items()}
-    print(f"fwd {t['fwd']:.1f} us  wgrad {t['wgrad']:.1f} us  frac {578.9e6 / ((t['fwd'] + t['wgrad']) * 1e-6) / 8e12:.4f}"
+    print(f"fwd {t['fwd']:.1f} us (14-step {t['fwd14']:.1f})  wgrad {t['wgrad']:.1f} us  wgrad_bn {t['wgrad_bn']:.1f} us  "
+          f"frac(847.3 MB) {847.3e6 / ((t['fwd'] + t['wgrad_bn']) * 1e-6) / 8e12:.4f}"
           f"  (all: {res})", flush=True)
 
 
