@@ -86,6 +86,13 @@ int pcms_conv3_fwd(int dtype, const void* x0, int c0, const void* x1, int c1,
 int pcms_conv3_fwd_bnin(int dtype, const void* x, int cin, const float* isc, const float* ish, const void* wpack,
                         const float* bias, void* y, float* stats, int N, int D, int H, int W, int Cout,
                         hipStream_t s);
+/* The weight gradient of that conv: x is the pre-BatchNorm input, relu(x * isc + ish) is
+ * applied to the staged halo in LDS (bf16, one source, the LDS-DMA shapes; -5 otherwise).
+ * pcms_conv3_bnin_ok: 1 when both pcms_conv3_fwd_bnin and this run the layer.              */
+int pcms_conv3_wgrad_bnin(int dtype, const void* x, int cin, const float* isc, const float* ish, const void* dy,
+                          float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w, int target_wgs,
+                          int flags, hipStream_t s);
+int pcms_conv3_bnin_ok(int N, int D, int H, int W, int cin, int Cout, int target_wgs);
 /* dw [Cout][cin_w][27] fp32 += sum_v dy[v, co] * x[v + tap, ci] (ci < cin_w <= c0 + c1;
  * flags PCMS_GRAD_STORE: dw = ...);
  * dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (one partial row per voxel split,
@@ -105,6 +112,9 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
  * does (other shapes: the general pcms_conv3_fwd / pcms_conv3_wgrad).                   */
 int pcms_stem_supported(int N, int D, int H, int W);
 int pcms_stem_pack_elems(void);
+/* the stem weight gradient's MFMA columns: 1 (default) dense tap rows x 16 for cin_w <= 5,
+ * 0 taps x 8 channels; v < 0 queries; returns the previous setting                        */
+int pcms_stem_wgrad_dense(int v);
 int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
 /* y = stem conv(x) + bias; BatchNorm partial moments into stats, laid out as pcms_conv3_fwd
  * with rows = pcms_stem_fwd_rows(N, D, H, W) (one row per workgroup on the hot shapes)   */

@@ -28,11 +28,14 @@ SIGNATURES = {
     "pcms_conv3_pack2": "ipppiis",
     "pcms_conv3_splits": "iii",
     "pcms_conv3_fwd": "ipipippppippiiiiiiis",
-    "pcms_conv3_fwd_bnin": "ipippppppiiiiiis",
+    "pcms_conv3_fwd_bnin": "ipi" + "p" * 6 + "iiiii" + "s",
+    "pcms_conv3_wgrad_bnin": "ipi" + "p" * 5 + "i" * 8 + "s",
+    "pcms_conv3_bnin_ok": "iiiiiii",
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiiis",
     "pcms_conv3_wgrad_tg_maxbox": "i",
     "pcms_stem_pack_elems": "",
+    "pcms_stem_wgrad_dense": "i",
     "pcms_stem_pack": "ppis",
     "pcms_stem_supported": "iiii",
     "pcms_stem_fwd_rows": "iiii",

@@ -456,12 +456,18 @@ struct WgradParams {
   int cw, direct;
   int store;             // PCMS_GRAD_STORE: dw = (the first writer of a fresh gradient), not +=
   int ntg;               // tap groups (TG kernels: 2, taps [0, 16) / [16, 27) per workgroup)
+  // BNIN kernels (pcms_conv3_wgrad_bnin): x is relu(x0 * isc + ish) per input channel
+  const float* isc = nullptr; const float* ish = nullptr;
 };
 
 
 // TG: the taps are split over two workgroups per (tile, split) -- for grids of few boxes,
 // where splitting the voxels instead would add partial rows and a reduction pass
-template <typename T, int LBD, int LBH, int LBW, bool TG = false, bool P4 = false>
+// BNIN (bf16, LDS-DMA staging, one source): the staged x halo is relu(x * isc + ish), applied
+// in LDS by the thread that staged each piece, after its DMA landed and before the barrier that
+// publishes the buffer (the BatchNorm + ReLU of the layer below, fused as in
+// conv3_fwd_big_kernel<true>); out-of-range pieces (zero padding) stay zero
+template <typename T, int LBD, int LBH, int LBW, bool TG = false, bool P4 = false, bool BNIN = false>
 __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p) {
   const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   typedef WTraits<T> Tr;
@@ -822,7 +828,9 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // streams in while this one computes.  The dy tile keeps dy_off_bf16's half swap (applied
   // to the source address); each wave instruction is all-dy or all-halo (2048 dy pieces);
   // out-of-range pieces read zeros.
-  auto stage_dma = [&](char* buf, int b) {
+  // BNIN: bit i = piece i of this thread is a real (in-range) x-halo piece
+  auto stage_dma = [&](char* buf, int b) -> uint32_t {
+    uint32_t xm = 0;
     int n, d0, h0, w0;
     box_origin(b, n, d0, h0, w0);
     const uint32_t lb0 = lds_addr(buf);
@@ -854,20 +862,54 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         if (hp < XP && gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && xc + q * 8 < xs)
           voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * xs + xc + q * 8) * 2);
         dma16(xr, __builtin_amdgcn_readfirstlane(lb0 + DYBYTES + (pc0 - DYP) * 16), voff, 0);
+        if (voff != kOOB) xm |= 1u << i;
       }
     }
+    return xm;
   };
+  // BNIN: this thread's landed x pieces of buffer buf in place (every piece of a thread has
+  // channel group q = tid & 3: DYP and the 512-piece rounds are multiples of 4)
+  float* bnt = reinterpret_cast<float*>(wlds + Tr::NBUF * BUFBYTES);
+  auto bn_x = [&](char* buf, uint32_t xm) {
+    const int q = tid & 3;
+    const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(bnt + q * 8), s1 = *reinterpret_cast<const f32x4_t*>(bnt + q * 8 + 4);
+    const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(bnt + 32 + q * 8);
+    const f32x4_t h1 = *reinterpret_cast<const f32x4_t*>(bnt + 32 + q * 8 + 4);
+    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      if (!((xm >> i) & 1)) continue;
+      u32x4_t* v = reinterpret_cast<u32x4_t*>(buf + DYBYTES + (tid + i * kWThreads - DYP) * 16);
+      u32x4_t x = *v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        x[k] = pack_bf16x2(bn_relu1(__uint_as_float(x[k] << 16), sc[2 * k], sh[2 * k]),
+                           bn_relu1(__uint_as_float(x[k] & 0xffff0000u), sc[2 * k + 1], sh[2 * k + 1]));
+      *v = x;
+    }
+  };
+  if constexpr (BNIN) {
+    if (tid < 32) {
+      const int c = ci_base + tid;
+      bnt[tid] = c < p.Cin ? p.isc[c] : 0.f;
+      bnt[32 + tid] = c < p.Cin ? p.ish[c] : 0.f;
+    }
+    __syncthreads();
+  }
 
   if (b_beg < b_end && p.dma) {
     if constexpr (Tr::NBUF == 2) {
-      stage_dma(wlds, b_beg);
+      uint32_t xm = stage_dma(wlds, b_beg);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (BNIN) bn_x(wlds, xm);
       __syncthreads();
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
-        if (b + 1 < b_end) stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
+        if (b + 1 < b_end) xm = stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
         compute_box(wlds + cur * BUFBYTES);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (BNIN) if (b + 1 < b_end) bn_x(wlds + (cur ^ 1) * BUFBYTES, xm);
         __syncthreads();
       }
     }
@@ -1946,9 +1988,40 @@ int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, in
 // cin_w <= c0 + c1 is the weight's input-channel count (the stored input may be padded).
 // dwt: pcms_conv3_wgrad_ws_floats(...) fp32 workspace (per-split partial rows, summed in a
 // fixed order: the result is deterministic).
+static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, int c1, const float* isc,
+                           const float* ish, const void* dy, float* dw, float* dwt, int N, int D, int H, int W,
+                           int Cout, int cin_w, int target_wgs, int flags, hipStream_t s);
+
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w, int target_wgs,
                      int flags, hipStream_t s) {
+  return conv3_wgrad_any(dtype, x0, c0, x1, c1, nullptr, nullptr, dy, dw, dwt, N, D, H, W, Cout, cin_w, target_wgs,
+                         flags, s);
+}
+
+// 1: pcms_conv3_fwd_bnin and pcms_conv3_wgrad_bnin (target_wgs) both run this bf16 layer
+int pcms_conv3_bnin_ok(int N, int D, int H, int W, int cin, int Cout, int target_wgs) {
+  const long nvox = (long)N * D * H * W;
+  if (cin > kBgBnMax || cin % 16 || Cout % 64 || !big_fwd_ok(PCMS_BF16, N, D, H, W, cin, 0)) return 0;
+  if (nvox * std::max(Cout, cin) * 2 >= (long)kOOB) return 0;
+  return wgrad_plan(PCMS_BF16, N, D, H, W, cin, Cout, target_wgs).ntg == 1 ? 1 : 0;
+}
+
+// the weight gradient of the conv of relu(x * isc + ish) (pcms_conv3_fwd_bnin's forward):
+// bf16, one source; the LDS-DMA shapes only (-5 otherwise)
+int pcms_conv3_wgrad_bnin(int dtype, const void* x, int cin, const float* isc, const float* ish, const void* dy,
+                          float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w, int target_wgs,
+                          int flags, hipStream_t s) {
+  if (!isc || !ish || dtype != PCMS_BF16) return -1;
+  return conv3_wgrad_any(dtype, x, cin, nullptr, 0, isc, ish, dy, dw, dwt, N, D, H, W, Cout, cin_w, target_wgs,
+                         flags, s);
+}
+
+}  // extern "C"
+
+static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, int c1, const float* isc,
+                           const float* ish, const void* dy, float* dw, float* dwt, int N, int D, int H, int W,
+                           int Cout, int cin_w, int target_wgs, int flags, hipStream_t s) {
   const int Cin = c0 + c1;
   if (cin_w <= 0 || cin_w > Cin) return -4;
   if (flags & ~PCMS_GRAD_STORE) return -8;
@@ -1975,9 +2048,20 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
   p.direct = splits == 1;
   p.store = flags & PCMS_GRAD_STORE;
   p.ntg = q.ntg;
+  p.isc = isc; p.ish = ish;
+  if (isc && (!p.dma || c1 != 0 || q.ntg != 1)) return -5;  // BNIN: the LDS-DMA one-source kernels
   dim3 grid(splits * p.nco * p.nci * q.ntg);
   size_t lds;
-  if (dtype == PCMS_BF16) {
+  if (dtype == PCMS_BF16 && isc) {
+    lds = (size_t)WTraits<bf16_t>::NBUF * (WTraits<bf16_t>::BV * WTraits<bf16_t>::DYROW + kWHaloMax * WTraits<bf16_t>::XROW) +
+          64 * sizeof(float);
+    auto kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1, false, false, true>;
+    if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4, false, false, true>;
+    else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4, false, false, true>;
+    else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3, false, false, true>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
+  } else if (dtype == PCMS_BF16) {
     lds = (size_t)WTraits<bf16_t>::NBUF * (WTraits<bf16_t>::BV * WTraits<bf16_t>::DYROW + kWHaloMax * WTraits<bf16_t>::XROW);
     auto kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1>;
     if (q.ntg == 2) {
@@ -2018,5 +2102,3 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
                      dw, Cout, Cin, cin_w, p.store);
   PCMS_CHECK_LAUNCH();
 }
-
-}  // extern "C"

@@ -81,8 +81,9 @@ constexpr int kSDLds = kSDRed + 8 * 64 * 3 * 4;               // + stats reducti
 // K-dense form: the two raw halo buffers, then the repacked windows R (960 rows x 32 B: the
 // box's (bd + 2)(bh + 2) tap rows x 16 output w), weights [9][64][32 B], stats reduction
 constexpr int kSDRRows = 6 * 10 * 16;
-constexpr int kSD2R = 2 * kSDHaloBytes;
-constexpr int kSD2W = kSD2R + kSDRRows * 32;
+constexpr int kSDRBytes = kSDRRows * 32;
+constexpr int kSD2R = 2 * kSDHaloBytes;                       // two R buffers
+constexpr int kSD2W = kSD2R + 2 * kSDRBytes;
 constexpr int kSD2Red = kSD2W + kStemDSteps * 64 * 32;
 constexpr int kSD2Lds = kSD2Red + 8 * 64 * 3 * 4;
 static_assert(kSD2Lds <= 160 * 1024, "LDS");
@@ -133,12 +134,15 @@ __device__ __forceinline__ void quad_transpose4(uint32_t (&d)[4], bool b0, bool 
 // RELU: eval mode with the BatchNorm folded into the weights / bias (the output is the ReLU
 // activation; no statistics).
 // DENSE (<= 5 input channels, the product): K = 9 tap rows x 16 instead of 14 tap pairs x 16.
-// After a box's halo has landed every thread repacks two of its 960 (tap row, w) windows:
+// Every thread repacks two of a box's 960 (tap row, w) windows from its landed halo:
 // R1 = [x(w) c0-4, x(w + 1) c0-2], R2 = [x(w + 1) c3-4, x(w + 2) c0-4, 0] (halo w), one 32-B
 // LDS row per window with the 16-B halves swapped on w bit 3 (a 16-lane read group covers
 // all 16 slots of a 256-B bank row); the A fragment of (M-tile, tap row) is then one
 // ds_read_b128 of R1 (k-half 0) or R2 (k-half 1), and a box takes 36 MFMAs per wave instead
-// of 56.  One more raw barrier per box (repack -> MFMAs).  Measured why it pays: the stem
+// of 56.  Pipelined so the repack costs no barrier of its own: the halo DMA runs two boxes
+// ahead of the MFMAs and the repack one box ahead, inside the MFMA steps (R double-buffered:
+// box b's MFMAs read R[b] while the threads build R[b + 1] from the halo that landed during
+// box b - 1; the one barrier per box publishes both).  Measured why it pays: the stem
 // forward's MFMA phase does not hide under its store stream (standalone launches, same box:
 // 14 MFMA steps 81.3-81.8 us, the first 9 steps only 64.8-67.2 us, none 55.4 us:
 // tests/tools/ab_stem_multi.sh with -DSTEM_MFMA_STEPS).
@@ -181,7 +185,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   for (int mt = 0; mt < 2; ++mt) {
     const int r = wave * 64 + mt * 32 + perm32(r_lane);
     const int rd = r >> (LBH + 4), rh = (r >> 4) & (bh - 1), rw = r & 15;
-    if constexpr (DENSE)  // window row (rd, rh, rw) of R, k-half hsel
+    if constexpr (DENSE)  // window row (rd, rh, rw) of R buffer 0, k-half hsel
       hb16[mt] = kSD2R + ((rd * HH + rh) * 16 + rw) * 32 + ((((rw >> 3) & 1) ^ hsel) * 16);
     else
       hb16[mt] = ((rd * HH + rh) * HW + rw) * 16;
@@ -319,8 +323,34 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   f32x16_t prev[2][2];
   int pb = -1;  // box whose epilogue is still owed
   int b = blockIdx.x;
+  // DENSE: box b's windows -> R buffer rb from halo buffer rb (two per thread)
+  auto repack = [&](int rb) {
+    const char* raw = lds + rb * kSDHaloBytes;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int j = tid + k * kSDThr;
+      if (j < (bd + 2) * HH * 16) {
+        const int row = j >> 4, w = j & 15;
+        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(raw + (row * HW + w) * 16);
+        const u32x4_t a = src[0], bb = src[1], c = src[2];
+        const u32x4_t r1 = {a[0], a[1], __builtin_amdgcn_perm(bb[0], a[2], 0x05040100u),
+                            __builtin_amdgcn_perm(bb[1], bb[0], 0x05040302u)};
+        const u32x4_t r2 = {__builtin_amdgcn_perm(bb[2], bb[1], 0x05040302u), c[0], c[1], c[2] & 0xffffu};
+        char* dst = lds + kSD2R + rb * kSDRBytes + j * 32;
+        const int sw = ((w >> 3) & 1) * 16;
+        *reinterpret_cast<u32x4_t*>(dst + sw) = r1;
+        *reinterpret_cast<u32x4_t*>(dst + (16 - sw)) = r2;
+      }
+    }
+  };
   if (b < nbox) stage(b, 0);
+  if (DENSE && b + (int)gridDim.x < nbox) stage(b + gridDim.x, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DENSE) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (b < nbox) repack(0);
+  }
   for (int it = 0; b < nbox; b += gridDim.x, ++it) {
     // halo(b) has landed for this wave (vmcnt at the loop end); barrier: for all waves, and
     // every wave is done reading the buffer the next DMA overwrites.  A raw s_barrier, not
@@ -331,29 +361,15 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
     __builtin_amdgcn_s_barrier();
     STEM_STAMP(0);
     const int bn = b + gridDim.x;
-    if (bn < nbox) stage(bn, (it + 1) & 1);
+    // DENSE: halo(b + 2G) into the buffer halo(b) left (repacked during the previous box);
+    // halo(b + G) landed at the previous box's end and is repacked during this box's MFMAs
     if constexpr (DENSE) {
-      // this box's halo -> the R1 | R2 windows (every wave is done with R: the barrier above)
-      const char* raw = lds + (it & 1) * kSDHaloBytes;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int j = tid + k * kSDThr;
-        if (j < (bd + 2) * HH * 16) {
-          const int row = j >> 4, w = j & 15;
-          const u32x4_t* src = reinterpret_cast<const u32x4_t*>(raw + (row * HW + w) * 16);
-          const u32x4_t a = src[0], bb = src[1], c = src[2];
-          const u32x4_t r1 = {a[0], a[1], __builtin_amdgcn_perm(bb[0], a[2], 0x05040100u),
-                              __builtin_amdgcn_perm(bb[1], bb[0], 0x05040302u)};
-          const u32x4_t r2 = {__builtin_amdgcn_perm(bb[2], bb[1], 0x05040302u), c[0], c[1], c[2] & 0xffffu};
-          char* dst = lds + kSD2R + j * 32;
-          const int sw = ((w >> 3) & 1) * 16;
-          *reinterpret_cast<u32x4_t*>(dst + sw) = r1;
-          *reinterpret_cast<u32x4_t*>(dst + (16 - sw)) = r2;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if (bn + (int)gridDim.x < nbox) stage(bn + gridDim.x, it & 1);
+    } else {
+      if (bn < nbox) stage(bn, (it + 1) & 1);
     }
+    const int rp = DENSE && bn < nbox ? (it + 1) & 1 : -1;  // R / halo buffer repacked this box
+    const int rcur = (it & 1) * kSDRBytes;                  // DENSE: this box's R buffer
     STEM_STAMP(1);
     const bool interleave = pb >= 0 && is_full(pb);
     if (pb >= 0 && !interleave) epilogue(prev, pb);
@@ -376,7 +392,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         if constexpr (DENSE) {  // tap row (kd, kh) = (st / 3, st % 3): a whole-row offset in R
           const int off = ((st / 3) * HH + st % 3) * 16 * 32;
 #pragma unroll
-          for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(lds + hb16[mt] + off);
+          for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const s16x8_t*>(lds + rcur + hb16[mt] + off);
           return;
         }
         const int o0 = tap_off(2 * st, HH, HW), o1 = tap_off(2 * st + 1, HH, HW);
@@ -440,6 +456,7 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         } else {
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         }
+        if (DENSE && st == 1 && rp >= 0) repack(rp);  // the next box's windows, under these MFMAs
         __builtin_amdgcn_sched_barrier(0);
       }
     };
@@ -549,6 +566,14 @@ constexpr int kSWRegion = 14 * 64 * kSWLaneStride * 4;   // 14 tiles (2 co x 7 c
 constexpr int kSWRing = kSWNS * SWGeom<kSWBD>::Buf;
 constexpr int kSWLds = kSWRing > 2 * kSWRegion ? kSWRing : 2 * kSWRegion;
 static_assert(kSWLds <= 160 * 1024, "ring / flush regions fit in LDS");
+// DENSE (<= 5 input channels): the MFMA columns are (tap row (kd, kh), k = 5 kw + c) -- 9 x 16
+// = 144 in 5 column tiles instead of (tap, channel) = 28 x 8 in 7 -- over the R1 | R2 windows
+// of the x halo (the forward's layout: one 32-B row per (halo d, halo h, w), halves swapped on
+// w bit 3), repacked after each box's halo lands (one more barrier per box).  R after the ring.
+constexpr int kSWRRows = (kSWBD + 2) * 6 * 16;
+constexpr int kSWR = kSWRing;
+constexpr int kSWLdsD = (kSWRing + kSWRRows * 32) > 2 * kSWRegion ? kSWRing + kSWRRows * 32 : 2 * kSWRegion;
+static_assert(kSWLdsD <= 160 * 1024, "ring + windows / flush regions fit in LDS");
 
 // BN: the stem's BatchNorm + ReLU backward apply fused in (models/unet3d.py:29-33: inc's
 // conv.0 -> bn -> relu).  ``dy`` is then the gradient of the ReLU output (da) and ``bn.y``
@@ -562,10 +587,11 @@ struct StemBN {
   const bf16_t* y;
   const float *scale, *shift, *mean, *invstd, *coef;
 };
-template <int BD, int NS, bool BN>
+template <int BD, int NS, bool BN, bool DENSE = false>
 __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t* x, const bf16_t* dy, float* part,
                                                                     int N, int D, int H, int W, int cin_w,
                                                                     uint32_t xbytes, uint32_t dybytes, StemBN bn) {
+  constexpr int NT = DENSE ? 5 : 7;  // MFMA column tiles
   typedef SWGeom<BD> Gm;
   constexpr int BH = 4, BW = 16, HH = BH + 2, HW = BW + 2;
   constexpr int kSWBV = Gm::BV, kSWHV = Gm::HV, kSWBuf = Gm::Buf;
@@ -688,45 +714,82 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   };
 
   const int g = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
-  f32x16_t acc[7];
+  f32x16_t acc[NT];
 #pragma unroll
-  for (int j = 0; j < 7; ++j)
+  for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
   // lane offsets of the tr reads, with the wave's k-step offset folded in (k-step s = ks +
   // 4 i is box row (rd = i, rh = ks): dy rows at s * 2048, halo rows at (i HH + ks) HW)
   const int aoff = dy_off_bf16(8 * hsel + qq, ct * 32 + g * 16 + pp * 4) + ks * 2048;
-  int boff[7];  // column tile j: taps 4 j + 2 g + (pp >> 1), channels 4 (pp & 1) .. + 3
+  int boff[NT];
 #pragma unroll
-  for (int j = 0; j < 7; ++j)
-    boff[j] = kSWBV * 128 + (8 * hsel + qq + tap_off(4 * j + 2 * g + (pp >> 1), HH, HW) + ks * HW) * 16 + (pp & 1) * 8;
+  for (int j = 0; j < NT; ++j) {
+    if constexpr (DENSE) {
+      // column tile j: tap row tr = 2 j + g (tile 4's upper half re-reads row 8: dropped in the
+      // flush), k = 4 pp .. + 3 = 8 B of the 32-B window row (hd = i + kd, hh = ks + kh, w =
+      // 8 hsel + qq: the halves swapped on w bit 3 = hsel); relative to the window region
+      const int trow = min(2 * j + g, 8), kd = trow / 3, kh = trow % 3;
+      boff[j] = ((kd * HH + kh + ks) * 16 + 8 * hsel + qq) * 32 + (((pp >> 1) ^ hsel) * 16) + (pp & 1) * 8;
+    } else {  // column tile j: taps 4 j + 2 g + (pp >> 1), channels 4 (pp & 1) .. + 3
+      boff[j] = kSWBV * 128 + (8 * hsel + qq + tap_off(4 * j + 2 * g + (pp >> 1), HH, HW) + ks * HW) * 16 + (pp & 1) * 8;
+    }
+  }
+#ifndef STEM_WG_TILES  // ablation builds: MFMAs of the first N column tiles only
+#define STEM_WG_TILES 99
+#endif
+  constexpr int NTM = STEM_WG_TILES < NT ? STEM_WG_TILES : NT;
   auto compute = [&](const char* buf) {
+    const uint32_t bbase = DENSE ? lds_addr(swl) + kSWR : lds_addr(buf);
     uint32_t pa = lds_addr(buf) + aoff, pb[7];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) pb[j] = lds_addr(buf) + boff[j];
-    asm volatile("" : "+v"(pa), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]), "+v"(pb[5]),
-                 "+v"(pb[6]));
+    for (int j = 0; j < NT; ++j) pb[j] = bbase + boff[j];
+    if constexpr (DENSE)
+      asm volatile("" : "+v"(pa), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]));
+    else
+      asm volatile("" : "+v"(pa), "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]), "+v"(pb[3]), "+v"(pb[4]), "+v"(pb[5]),
+                   "+v"(pb[6]));
     auto tr = [](uint32_t p, int off) {
       return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4_t*)(uintptr_t)(p + off));
     };
     auto cat = [](s16x4_t lo, s16x4_t hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); };
-    auto load = [&](int i, s16x8_t& a, s16x8_t (&bq)[7]) {
+    auto load = [&](int i, s16x8_t& a, s16x8_t (&bq)[NT]) {
       const int dyb = i * 4 * 2048;
-      const int hrb = i * HH * HW * 16;
+      // box d-row i: halo rows i HH HW (16 B) / window rows i HH 16 (32 B); the lane's second
+      // voxel 4 w further
+      const int hrb = DENSE ? i * HH * 16 * 32 : i * HH * HW * 16;
+      constexpr int w4 = DENSE ? 4 * 32 : 4 * 16;
       a = cat(tr(pa, dyb), tr(pa, dyb + 512));
 #pragma unroll
-      for (int j = 0; j < 7; ++j) bq[j] = cat(tr(pb[j], hrb), tr(pb[j], hrb + 64));
+      for (int j = 0; j < NT; ++j) bq[j] = cat(tr(pb[j], hrb), tr(pb[j], hrb + w4));
     };
-    s16x8_t a[2], bq[2][7];
+    s16x8_t a[2], bq[2][NT];
     load(0, a[0], bq[0]);
 #pragma unroll
     for (int i = 0; i < BD; ++i) {
       if (i + 1 < BD) load(i + 1, a[(i + 1) & 1], bq[(i + 1) & 1]);
-#ifndef STEM_WG_TILES  // ablation builds: MFMAs of the first N column tiles only
-#define STEM_WG_TILES 7
-#endif
 #pragma unroll
-      for (int j = 0; j < STEM_WG_TILES; ++j) acc[j] = mfma(a[i & 1], bq[i & 1][j], acc[j]);
+      for (int j = 0; j < NTM; ++j) acc[j] = mfma(a[i & 1], bq[i & 1][j], acc[j]);
+    }
+  };
+  // DENSE: box halo (ring slot buf) -> the R1 | R2 windows (two per thread)
+  auto repack = [&](const char* buf) {
+    const char* raw = buf + kSWBV * 128;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int j = tid + k * kSWT;
+      if (j < (BD + 2) * HH * 16) {
+        const int row = j >> 4, w = j & 15;
+        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(raw + (row * HW + w) * 16);
+        const u32x4_t a = src[0], bb = src[1], c = src[2];
+        const u32x4_t r1 = {a[0], a[1], __builtin_amdgcn_perm(bb[0], a[2], 0x05040100u),
+                            __builtin_amdgcn_perm(bb[1], bb[0], 0x05040302u)};
+        const u32x4_t r2 = {__builtin_amdgcn_perm(bb[2], bb[1], 0x05040302u), c[0], c[1], c[2] & 0xffffu};
+        char* dst = swl + kSWR + j * 32;
+        const int sw = ((w >> 3) & 1) * 16;
+        *reinterpret_cast<u32x4_t*>(dst + sw) = r1;
+        *reinterpret_cast<u32x4_t*>(dst + (16 - sw)) = r2;
+      }
     }
   };
 
@@ -751,6 +814,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const int b2 = b + (NS - 1) * G;
+    if constexpr (DENSE) repack(swl + (it % NS) * kSWBuf);  // R is free: every wave passed the barrier
     if constexpr (BN) {
       // box b's da tile and y chunks have landed: this wave's dy in place, then the next box's
       // y loads (before the DMA of box b + 2 G: the wait above stays a count of that DMA alone)
@@ -758,7 +822,12 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
       if (b + G < nbox) load_y(b + G);
     }
     if (b2 < nbox) stage(b2, (it + NS - 1) % NS);
-    if constexpr (BN) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own dy writes before own reads
+    if constexpr (DENSE) {  // every thread's windows (and own dy) written before any MFMA reads them
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else if constexpr (BN) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own dy writes before own reads
+    }
     compute(swl + (it % NS) * kSWBuf);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -771,8 +840,8 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   float* reg = reinterpret_cast<float*>(swl) + (ks & 1) * (kSWRegion / 4);
   if (ks < 2) {
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
+    for (int j = 0; j < NT; ++j) {
+      float* dst = reg + ((ct * NT + j) * 64 + lane) * kSWLaneStride;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         *reinterpret_cast<f32x4_t*>(dst + 4 * q) =
@@ -782,8 +851,8 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   __syncthreads();
   if (ks >= 2) {
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      float* dst = reg + ((ct * 7 + j) * 64 + lane) * kSWLaneStride;
+    for (int j = 0; j < NT; ++j) {
+      float* dst = reg + ((ct * NT + j) * 64 + lane) * kSWLaneStride;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         f32x4_t v = *reinterpret_cast<f32x4_t*>(dst + 4 * q);
@@ -802,8 +871,9 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   const int hh = tid >> 8, rem = tid & 255;
   if (rem < per_co) {
     const int c = rem / 27, t = rem - c * 27;
-    const int col = 8 * t + c;
-    const int cb = ((hh * 7 + (col >> 5)) * 64 + (col & 31)) * kSWLaneStride;
+    // column of (tap t, channel c): 8 t + c; DENSE: 16 (tap row) + 5 kw + c
+    const int col = DENSE ? 16 * (t / 3) + 5 * (t % 3) + c : 8 * t + c;
+    const int cb = ((hh * NT + (col >> 5)) * 64 + (col & 31)) * kSWLaneStride;
 #pragma unroll
     for (int cr = 0; cr < 32; ++cr) {
       const int hs = (cr >> 2) & 1, e = (cr & 3) + 4 * (cr >> 3);
@@ -844,6 +914,10 @@ __global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* par
 
 }  // namespace
 
+// the dense-column stem weight gradient for <= 5 input channels (1, the product) or the
+// 28-tap x 8-channel columns (0: A/B); pcms_stem_wgrad_dense sets it
+static int g_stem_wgrad_dense = 1;
+
 // the dedicated stem kernels' shape conditions (other shapes take the general conv kernels)
 static bool stem_fwd_direct_shape(int N, int D, int H, int W) {
   const Box b = fwd_box(D, H, W);
@@ -861,6 +935,14 @@ int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s) {
   PCMS_CHECK_LAUNCH();
 }
 int pcms_stem_pack_elems(void) { return kStemPackElems; }
+
+// the stem weight gradient's column form: 1 dense (tap row x 16, <= 5 channels), 0 tap x 8
+// channels; v < 0 only queries.  Returns the previous setting (test / A/B switch)
+int pcms_stem_wgrad_dense(int v) {
+  const int old = g_stem_wgrad_dense;
+  if (v >= 0) g_stem_wgrad_dense = v;
+  return old;
+}
 
 // bit 0: pcms_stem_fwd runs this shape; bit 1: pcms_stem_wgrad runs it
 int pcms_stem_supported(int N, int D, int H, int W) {
@@ -919,9 +1001,12 @@ static int stem_wgrad_any(const void* x, const void* dy, float* dw, float* ws, i
   const int nbox = N * (D / kSWBD) * (H / 4) * (W / 16);
   const int grid = std::min(nbox, device_cus());
   const long xbytes = (long)N * D * H * W * 16, dybytes = (long)N * D * H * W * 128;
-  auto kern = bn.y ? stem_wgrad_stream_kernel<kSWBD, kSWNS, true> : stem_wgrad_stream_kernel<kSWBD, kSWNS, false>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kSWLds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT), kSWLds, s, (const bf16_t*)x, (const bf16_t*)dy, ws, N, D, H, W,
+  const bool dense = cin_w <= 5 && g_stem_wgrad_dense;
+  auto kern = bn.y ? (dense ? stem_wgrad_stream_kernel<kSWBD, kSWNS, true, true> : stem_wgrad_stream_kernel<kSWBD, kSWNS, true>)
+                   : (dense ? stem_wgrad_stream_kernel<kSWBD, kSWNS, false, true> : stem_wgrad_stream_kernel<kSWBD, kSWNS, false>);
+  const int lds = dense ? kSWLdsD : kSWLds;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSWT), lds, s, (const bf16_t*)x, (const bf16_t*)dy, ws, N, D, H, W,
                      cin_w, (uint32_t)xbytes, (uint32_t)dybytes, bn);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;

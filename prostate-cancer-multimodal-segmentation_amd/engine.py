@@ -109,6 +109,12 @@ class UNetEngine:
         # PCMS_STEM_DENSE: the K-dense stem forward (9 tap rows of 3 kw x 5 channels) when the
         # weight has <= 5 input channels; 0 selects the 14-tap-pair kernel (A/B)
         self.stem_dense = 16 if self.nmod <= 5 else 0
+        # a DoubleConv's first BatchNorm + ReLU applied inside its second conv's staging (forward:
+        # pcms_conv3_fwd_bnin, weight gradient: pcms_conv3_wgrad_bnin) instead of a y1 -> a1 HBM
+        # pass, on the layers both kernels run (levels 0-1, bf16); bit-identical to the unfused
+        # pair (same arithmetic and rounding).  False: the a1 pass (A/B)
+        self.fuse_bnin = True
+        self._bnin_cache = {}
         self.stem_pack = None
         self._flat_ptrs = None
         self._packed_version = -1
@@ -574,15 +580,30 @@ class UNetEngine:
             return 1
         return max(1, min(nch, -(-384 // wgs)))
 
+    def _bnin(self, blk: BlockSpec, N, S) -> bool:
+        """The block's first BN + ReLU fused into its second conv (forward and weight gradient)?"""
+        if not self.fuse_bnin or self.code != BF16:
+            return False
+        key = (id(blk), N, tuple(S), self.wgrad_target)
+        if key not in self._bnin_cache:
+            self._bnin_cache[key] = bool(query("pcms_conv3_bnin_ok", N, *S, blk.c1.cin, blk.c1.cout,
+                                               self.wgrad_target))
+        return self._bnin_cache[key]
+
     def _conv(self, cs: ConvSpec, x0, c0, x1, c1, y, N, S, stats: bool, training: bool, bn: BNSpec,
-              recompute: bool = False):
+              recompute: bool = False, bnin: Optional[BNSpec] = None):
         """y = conv(x) + b; then BN statistics (train) or eval coefficients.  ``recompute``:
-        the conv alone (checkpointed decoder: the forward's BN coefficients are reused)."""
+        the conv alone (checkpointed decoder: the forward's BN coefficients are reused).
+        ``bnin``: the input is the pre-BN y1 of that BatchNorm; conv(relu(bn(x)))."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
         splits = self._splits(N, S, c0 + c1, cs.cout, cs.code)
         st = b["stats"] if training and not recompute else None
-        if cs is self.convs[0] and self.stem_sup & 1:
+        if bnin is not None:
+            call("pcms_conv3_fwd_bnin", cs.code, x0, c0, bnin.scale, bnin.shift, cs.fwd, cs.mod.bias, y, st, N,
+                 *S, cs.cout)
+            rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, 0, cs.cout)
+        elif cs is self.convs[0] and self.stem_sup & 1:
             with self._timed("stem_fwd"):
                 call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2], self.stem_dense)
             rows = query("pcms_stem_fwd_rows", N, *S)
@@ -631,8 +652,12 @@ class UNetEngine:
                 call("pcms_maxpool_fwd", self.code, a2, pool_out, N, *S, blk.c1.cout)
             return
         self._conv(blk.c0, x0, c0, x1, c1, out["y1"], N, S, True, training, blk.b0, recompute)
-        call("pcms_bn_relu", self.code, out["y1"], out["a1"], blk.b0.scale, blk.b0.shift, blk.c0.cout, nvox)
-        self._conv(blk.c1, out["a1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1, recompute)
+        if self._bnin(blk, N, S):  # a1 is never stored: the second conv applies BN0 + ReLU itself
+            self._conv(blk.c1, out["y1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1, recompute,
+                       bnin=blk.b0)
+        else:
+            call("pcms_bn_relu", self.code, out["y1"], out["a1"], blk.b0.scale, blk.b0.shift, blk.c0.cout, nvox)
+            self._conv(blk.c1, out["a1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1, recompute)
         if recompute or out["a2"] is None:
             return
         if pool_out is not None:
@@ -725,8 +750,13 @@ class UNetEngine:
         elif ga2 is not None:
             self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         with self._side():
-            call("pcms_conv3_wgrad", blk.c1.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
-                 b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target, int(self._gstore))
+            if self._bnin(blk, N, S):  # x = relu(bn0(y1)), applied in the kernel's staging
+                call("pcms_conv3_wgrad_bnin", blk.c1.code, acts["y1"], blk.c0.cout, blk.b0.scale, blk.b0.shift, gY,
+                     blk.c1.mod.weight.grad, b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target,
+                     int(self._gstore))
+            else:
+                call("pcms_conv3_wgrad", blk.c1.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
+                     b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target, int(self._gstore))
         # dgrad conv1 -> grad of a1
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
         # BN0/ReLU backward -> dy1 (a second buffer: the side stream may still read gY)

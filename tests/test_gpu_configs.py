@@ -189,6 +189,30 @@ def _heartbeat(tag):
             f.write(f"{time.strftime('%H:%M:%S')} {tag}\n")
 
 
+class _Beat:
+    """_heartbeat every 30 s from a background thread (the oracle's torch ops hold the main one)."""
+
+    def __init__(self, tag):
+        import threading
+        self.tag, self.stop = tag, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        i = 0
+        while not self.stop.wait(30):
+            i += 1
+            _heartbeat(f"{self.tag} +{30 * i}s")
+
+    def __enter__(self):
+        _heartbeat(self.tag)
+        self.t.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop.set()
+        self.t.join()
+
+
 def _oracle_train_grads(sd, x, y, bf16):
     """One oracle forward / BCEDice / backward at fp32 or under CPU bf16 autocast (the
     reference's reduced-precision form): logits, loss, every gradient."""
@@ -207,20 +231,31 @@ def _oracle_train_grads(sd, x, y, bf16):
 
 def test_config5_checkpointed_bf16_vs_oracle():
     """Config 5 (1 x 5x256x256x96, decoder checkpointing, bf16) against the oracle at that
-    shape with autocast-relative bf16 bars: the train logits / masks / loss as at configs 2
-    and 4, and every gradient: its relative L2 distance to the oracle's fp32 gradient within
-    max(3x the oracle's own bf16-autocast run's distance, 2e-2) (pre-BN conv biases, exact
-    gradient 0, SURVEY H5: within 1e-4 absolute)."""
+    shape with the autocast-relative bf16 bar (train logits / masks / loss as at configs 2
+    and 4).  With PCMS_CFG5_GRADS=1 also every gradient: its relative L2 distance to the
+    oracle's fp32 gradient within max(3x the oracle's own bf16-autocast run's distance, 2e-2)
+    (pre-BN conv biases, exact gradient 0, SURVEY H5: within 1e-4 absolute).  The gradient
+    form runs the oracle's fp32 AND autocast backward at this size (minutes of host time on
+    the GPU box), so it is opt-in; its record is profiles/r4_cfg5_grad_parity.txt."""
     from oracle import unet3d_cpu as ref
     from pcms_amd.synthetic import make_batch
     torch.set_num_threads(_threads())
     b = make_batch(*CFG5, seed=1234)
     torch.manual_seed(0)
     sd = ref.init_params(5, 1)
-    _heartbeat("oracle fp32 step")
-    l32, loss32, g32 = _oracle_train_grads(sd, b["image"], b["label"], bf16=False)
-    _heartbeat("oracle bf16-autocast step")
-    lbf, lossbf, gbf = _oracle_train_grads(sd, b["image"], b["label"], bf16=True)
+    grads_too = os.environ.get("PCMS_CFG5_GRADS") == "1"
+    if not grads_too:
+        with _Beat("oracle fp32 + autocast forward"):
+            r = _oracle_forward_pair(sd, b["image"], b["label"])
+        m, lg, loss = _gpu_step("bf16", b["image"], b["label"], ckpt=True)
+        del m
+        torch.cuda.empty_cache()
+        _bf16_bar(lg, loss, r, "cfg5 ckpt")
+        return
+    with _Beat("oracle fp32 step"):
+        l32, loss32, g32 = _oracle_train_grads(sd, b["image"], b["label"], bf16=False)
+    with _Beat("oracle bf16-autocast step"):
+        lbf, lossbf, gbf = _oracle_train_grads(sd, b["image"], b["label"], bf16=True)
     _heartbeat("GPU step")
     r = {"l32": l32, "loss32": loss32, "lbf": lbf, "lossbf": lossbf}
     m, lg, loss, grads = _gpu_step("bf16", b["image"], b["label"], ckpt=True, keep_grad=True)
@@ -228,6 +263,7 @@ def test_config5_checkpointed_bf16_vs_oracle():
     torch.cuda.empty_cache()
     _bf16_bar(lg, loss, r, "cfg5 ckpt")
     worst = (0.0, "")
+    rows = []
     for k, t in g32.items():
         got = grads[k].double()
         if k.endswith(gu.PRE_BN_BIAS):
@@ -238,6 +274,10 @@ def test_config5_checkpointed_bf16_vs_oracle():
         rl = float((got - t).norm()) / nrm
         rl_auto = float((gbf[k].double() - t).norm()) / nrm
         bar = max(3 * rl_auto, 2e-2)
+        rows.append((k, rl, rl_auto))
         worst = max(worst, (rl / bar, k))
-        assert rl <= bar, (k, rl, rl_auto)
+    for k, rl, rl_auto in rows:
+        print(f"  {k:48s} rel-L2 {rl:.3e} (oracle autocast {rl_auto:.3e})")
     print(f"[cfg5 ckpt bf16] worst gradient rel-L2 / bar {worst[0]:.3f} ({worst[1]})")
+    for k, rl, rl_auto in rows:
+        assert rl <= max(3 * rl_auto, 2e-2), (k, rl, rl_auto)

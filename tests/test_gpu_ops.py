@@ -815,14 +815,19 @@ def test_stem_fwd_wgrad_bf16(N, S, cin, dense):
         guard = 4096
         dw = torch.zeros(64 * cin * 27 + guard, device=DEV)
         ws = torch.empty(L.query("pcms_stem_wgrad_ws_floats", N, *S, cin), device=DEV)
-        L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, ws, cin, N, *S)
-        torch.cuda.synchronize()
+        old = L.query("pcms_stem_wgrad_dense", 1 if dense else 0)  # the weight gradient's column form too
+        try:
+            L.call("pcms_stem_wgrad", xd, ndhwc(dy).to(DEV), dw, ws, cin, N, *S)
+            torch.cuda.synchronize()
+        finally:
+            L.query("pcms_stem_wgrad_dense", old)
         assert dw[64 * cin * 27:].abs().max().item() == 0.0
         close(dw[:64 * cin * 27].cpu().view(64, cin, 3, 3, 3), wr.grad, 1e-4, "stem wgrad")
 
 
 @pytest.mark.parametrize("N,S", [(2, (16, 16, 16)), (3, (4, 4, 16)), (1, (12, 16, 32)), (2, (32, 64, 64))])
-def test_stem_wgrad_bn_fused(N, S):
+@pytest.mark.parametrize("dense", [1, 0])
+def test_stem_wgrad_bn_fused(N, S, dense):
     """The stem's BatchNorm + ReLU backward apply fused into its weight gradient
     (pcms_stem_wgrad_bn) vs the unfused pair (pcms_bn_relu_bwd's apply pass -> dy in HBM ->
     pcms_stem_wgrad) on the same bf16 inputs -- the in-LDS dy uses the apply kernel's
@@ -830,6 +835,14 @@ def test_stem_wgrad_bn_fused(N, S):
     conv3d -> batch_norm -> relu."""
     L = _lib()
     assert L.query("pcms_stem_supported", N, *S) & 2
+    old = L.query("pcms_stem_wgrad_dense", dense)
+    try:
+        _stem_wgrad_bn_case(L, N, S)
+    finally:
+        L.query("pcms_stem_wgrad_dense", old)
+
+
+def _stem_wgrad_bn_case(L, N, S):
     g = torch.Generator().manual_seed(11 + sum(S))
     nvox = N * S[0] * S[1] * S[2]
     x = torch.rand(N, 5, *S, generator=g).to(torch.bfloat16)
@@ -924,3 +937,57 @@ def test_conv3_pack_x6_layout(flip, cout, cin):
     lo = (r - m.float()).to(torch.bfloat16)
     exp = torch.cat([h, h, m, h, lo, m], dim=3).view(torch.int16)
     assert torch.equal(got, exp)
+
+
+@pytest.mark.parametrize("N,S,C,wgs", [(2, (32, 32, 32), 64, 0), (1, (32, 32, 32), 128, 24)])
+def test_bnin_conv_and_wgrad_bit_identical(N, S, C, wgs):
+    """The BatchNorm + ReLU of a DoubleConv's first conv applied inside its second conv's
+    staging (pcms_conv3_fwd_bnin / pcms_conv3_wgrad_bnin: models/unet3d.py:31-35) against the
+    stored a1 = pcms_bn_relu(y1) fed to pcms_conv3_fwd / pcms_conv3_wgrad: bit-identical outputs,
+    BatchNorm partials and weight gradients (the same bn_relu1 arithmetic and bf16 rounding);
+    padding stays zero (relu(0 * sc + sh) would not be).  wgs > 0: a persistent grid smaller
+    than the box count (several boxes per workgroup)."""
+    L = _lib()
+    old = L.query("pcms_conv3_big_min_boxes", 1)
+    old_w = L.query("pcms_conv3_big_max_wgs", wgs)
+    try:
+        assert L.query("pcms_conv3_bnin_ok", N, *S, C, C, 256) == 1
+        g = torch.Generator().manual_seed(21)
+        nvox = N * S[0] * S[1] * S[2]
+        T = torch.bfloat16
+        y1 = (torch.randn(nvox * C, generator=g) * 2).to(T).to(DEV)
+        sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        sh = (torch.randn(C, generator=g) * 0.5).to(DEV)  # positive shifts: padding must not become relu(sh)
+        w = (torch.randn(C, C, 27, generator=g) * 0.05).to(DEV)
+        wp = torch.empty(L.query("pcms_conv3_pack_elems", 1, C, C), dtype=T, device=DEV)
+        L.call("pcms_conv3_pack", 1, w, wp, C, C, 0)
+        bias = torch.randn(C, generator=g).to(DEV)
+        dy = (torch.randn(nvox * C, generator=g)).to(T).to(DEV)
+        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, C, 0, C)
+        a1 = torch.empty_like(y1)
+        L.call("pcms_bn_relu", 1, y1, a1, sc, sh, C, nvox)
+        out = []
+        for fused in (False, True):
+            y = torch.full_like(y1, float("nan"))
+            st = torch.full((rows * (2 * C + 1),), float("nan"), device=DEV)
+            dw = torch.zeros(C * C * 27, device=DEV)
+            dwt = torch.empty(max(1, L.query("pcms_conv3_wgrad_ws_floats", 1, N, *S, C, 0, C, 256)), device=DEV)
+            if fused:
+                L.call("pcms_conv3_fwd_bnin", 1, y1, C, sc, sh, wp, bias, y, st, N, *S, C)
+                L.call("pcms_conv3_wgrad_bnin", 1, y1, C, sc, sh, dy, dw, dwt, N, *S, C, C, 256, 0)
+            else:
+                L.call("pcms_conv3_fwd", 1, a1, C, None, 0, wp, bias, y, None, C, None, st, 0, N, *S, C, 1)
+                L.call("pcms_conv3_wgrad", 1, a1, C, None, 0, dy, dw, dwt, N, *S, C, C, 256, 0)
+            torch.cuda.synchronize()
+            out.append((y.view(torch.int16).clone(), st.clone(), dw.clone()))
+        (y0, s0, d0), (y1_, s1, d1) = out
+        assert torch.equal(y0, y1_)
+        assert torch.equal(s0, s1)
+        assert torch.equal(d0, d1)
+        # and against fp64 on the rounded activation (the fused forward computes the same conv)
+        a64 = ncdhw(a1.view(N, *S, C).cpu()).double()
+        ref = F.conv3d(a64, w.view(C, C, 3, 3, 3).cpu().double(), bias.cpu().double(), padding=1)
+        close(ncdhw(y1_.view(T).view(N, *S, C).cpu()), ref, 1e-2, "fused conv vs fp64")
+    finally:
+        L.query("pcms_conv3_big_min_boxes", old)
+        L.query("pcms_conv3_big_max_wgs", old_w)

@@ -317,3 +317,45 @@ def test_fresh_gradient_store_equals_zero_fill(precision):
     BCEDiceLoss()(m(x), y).backward()  # accumulates
     torch.testing.assert_close(eng.flat_g, 2 * g_store, rtol=1e-6, atol=0)
     assert all(p.grad is not None and p.grad.data_ptr() >= eng.flat_g.data_ptr() for p in m.parameters())
+
+
+@pytest.mark.gpu
+def test_bnin_fusion_step_bit_identical():
+    """A whole bf16 training step with the DoubleConvs' first BatchNorm + ReLU fused into the
+    second conv's staging (engine.fuse_bnin, forward and weight gradient) equals the step with
+    the separate a1 = relu(bn(y1)) pass bit for bit: logits, loss, every gradient, the Adam
+    update and the BatchNorm buffers.  The big-box threshold is lowered so the fused kernels
+    run at this size (level 0: 2 x 32x32x32)."""
+    from pcms_amd import _lib as L
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    gen = torch.Generator().manual_seed(8)
+    x = torch.rand(2, 5, 32, 32, 32, generator=gen).cuda()
+    y = (torch.rand(2, 1, 32, 32, 32, generator=gen) < 0.4).float().cuda()
+    old = L.query("pcms_conv3_big_min_boxes", 1)
+    try:
+        runs = []
+        for fuse in (False, True):
+            torch.manual_seed(0)
+            m = UNet3D(n_modalities=5, n_classes=1).cuda()
+            eng = m.engine()
+            eng.fuse_bnin = fuse
+            opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
+            opt.zero_grad()
+            lg = m(x)
+            loss = BCEDiceLoss()(lg, y)
+            loss.backward()
+            g = eng.flat_g.clone()
+            opt.step()
+            torch.cuda.synchronize()
+            if fuse:
+                assert eng._bnin(eng.enc[0], 2, (32, 32, 32)), "the fused kernels did not run"
+            runs.append((lg.detach().clone(), float(loss.detach()), g, eng.flat_p.clone(), eng.flat_bn.clone()))
+        (l0, s0, g0, p0, b0), (l1, s1, g1, p1, b1) = runs
+        assert torch.equal(l0, l1) and s0 == s1
+        assert torch.equal(g0, g1)
+        assert torch.equal(p0, p1)
+        assert torch.equal(b0, b1)
+    finally:
+        L.query("pcms_conv3_big_min_boxes", old)

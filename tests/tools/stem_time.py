@@ -28,7 +28,10 @@ def main():
     fns = {"fwd": lambda s: L.call("pcms_stem_fwd", s[0], wp, bias, s[1], stats, N, D, H, W, 16),
            "fwd14": lambda s: L.call("pcms_stem_fwd", s[0], wp, bias, s[1], stats, N, D, H, W, 0),
            "wgrad": lambda s: L.call("pcms_stem_wgrad", s[0], s[2], dw, ws, 5, N, D, H, W),
-           "wgrad_bn": lambda s: L.call("pcms_stem_wgrad_bn", s[0], s[2], s[1], *bnv, coef, dw, ws, 5, N, D, H, W)}
+           "wgrad_bn": lambda s: L.call("pcms_stem_wgrad_bn", s[0], s[2], s[1], *bnv, coef, dw, ws, 5, N, D, H, W),
+           "wgrad_bn_taps": lambda s: (L.query("pcms_stem_wgrad_dense", 0),
+                                       L.call("pcms_stem_wgrad_bn", s[0], s[2], s[1], *bnv, coef, dw, ws, 5, N, D, H, W),
+                                       L.query("pcms_stem_wgrad_dense", 1))}
     res = {}
     for rep in range(3):
         for name, fn in fns.items():
@@ -43,7 +46,8 @@ def main():
             e1.synchronize()
             res.setdefault(name, []).append(e0.elapsed_time(e1) / 30 * 1e3)
     t = {k: min(v) for k, v in res.items()}
-    print(f"fwd {t['fwd']:.1f} us (14-step {t['fwd14']:.1f})  wgrad {t['wgrad']:.1f} us  wgrad_bn {t['wgrad_bn']:.1f} us  "
+    print(f"fwd {t['fwd']:.1f} us (14-step {t['fwd14']:.1f})  wgrad {t['wgrad']:.1f} us  wgrad_bn {t['wgrad_bn']:.1f} us "
+          f"(tap x 8-channel columns {t['wgrad_bn_taps']:.1f})  "
           f"frac(847.3 MB) {847.3e6 / ((t['fwd'] + t['wgrad_bn']) * 1e-6) / 8e12:.4f}"
           f"  (all: {res})", flush=True)
 
