@@ -765,7 +765,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // LDS latency is behind the MFMAs instead of in front of each pair.  Taps wave + 8 j, j < 3
   // for every wave; the fourth (waves 0-2: taps 24-26) in a uniform branch at the step's end,
   // its fragment also one step ahead (one code path: no per-variant register allocation).
-  auto compute_fixed = [&](const char* buf) __attribute__((always_inline)) {
+  auto compute_fixed = [&](const char* buf, auto&& mid) __attribute__((always_inline)) {
     constexpr int LD = LBW >= 2 ? LBD : 0, LH = LBW >= 2 ? LBH : 0, LW = LBW >= 2 ? LBW : 4;
     constexpr int HHc = (1 << LH) + 2, HWc = (1 << LW) + 2;
     constexpr int NK = (1 << (LD + LH + LW)) / 16;
@@ -806,6 +806,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     if (four) load3(0, 0);
     static_for<NK>([&](auto sc) __attribute__((always_inline)) {
       constexpr int s = decltype(sc)::value, cs = s & 1, ns = cs ^ 1;
+      if constexpr (s == NK / 2) mid();  // BNIN: the next box's BN apply under this box's MFMAs
       if constexpr (s + 1 < NK) load(s + 1, ns);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -819,10 +820,16 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       }
     });
   };
-  auto compute_box = [&](const char* buf) __attribute__((always_inline)) {
-    if constexpr (!kX3 && !kX6 && LBW >= 2) compute_fixed(buf);
-    else compute(buf);
+  // mid(): work placed halfway through the box's MFMA steps (compute_fixed), or after them
+  auto compute_box = [&](const char* buf, auto&& mid) __attribute__((always_inline)) {
+    if constexpr (!kX3 && !kX6 && LBW >= 2) {
+      compute_fixed(buf, mid);
+    } else {
+      compute(buf);
+      mid();
+    }
   };
+  auto nomid = []() __attribute__((always_inline)) {};
 
   // bf16 hot path: both tiles arrive by buffer LDS-DMA (no register staging); the next box
   // streams in while this one computes.  The dy tile keeps dy_off_bf16's half swap (applied
@@ -907,9 +914,17 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
         if (b + 1 < b_end) xm = stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
-        compute_box(wlds + cur * BUFBYTES);
+        if constexpr (BNIN) {
+          // this thread's pieces of box b + 1 have landed once its vmcnt drains (LDS-DMA
+          // completion is per wave); nobody reads buffer cur ^ 1 before the barrier below
+          compute_box(wlds + cur * BUFBYTES, [&]() __attribute__((always_inline)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (b + 1 < b_end) bn_x(wlds + (cur ^ 1) * BUFBYTES, xm);
+          });
+        } else {
+          compute_box(wlds + cur * BUFBYTES, nomid);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (BNIN) if (b + 1 < b_end) bn_x(wlds + (cur ^ 1) * BUFBYTES, xm);
         __syncthreads();
       }
     }
@@ -921,7 +936,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
         if (b + 1 < b_end) stage_load(b + 1);
-        compute_box(wlds + cur * BUFBYTES);
+        compute_box(wlds + cur * BUFBYTES, nomid);
         if (b + 1 < b_end) stage_store(wlds + (cur ^ 1) * BUFBYTES);
         __syncthreads();
       }

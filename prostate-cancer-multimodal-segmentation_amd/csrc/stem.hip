@@ -131,6 +131,45 @@ __device__ __forceinline__ void quad_transpose4(uint32_t (&d)[4], bool b0, bool 
   }
 }
 
+// L2-aware box walk of the persistent stem kernels (boxes are numbered n, d, h, w; w fastest).
+// Dispatch is round-robin over the 8 XCDs (workgroup i on XCD i % 8), each with its own 4 MB
+// L2, and a box's halo overlaps its d / h / w neighbours' (2 of BD + 2 planes, 2 of BH + 2 rows).
+// STEM_WALK 2 (the product): column walk -- every workgroup owns one (n, h, w) box column and
+// walks a d range of it (b += nbh nbw), so the 2 halo planes it shares with its previous box
+// were staged one step ago by itself; the G / 8 workgroups of one XCD hold consecutive
+// columns (h-adjacent), so the halo rows shared across h are staged by a neighbour on the same
+// XCD at the same step.  Needs G a multiple of the column count and the d ranges equal;
+// otherwise, and for STEM_WALK 1, the XCD-range walk (XCD x walks [x nbox / 8, (x + 1) nbox / 8)
+// with its G / 8 workgroups side by side), or the plain b = blockIdx.x + k G (STEM_WALK 0).
+#ifndef STEM_WALK
+#define STEM_WALK 2
+#endif
+__device__ inline void stem_box_walk(int nbox, int nbd, int hw, int& b, int& step, int& end) {
+  const int G = gridDim.x;
+  if (STEM_WALK >= 2 && (G & 7) == 0) {
+    const int ncol = nbox / nbd;  // N nbh nbw
+    const int sp = G / ncol;      // d ranges per column
+    if (sp * ncol == G && nbd % sp == 0) {
+      const int lg = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+      const int col = lg % ncol, dr = lg / ncol, dlen = nbd / sp;
+      b = ((col / hw) * nbd + dr * dlen) * hw + col % hw;
+      step = hw;
+      end = b + dlen * hw;
+      return;
+    }
+  }
+  if (STEM_WALK >= 1 && (G & 7) == 0 && (nbox & 7) == 0) {
+    const int per = nbox >> 3, x = blockIdx.x & 7;
+    b = x * per + (blockIdx.x >> 3);
+    step = G >> 3;
+    end = (x + 1) * per;
+  } else {
+    b = blockIdx.x;
+    step = G;
+    end = nbox;
+  }
+}
+
 // RELU: eval mode with the BatchNorm folded into the weights / bias (the output is the ReLU
 // activation; no statistics).
 // DENSE (<= 5 input channels, the product): K = 9 tap rows x 16 instead of 14 tap pairs x 16.
@@ -322,7 +361,8 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
   // store stream runs under the MFMAs instead of in bursts between them.
   f32x16_t prev[2][2];
   int pb = -1;  // box whose epilogue is still owed
-  int b = blockIdx.x;
+  int b, bstep, bend;
+  stem_box_walk(nbox, p.nbd, p.nbh * p.nbw, b, bstep, bend);
   // DENSE: box b's windows -> R buffer rb from halo buffer rb (two per thread)
   auto repack = [&](int rb) {
     const char* raw = lds + rb * kSDHaloBytes;
@@ -343,15 +383,15 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
       }
     }
   };
-  if (b < nbox) stage(b, 0);
-  if (DENSE && b + (int)gridDim.x < nbox) stage(b + gridDim.x, 1);
+  if (b < bend) stage(b, 0);
+  if (DENSE && b + bstep < bend) stage(b + bstep, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (DENSE) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (b < nbox) repack(0);
+    if (b < bend) repack(0);
   }
-  for (int it = 0; b < nbox; b += gridDim.x, ++it) {
+  for (int it = 0; b < bend; b += bstep, ++it) {
     // halo(b) has landed for this wave (vmcnt at the loop end); barrier: for all waves, and
     // every wave is done reading the buffer the next DMA overwrites.  A raw s_barrier, not
     // __syncthreads(): its fence would wait vmcnt(0), draining this wave's output stores
@@ -360,15 +400,15 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     STEM_STAMP(0);
-    const int bn = b + gridDim.x;
+    const int bn = b + bstep;
     // DENSE: halo(b + 2G) into the buffer halo(b) left (repacked during the previous box);
     // halo(b + G) landed at the previous box's end and is repacked during this box's MFMAs
     if constexpr (DENSE) {
-      if (bn + (int)gridDim.x < nbox) stage(bn + gridDim.x, it & 1);
+      if (bn + bstep < bend) stage(bn + bstep, it & 1);
     } else {
-      if (bn < nbox) stage(bn, (it + 1) & 1);
+      if (bn < bend) stage(bn, (it + 1) & 1);
     }
-    const int rp = DENSE && bn < nbox ? (it + 1) & 1 : -1;  // R / halo buffer repacked this box
+    const int rp = DENSE && bn < bend ? (it + 1) & 1 : -1;  // R / halo buffer repacked this box
     const int rcur = (it & 1) * kSDRBytes;                  // DENSE: this box's R buffer
     STEM_STAMP(1);
     const bool interleave = pb >= 0 && is_full(pb);
@@ -793,19 +833,19 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
     }
   };
 
-  const int G = gridDim.x;
-  int b = blockIdx.x;
+  int b, G, bend;  // G: this workgroup's box stride
+  stem_box_walk(nbox, nbd, nbh * nbw, b, G, bend);
   static_assert(!BN || NS == 3, "the y loads sit between the DMA of two consecutive boxes");
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k) {
-    if (b + k * G < nbox) stage(b + k * G, k);
-    if (BN && k == 0 && b < nbox) load_y(b);  // order: DMA(b), y(b), DMA(b + G)
+    if (b + k * G < bend) stage(b + k * G, k);
+    if (BN && k == 0 && b < bend) load_y(b);  // order: DMA(b), y(b), DMA(b + G)
   }
-  for (int it = 0; b < nbox; b += G, ++it) {
+  for (int it = 0; b < bend; b += G, ++it) {
     // retire box b's DMA (the NS - 2 boxes after it may stay in flight), then barrier:
     // every wave's share of box b has landed and every wave is done reading the slot
     // refilled below
-    if (b + (NS - 2) * G < nbox) {
+    if (b + (NS - 2) * G < bend) {
       if (nxp == XI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + XI)) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (Gm::DYP + XI - 1)) : "memory");
     } else {
@@ -819,9 +859,9 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
       // box b's da tile and y chunks have landed: this wave's dy in place, then the next box's
       // y loads (before the DMA of box b + 2 G: the wait above stays a count of that DMA alone)
       transform(swl + (it % NS) * kSWBuf);
-      if (b + G < nbox) load_y(b + G);
+      if (b + G < bend) load_y(b + G);
     }
-    if (b2 < nbox) stage(b2, (it + NS - 1) % NS);
+    if (b2 < bend) stage(b2, (it + NS - 1) % NS);
     if constexpr (DENSE) {  // every thread's windows (and own dy) written before any MFMA reads them
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -916,7 +956,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* par
 
 // the dense-column stem weight gradient for <= 5 input channels (1, the product) or the
 // 28-tap x 8-channel columns (0: A/B); pcms_stem_wgrad_dense sets it
-static int g_stem_wgrad_dense = 1;
+static int g_stem_wgrad_dense = 0;
 
 // the dedicated stem kernels' shape conditions (other shapes take the general conv kernels)
 static bool stem_fwd_direct_shape(int N, int D, int H, int W) {

@@ -133,6 +133,7 @@ class UNetEngine:
         # slabs, BN partial rows, weight-gradient partial rows), so the recomputed tensors are
         # bit-identical to the forward's and two identical steps give identical results.
         self.act_ckpt = False
+        self.split_target = 384  # split-K conv launches (levels 2-4): workgroups aimed at
         self.wgrad_target = 256  # conv weight-gradient workgroups: one round of 1 WG per CU (fewer partial rows to reduce than 512)
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
         self.kernel_timer = None  # dict name -> [(start, end) events] (bench.py roofline timing)
@@ -578,16 +579,19 @@ class UNetEngine:
         nch = -(-cin // query("pcms_conv3_chunk", code))
         if wgs >= 192 or nch == 1 or wgs == 0:
             return 1
-        return max(1, min(nch, -(-384 // wgs)))
+        return max(1, min(nch, -(-self.split_target // wgs)))
 
     def _bnin(self, blk: BlockSpec, N, S) -> bool:
         """The block's first BN + ReLU fused into its second conv (forward and weight gradient)?"""
         if not self.fuse_bnin or self.code != BF16:
             return False
-        key = (id(blk), N, tuple(S), self.wgrad_target)
+        key = (id(blk), N, tuple(S), self.wgrad_target, self.split_target)
         if key not in self._bnin_cache:
+            # only where the unfused conv runs unsplit (the same big-box kernel, so the fused
+            # step stays bit-identical to the unfused one)
             self._bnin_cache[key] = bool(query("pcms_conv3_bnin_ok", N, *S, blk.c1.cin, blk.c1.cout,
-                                               self.wgrad_target))
+                                               self.wgrad_target)) and \
+                self._splits(N, S, blk.c1.cin, blk.c1.cout, self.code) == 1
         return self._bnin_cache[key]
 
     def _conv(self, cs: ConvSpec, x0, c0, x1, c1, y, N, S, stats: bool, training: bool, bn: BNSpec,

@@ -10,7 +10,7 @@ import os
 import sys
 
 csv.field_size_limit(sys.maxsize)
-KERNELS = {"fwd": "stem_fwd_direct_kernel", "wgrad": "stem_wgrad_stream_kernel<4, 3, true>",
+KERNELS = {"fwd": "stem_fwd_direct_kernel", "wgrad": "stem_wgrad_stream_kernel<4, 3, true",
            "reduce": "stem_wgrad_reduce_kernel"}
 
 

@@ -137,7 +137,7 @@ def test_grad_scaler_step_skip_and_scale_update():
     p_before = amp.model.engine().flat_p.clone()
     sc = amp.scaler
     eng = amp.model.engine()
-    amp.optimizer.zero_grad()
+    amp.optimizer.zero_grad(set_to_none=False)  # grads stay attached (zeroed), as after a backward
     eng.flat_g[123] = float("inf")
     sc.unscale_(amp.optimizer)
     sc.step(amp.optimizer)
@@ -324,16 +324,16 @@ def test_bnin_fusion_step_bit_identical():
     """A whole bf16 training step with the DoubleConvs' first BatchNorm + ReLU fused into the
     second conv's staging (engine.fuse_bnin, forward and weight gradient) equals the step with
     the separate a1 = relu(bn(y1)) pass bit for bit: logits, loss, every gradient, the Adam
-    update and the BatchNorm buffers.  The big-box threshold is lowered so the fused kernels
-    run at this size (level 0: 2 x 32x32x32)."""
+    update and the BatchNorm buffers (level 0: 2 x 64x64x32, the fused kernels' smallest
+    unsplit big-box size)."""
     from pcms_amd import _lib as L
     from pcms_amd.models.unet3d import UNet3D
     from pcms_amd.optim import FlatAdam
     from pcms_amd.utils.losses import BCEDiceLoss
     gen = torch.Generator().manual_seed(8)
-    x = torch.rand(2, 5, 32, 32, 32, generator=gen).cuda()
-    y = (torch.rand(2, 1, 32, 32, 32, generator=gen) < 0.4).float().cuda()
-    old = L.query("pcms_conv3_big_min_boxes", 1)
+    x = torch.rand(2, 5, 64, 64, 32, generator=gen).cuda()
+    y = (torch.rand(2, 1, 64, 64, 32, generator=gen) < 0.4).float().cuda()
+    old = L.query("pcms_conv3_big_min_boxes", -1)
     try:
         runs = []
         for fuse in (False, True):
@@ -350,7 +350,7 @@ def test_bnin_fusion_step_bit_identical():
             opt.step()
             torch.cuda.synchronize()
             if fuse:
-                assert eng._bnin(eng.enc[0], 2, (32, 32, 32)), "the fused kernels did not run"
+                assert eng._bnin(eng.enc[0], 2, (64, 64, 32)), "the fused kernels did not run"
             runs.append((lg.detach().clone(), float(loss.detach()), g, eng.flat_p.clone(), eng.flat_bn.clone()))
         (l0, s0, g0, p0, b0), (l1, s1, g1, p1, b1) = runs
         assert torch.equal(l0, l1) and s0 == s1

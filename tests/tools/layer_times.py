@@ -19,6 +19,10 @@ def flops(name, a):
         return 2 * 27 * (a[2] + a[4]) * a[17] * a[13] * a[14] * a[15] * a[16]
     if name == "pcms_conv3_wgrad":
         return 2 * 27 * (a[2] + a[4]) * a[12] * a[8] * a[9] * a[10] * a[11]
+    if name == "pcms_conv3_fwd_bnin":
+        return 2 * 27 * a[2] * a[13] * a[9] * a[10] * a[11] * a[12]
+    if name == "pcms_conv3_wgrad_bnin":
+        return 2 * 27 * a[2] * a[12] * a[8] * a[9] * a[10] * a[11]
     if name == "pcms_stem_fwd":
         return 2 * 27 * 5 * 64 * a[5] * a[6] * a[7] * a[8]
     if name == "pcms_stem_wgrad":
@@ -37,6 +41,10 @@ def desc(name, a):
         return f"{a[2]}+{a[4]}->{a[12]} {a[9]}x{a[10]}x{a[11]}"
     if name == "pcms_convt_dgrad":
         return f"{a[8]}->{a[9]} {a[5]}x{a[6]}x{a[7]}"
+    if name == "pcms_conv3_fwd_bnin":
+        return f"bn({a[2]})->{a[13]} {a[10]}x{a[11]}x{a[12]}"
+    if name == "pcms_conv3_wgrad_bnin":
+        return f"bn({a[2]})->{a[12]} {a[9]}x{a[10]}x{a[11]}"
     if name in ("pcms_convt_fwd", "pcms_convt_wgrad", "pcms_convt_dgrad_ws"):
         return f"{a[9]}->{a[10]} {a[6]}x{a[7]}x{a[8]}"
     return ""
@@ -51,6 +59,7 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="fp32: the conv MFMA fraction counts the bf16x6 work (6 bf16 MFMA products per product)")
     ap.add_argument("--wgrad-target", type=int, default=0, help="engine.wgrad_target override")
+    ap.add_argument("--split-target", type=int, default=0, help="engine.split_target override")
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
     from pcms_amd import engine as E
@@ -63,6 +72,8 @@ def main():
     xf = 6 if a.precision == "fp32" else 1  # bf16 MFMA work per FLOP of the 3x3x3 convs
     if a.wgrad_target:
         tr.model.engine().wgrad_target = a.wgrad_target
+    if a.split_target:
+        tr.model.engine().split_target = a.split_target
     b = make_batch(a.batch, spatial, seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
     for _ in range(3):

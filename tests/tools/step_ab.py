@@ -1,0 +1,78 @@
+"""In-step A/B of engine knobs on ONE box (test tooling): the bench workload (2 x 5x128x128x64,
+BCEDice, Adam) stepped with each variant in turn, rounds interleaved so box drift hits every
+variant alike; HIP events around K back-to-back steps, median over rounds.
+
+    python tests/tools/step_ab.py [--rounds 4] [--steps 10] [--variants base,nobnin,...]
+
+Variants: base (the defaults), nobnin (engine.fuse_bnin off), densewg (stem weight gradient
+in the dense-column form), split256 / split512 (engine.split_target)."""
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--variants", default="base,nobnin,densewg")
+    a = ap.parse_args()
+    import pcms_amd  # noqa: F401
+    from pcms_amd import _lib as L
+    from pcms_amd.synthetic import make_batch
+    from pcms_amd.utils.trainer import Trainer
+    torch.manual_seed(0)
+    tr = Trainer({"device": "cuda", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1,
+                  "loss": "bce_dice", "precision": "bf16"})
+    eng = tr.model.engine()
+    b = make_batch(2, (128, 128, 64), seed=1)
+    batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
+    dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target}
+    dense0 = L.query("pcms_stem_wgrad_dense", -1)
+
+    def setup(v):
+        eng.fuse_bnin, eng.split_target = dflt["fuse_bnin"], dflt["split_target"]
+        L.query("pcms_stem_wgrad_dense", dense0)
+        if v == "nobnin":
+            eng.fuse_bnin = False
+        elif v == "bnin":
+            eng.fuse_bnin = True
+        elif v == "densewg":
+            L.query("pcms_stem_wgrad_dense", 1)
+        elif v == "tapswg":
+            L.query("pcms_stem_wgrad_dense", 0)
+        elif v.startswith("split"):
+            eng.split_target = int(v[5:])
+        elif v != "base":
+            raise SystemExit(f"unknown variant {v}")
+
+    names = a.variants.split(",")
+    res = {v: [] for v in names}
+    for r in range(a.rounds):
+        for v in names:
+            setup(v)
+            for _ in range(2):
+                tr.step(batch)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.steps):
+                tr.step(batch)
+            e1.record()
+            e1.synchronize()
+            res[v].append(e0.elapsed_time(e1) / a.steps)
+        print(f"round {r}: " + "  ".join(f"{v} {res[v][-1]:.3f}" for v in names), flush=True)
+    base = statistics.median(res[names[0]])
+    for v in names:
+        m = statistics.median(res[v])
+        print(f"{v:10s} median {m:.3f} ms/step  ({m / base - 1:+.2%} vs {names[0]})  all {[round(x, 3) for x in res[v]]}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
