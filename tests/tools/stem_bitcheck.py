@@ -1,6 +1,6 @@
 """Bit-for-bit comparison of the stem kernels of two builds of the library (test tooling):
-the product library against a variant (``$1``, a file under the package directory, built by
-tests/tools/ab_build.sh).  A store / schedule change of pcms_stem_fwd or pcms_stem_wgrad_bn
+the product library (or ``$2``) against a variant (``$1``; files under the package directory,
+built by tests/tools/ab_build.sh).  A store / schedule change of pcms_stem_fwd or pcms_stem_wgrad_bn
 must leave every output byte unchanged; prints one line per shape and exits non-zero on a
 difference."""
 import ctypes
@@ -64,8 +64,9 @@ def run(call, N, S, seed):
 
 
 def main():
-    a = bind(os.path.join(REPO, "prostate-cancer-multimodal-segmentation_amd", "libpcms_hip.so"))
-    b = bind(os.path.join(REPO, "prostate-cancer-multimodal-segmentation_amd", sys.argv[1]))
+    pkg = os.path.join(REPO, "prostate-cancer-multimodal-segmentation_amd")
+    a = bind(os.path.join(pkg, sys.argv[2] if len(sys.argv) > 2 else "libpcms_hip.so"))
+    b = bind(os.path.join(pkg, sys.argv[1]))
     bad = 0
     for N, S in ((1, (12, 16, 32)), (3, (4, 4, 16)), (1, (32, 64, 64)), (2, (128, 128, 64))):
         ra, rb = run(a, N, S, 7), run(b, N, S, 7)
