@@ -54,11 +54,17 @@ def main():
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b) * 1e3)
         us = sorted(ts)[2]
+        # the clock the CUs ran at during the last launch: shader-clock ticks / 100 MHz ticks
+        clk = (ctypes.c_ulonglong * (4 * grid))()
+        mhz = float("nan")
+        if ex.probe_clocks(clk, grid) == 0:
+            c = [(clk[4 * i + 1] - clk[4 * i]) / max(1, clk[4 * i + 3] - clk[4 * i + 2]) * 100.0 for i in range(grid)]
+            mhz = sorted(c)[len(c) // 2]
         wide = F & 8
         per_box = 0 if F & 256 else (0 if F & 32 else 256 * 128) + (0 if F & 16 else 600 * (128 if wide else 64))
         gbs = grid * 64 * per_box / (us * 1e-6) / 1e9
         print(f"F={F:3d} {name:34s} {us:8.1f} us  {per_box / 1024:5.1f} KB/box  {gbs / 256:6.1f} GB/s/CU  "
-              f"{us / 64:5.2f} us/box", flush=True)
+              f"{us / 64:5.2f} us/box  clock {mhz:6.0f} MHz", flush=True)
 
 
 if __name__ == "__main__":
