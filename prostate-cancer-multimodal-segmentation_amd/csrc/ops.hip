@@ -643,6 +643,8 @@ __global__ void __launch_bounds__(TPB) box_channel_sum_kernel(const T* x, float*
 // out[c] += sum_r part[r][c] in a fixed order (deterministic).  Block = 8 columns x 32 row
 // lanes: lane l sums rows l, l + 32, ... (4 independent chains); the 32 lane sums are
 // added by a fixed LDS tree.
+// ACC: out[c] += the column sum (false: out[c] = it -- no zero fill of out first)
+template <bool ACC>
 __global__ void __launch_bounds__(256) rows_sum_kernel(const float* part, int rows, int C, float* out) {
   __shared__ float red[32][9];
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -662,7 +664,7 @@ __global__ void __launch_bounds__(256) rows_sum_kernel(const float* part, int ro
     if (rl < w) red[rl][cl] += red[rl + w][cl];
     __syncthreads();
   }
-  if (rl == 0 && c < C) out[c] += red[0][cl];
+  if (rl == 0 && c < C) out[c] = ACC ? out[c] + red[0][cl] : red[0][cl];
 }
 
 // ---------------- output head: logits (NCDHW fp32) = b + a . w ----------------
@@ -1449,7 +1451,7 @@ int pcms_box_channel_sum(int dtype, const void* x, float* out, float* ws, int N,
   else hipLaunchKernelGGL(box_channel_sum_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)x, ws, N, D, H, W, C, z0, y0, x0, bd, bh, bw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(rows_sum_kernel, dim3(cdiv(C, 8)), dim3(256), 0, s, (const float*)ws, grid, C, out);
+  hipLaunchKernelGGL(rows_sum_kernel<true>, dim3(cdiv(C, 8)), dim3(256), 0, s, (const float*)ws, grid, C, out);
   PCMS_CHECK_LAUNCH();
 }
 
@@ -1488,8 +1490,8 @@ static int head_bwd_rows(long nvox) { return grid_for(nvox * 8, TPB, 2048); }
 // the head partial rows [grid][ncls][65] -> dw[k][c] += (k, c), db[k] += (k, 64)
 static int head_finish(int grid, float* ws, int ncls, float* dw, float* db, hipStream_t s) {
   float* sums = ws + (long)grid * ncls * 65;
-  (void)hipMemsetAsync(sums, 0, sizeof(float) * ncls * 65, s);
-  hipLaunchKernelGGL(rows_sum_kernel, dim3(cdiv(ncls * 65, 8)), dim3(256), 0, s, (const float*)ws, grid, ncls * 65, sums);
+  hipLaunchKernelGGL(rows_sum_kernel<false>, dim3(cdiv(ncls * 65, 8)), dim3(256), 0, s, (const float*)ws, grid, ncls * 65,
+                     sums);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(head_bwd_finish_kernel, dim3(1), dim3(320), 0, s, (const float*)sums, ncls, dw, db);

@@ -708,14 +708,14 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
   const int tq = lane & 3, trs = lane >> 2;
   const int tcol = ((ct ^ ((trs >> 1) & 1)) * 64) + tq * 16;  // byte offset in the 128-B row
   const int tch = ct * 32 + tq * 8;                            // first logical channel
-  float bsc[8], bsh[8], bmu[8], bis[8], bk1[8], bk2[8], bk3[8];
+  float bsc[8], bsh[8], bmu[8], bk1[8], bka[8], bk3[8];  // bka = k2 invstd
   u32x4_t yreg[kTR];
   if constexpr (BN) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = tch + j;
-      bsc[j] = bn.scale[c]; bsh[j] = bn.shift[c]; bmu[j] = bn.mean[c]; bis[j] = bn.invstd[c];
-      bk1[j] = bn.coef[3 * c]; bk2[j] = bn.coef[3 * c + 1]; bk3[j] = bn.coef[3 * c + 2];
+      bsc[j] = bn.scale[c]; bsh[j] = bn.shift[c]; bmu[j] = bn.mean[c];
+      bk1[j] = bn.coef[3 * c]; bka[j] = bn.coef[3 * c + 1] * bn.invstd[c]; bk3[j] = bn.coef[3 * c + 2];
     }
   }
   // y chunks of box b into registers (plain global loads: counted by vmcnt like the DMA);
@@ -744,7 +744,7 @@ __global__ void __launch_bounds__(kSWT, 1) stem_wgrad_stream_kernel(const bf16_t
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float gg = (yv[j] * bsc[j] + bsh[j] > 0.f) ? ga[j] : 0.f;
-        o[j] = bk1[j] * gg + bk2[j] * ((yv[j] - bmu[j]) * bis[j]) + bk3[j];
+        o[j] = bk1[j] * gg + (bka[j] * (yv[j] - bmu[j]) + bk3[j]);  // centred: no cancellation at |mean| >> std
       }
       u32x4_t ov;
 #pragma unroll

@@ -52,6 +52,7 @@ class BaseTrainer:
     def __init__(self, config: dict, train_loader: Optional[Iterable] = None,
                  val_loader: Optional[Iterable] = None, model: Optional[UNet3D] = None):
         self.config = config
+        self._bw_seed = None  # the backward's ones seed, reused (see step)
         self.device = torch.device(config.get("device", "cuda"))
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -149,7 +150,13 @@ class BaseTrainer:
         try:
             outputs = self.model(images)
             loss = self.criterion(outputs, labels)
-            (self.scaler.scale(loss) if self.scaler is not None else loss).backward()
+            root = self.scaler.scale(loss) if self.scaler is not None else loss
+            # the backward's seed gradient held across steps (loss.backward() would fill a fresh
+            # ones tensor on the device every step)
+            seed = self._bw_seed
+            if seed is None or seed.dtype != root.dtype or seed.device != root.device or seed.shape != root.shape:
+                seed = self._bw_seed = torch.ones_like(root)
+            torch.autograd.backward(root, grad_tensors=seed)
         except BaseException:
             if self.distributed:
                 sync.reset()
