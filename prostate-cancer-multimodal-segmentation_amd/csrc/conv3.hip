@@ -40,13 +40,14 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r_lane = lane & 31, hsel = lane >> 5;
-  int mb = blockIdx.x;
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  int mb = bx;
   const int bwi = mb % p.nbw; mb /= p.nbw;
   const int bhi = mb % p.nbh; mb /= p.nbh;
   const int bdi = mb % p.nbd;
   const int n = mb / p.nbd;
-  const int co_base = blockIdx.y * 64;
-  const int cbeg = blockIdx.z * p.chunks_per_split;
+  const int co_base = by * 64;
+  const int cbeg = bz * p.chunks_per_split;
   const int cend = min(p.nchunk, cbeg + p.chunks_per_split);
   const int bd = 1 << lbd_, bh = 1 << lbh_, bw = 1 << lbw_;
   const int boxvol = bd * bh * bw;
@@ -320,7 +321,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
           const int co = co_base + nt * 32 + r_lane;
           float v = acc[mt][nt][e];
           if (p.yacc) {  // split-K: this split's own fp32 slab (summed in a fixed order later)
-            p.yacc[((long)blockIdx.z * p.nvox + vox) * p.Cout + co] = v;
+            p.yacc[((long)bz * p.nvox + vox) * p.Cout + co] = v;
             continue;
           }
           v += bias_l[nt];
@@ -393,10 +394,10 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
         }
       }
       if (Nn > 0.f) M2 -= sdd * sdd / Nn;
-      float* st = p.stats + ((long)blockIdx.x * p.Cout + co_base + tid) * 2;
+      float* st = p.stats + ((long)bx * p.Cout + co_base + tid) * 2;
       st[0] = S;
       st[1] = M2;
-      if (tid == 0 && blockIdx.y == 0) p.stats[(long)gridDim.x * p.Cout * 2 + blockIdx.x] = Nn;
+      if (tid == 0 && by == 0) p.stats[(long)gridDim.x * p.Cout * 2 + bx] = Nn;
     }
   }
 }
