@@ -35,7 +35,7 @@ def main():
     rec = {"shape": [2, 128, 128, 64], "kernels": list(KERNELS.values()),
            # the roofline kernel string bench.py reports for this pair (it uses the record only
            # when they match)
-           "kernel": "stem conv3d 5->64 fwd + wgrad with the BN0 backward apply fused in (stem_fwd_direct_kernel + "
+           "kernel": "stem conv3d 5->64 fwd + wgrad with the BN0 backward apply fused in (stem_fwd_direct_kernel<DENSE> + "
                      "stem_wgrad_stream_kernel<BN>)",
            "FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "dispatches": {"fetch": nf, "write": nw},
            "correction": "FETCH_SIZE x2 (gfx950 reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md "
