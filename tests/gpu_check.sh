@@ -10,7 +10,7 @@ stop_if_bad() {  # $1 = step name, $2 = status
   if [ "$2" -gt 1 ]; then echo "$1 ended with status $2: stopping"; exit "$2"; fi
 }
 if [ "$2" != "--no-tests" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread \
     -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1
   rc=$?
   echo "tests_rc=$rc"; grep -E "passed|failed|error" gpurun_out/tests_$TAG.log | tail -3

@@ -232,18 +232,19 @@ def _oracle_train_grads(sd, x, y, bf16):
 def test_config5_checkpointed_bf16_vs_oracle():
     """Config 5 (1 x 5x256x256x96, decoder checkpointing, bf16) against the oracle at that
     shape with the autocast-relative bf16 bar (train logits / masks / loss as at configs 2
-    and 4).  With PCMS_CFG5_GRADS=1 also every gradient: its relative L2 distance to the
-    oracle's fp32 gradient within max(3x the oracle's own bf16-autocast run's distance, 2e-2)
-    (pre-BN conv biases, exact gradient 0, SURVEY H5: within 1e-4 absolute).  The gradient
-    form runs the oracle's fp32 AND autocast backward at this size (minutes of host time on
-    the GPU box), so it is opt-in; its record is profiles/r4_cfg5_grad_parity.txt."""
+    and 4), and every gradient: its relative L2 distance to the oracle's fp32 gradient within
+    max(3x the oracle's own bf16-autocast run's distance, 2e-2) (pre-BN conv biases, exact
+    gradient 0, SURVEY H5: within 1e-4 absolute).  The gradient form runs the oracle's fp32 AND
+    autocast backward at this size (~4 minutes of host time on the GPU box, with a heartbeat
+    file under gpurun_out/); PCMS_CFG5_GRADS=0 keeps the forward checks only.  Record:
+    profiles/r4_cfg5_grad_parity.txt."""
     from oracle import unet3d_cpu as ref
     from pcms_amd.synthetic import make_batch
     torch.set_num_threads(_threads())
     b = make_batch(*CFG5, seed=1234)
     torch.manual_seed(0)
     sd = ref.init_params(5, 1)
-    grads_too = os.environ.get("PCMS_CFG5_GRADS") == "1"
+    grads_too = os.environ.get("PCMS_CFG5_GRADS", "1") != "0"
     if not grads_too:
         with _Beat("oracle fp32 + autocast forward"):
             r = _oracle_forward_pair(sd, b["image"], b["label"])
