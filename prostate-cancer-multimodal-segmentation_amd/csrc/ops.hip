@@ -692,6 +692,23 @@ __device__ __forceinline__ void head_st(T* p, const float (&x)[8]) {
 // BatchNorm + ReLU itself (models/unet3d.py:37-39 fused into :222): a = round_T(relu(y sc +
 // sh)), the value the bn_relu pass would have stored, so the logits are bit-identical and
 // the a2 tensor (the largest activation of the step) is never written or read.
+// voxel v of an (N, nvox) grid as (sample q, voxel-in-sample r), stepped without a division
+// per voxel (the heads index the NCDHW logit gradient by both; a runtime 32-bit division per
+// lane and voxel was a large share of their VALU)
+struct VoxQR {
+  uint32_t q, r, nv;
+  __device__ VoxQR(long v, long nvox) : q((uint32_t)(v / nvox)), r((uint32_t)(v % nvox)), nv((uint32_t)nvox) {}
+  __device__ void advance(uint32_t k) {
+    r += k;
+    while (r >= nv) { r -= nv; ++q; }
+  }
+  __device__ VoxQR plus(uint32_t k) const {
+    VoxQR o = *this;
+    o.advance(k);
+    return o;
+  }
+};
+
 template <typename T, bool NT, bool BN, int NC>
 __global__ void __launch_bounds__(TPB, 3) head_fwd_kernel(const T* a, const float* w, const float* b, float* logits,
                                                        long nvox_per_n, int N, int act, float thr,
@@ -705,12 +722,11 @@ __global__ void __launch_bounds__(TPB, 3) head_fwd_kernel(const T* a, const floa
 #pragma unroll
     for (int k = 0; k < NC; ++k) wk[k][j] = w[k * 64 + sub * 8 + j];
   }
-  auto one = [&](long v, float (&x)[8]) {
+  auto one = [&](const VoxQR& p, float (&x)[8]) {
     if constexpr (BN) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = round_st<T>(bn_relu1(x[j], sc[j], sh[j]));
     }
-    const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       float s = 0.f;
@@ -725,23 +741,26 @@ __global__ void __launch_bounds__(TPB, 3) head_fwd_kernel(const T* a, const floa
           const float pr = 1.f / (1.f + expf(-o));
           o = act == 1 ? pr : (pr > thr ? 1.f : 0.f);
         }
-        logits[(n * NC + k) * nvox_per_n + vv] = o;
+        logits[((long)p.q * NC + k) * nvox_per_n + p.r] = o;
       }
     }
   };
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
+  VoxQR pv(v, nvox_per_n);
   for (; v + (kHU - 1) * stride < total; v += kHU * stride) {
     float x[kHU][8];
 #pragma unroll
     for (int u = 0; u < kHU; ++u) head_ld<T, NT>(a + (v + u * stride) * 64 + sub * 8, x[u]);
 #pragma unroll
-    for (int u = 0; u < kHU; ++u) one(v + u * stride, x[u]);
+    for (int u = 0; u < kHU; ++u) one(u ? pv.plus((uint32_t)(u * stride)) : pv, x[u]);
+    pv.advance((uint32_t)(kHU * stride));
   }
   for (; v < total; v += stride) {
     float x[8];
     head_ld<T, NT>(a + v * 64 + sub * 8, x);
-    one(v, x);
+    one(pv, x);
+    pv.advance((uint32_t)stride);
   }
 }
 
@@ -777,10 +796,9 @@ __global__ void __launch_bounds__(TPB, (BN && NC > 2) ? 2 : 3) head_bwd_kernel(c
   }
 #pragma unroll
   for (int k = 0; k < NC; ++k) accb[k] = 0.f;
-  auto ld_dl = [&](long v, float (&dl)[NC]) {
-    const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
+  auto ld_dl = [&](const VoxQR& p, float (&dl)[NC]) {
 #pragma unroll
-    for (int k = 0; k < NC; ++k) dl[k] = dlogits[(n * NC + k) * nvox_per_n + vv];
+    for (int k = 0; k < NC; ++k) dl[k] = dlogits[((long)p.q * NC + k) * nvox_per_n + p.r];
   };
   auto one = [&](long v, const float (&x)[8], const float (&dl)[NC]) {
     float o[8], av[8];
@@ -812,6 +830,7 @@ __global__ void __launch_bounds__(TPB, (BN && NC > 2) ? 2 : 3) head_bwd_kernel(c
   };
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
+  VoxQR pv(v, nvox_per_n);
   constexpr int U = NC > 2 ? 1 : (BN || NC > 1) ? 2 : kHU;  // (registers: the BN form holds 6 x 8 per-channel values)
 #pragma unroll 1
   for (; v + (U - 1) * stride < total; v += U * stride) {
@@ -819,16 +838,18 @@ __global__ void __launch_bounds__(TPB, (BN && NC > 2) ? 2 : 3) head_bwd_kernel(c
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       head_ld<T, NT>(a + (v + u * stride) * 64 + sub * 8, x[u]);
-      ld_dl(v + u * stride, dl[u]);
+      ld_dl(u ? pv.plus((uint32_t)(u * stride)) : pv, dl[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) one(v + u * stride, x[u], dl[u]);
+    pv.advance((uint32_t)(U * stride));
   }
   for (; v < total; v += stride) {
     float x[8], dl[NC];
     head_ld<T, NT>(a + v * 64 + sub * 8, x);
-    ld_dl(v, dl);
+    ld_dl(pv, dl);
     one(v, x, dl);
+    pv.advance((uint32_t)stride);
   }
   // reduce accw over the 8 voxel-lanes of each wave that share `sub`
 #pragma unroll
@@ -898,10 +919,9 @@ __global__ void __launch_bounds__(TPB, 2) head_bn_apply_kernel(const T* y, const
 #pragma unroll
     for (int k = 0; k < NC; ++k) wk[k][j] = w[k * 64 + c];
   }
-  auto ld_dl = [&](long v, float (&dl)[NC]) {
-    const uint32_t n = (uint32_t)v / (uint32_t)nvox_per_n, vv = (uint32_t)v % (uint32_t)nvox_per_n;
+  auto ld_dl = [&](const VoxQR& p, float (&dl)[NC]) {
 #pragma unroll
-    for (int k = 0; k < NC; ++k) dl[k] = dlogits[(n * NC + k) * nvox_per_n + vv];
+    for (int k = 0; k < NC; ++k) dl[k] = dlogits[((long)p.q * NC + k) * nvox_per_n + p.r];
   };
   auto one = [&](long v, const float (&x)[8], const float (&dl)[NC]) {
     float o[8];
@@ -920,6 +940,7 @@ __global__ void __launch_bounds__(TPB, 2) head_bn_apply_kernel(const T* y, const
   };
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
+  VoxQR pv(v, nvox_per_n);
   constexpr int U = NC > 1 ? 1 : 2;  // (registers: 5 x 8 per-channel values + NC x 8 weights held)
 #pragma unroll 1
   for (; v + (U - 1) * stride < total; v += U * stride) {
@@ -927,16 +948,18 @@ __global__ void __launch_bounds__(TPB, 2) head_bn_apply_kernel(const T* y, const
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       head_ld<T, NT>(y + (v + u * stride) * 64 + sub * 8, x[u]);
-      ld_dl(v + u * stride, dl[u]);
+      ld_dl(u ? pv.plus((uint32_t)(u * stride)) : pv, dl[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) one(v + u * stride, x[u], dl[u]);
+    pv.advance((uint32_t)(U * stride));
   }
   for (; v < total; v += stride) {
     float x[8], dl[NC];
     head_ld<T, NT>(y + v * 64 + sub * 8, x);
-    ld_dl(v, dl);
+    ld_dl(pv, dl);
     one(v, x, dl);
+    pv.advance((uint32_t)stride);
   }
 }
 
