@@ -286,34 +286,38 @@ __global__ void bn_bwd_finalize_kernel(const double* ws, int C, double count, co
 // rl, rl + 4, ... in order (8 rows' loads in flight), the 4 lanes summed in a fixed order
 // (deterministic).  Saves the second launch of the two-stage path (~5 us each, 36 per step).
 constexpr int kSmallRows = 512;
+// 16 row lanes x 64 channels per block: a thread sums every 16th partial row, 8 rows' loads
+// in flight per trip (the sums were latency-bound chains of ~rows / 32 dependent trips on 4
+// row lanes); the 16 lane sums are added in lane order
+constexpr int kCfRL = 16;
 template <bool BWD>
-__global__ void __launch_bounds__(256) colsum_finalize_small_kernel(
+__global__ void __launch_bounds__(64 * kCfRL) colsum_finalize_small_kernel(
     const float* part, int rows, int C, const float* cnt, double count, const float* gamma, const float* beta,
     float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* scale, float* shift,
     float* mean_out, float* invstd, float* dgamma, float* dbeta, float* coef) {
-  __shared__ double red[4][64][2];
+  __shared__ double red[kCfRL][64][2];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   if (!BWD && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     int r = rl;
-    for (; r + 28 < rows; r += 32) {
+    for (; r + 7 * kCfRL < rows; r += 8 * kCfRL) {
       float2 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(part + ((long)(r + 4 * u) * C + c) * 2);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(part + ((long)(r + kCfRL * u) * C + c) * 2);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         s1 += (double)v[u].x;
         if (cnt) {
-          const double n = (double)cnt[r + 4 * u];
+          const double n = (double)cnt[r + kCfRL * u];
           s2 += (double)v[u].y + (n > 0.0 ? (double)v[u].x * (double)v[u].x / n : 0.0);
         } else {
           s2 += (double)v[u].y;
         }
       }
     }
-    for (; r < rows; r += 4) {
+    for (; r < rows; r += kCfRL) {
       const float2 v = *reinterpret_cast<const float2*>(part + ((long)r * C + c) * 2);
       s1 += (double)v.x;
       if (cnt) {
@@ -328,7 +332,7 @@ __global__ void __launch_bounds__(256) colsum_finalize_small_kernel(
   red[rl][cl][1] = s2;
   __syncthreads();
   if (rl == 0 && c < C) {
-    for (int g = 1; g < 4; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
+    for (int g = 1; g < kCfRL; ++g) { s1 += red[g][cl][0]; s2 += red[g][cl][1]; }
     if constexpr (BWD) bn_bwd_finalize_one(c, s1, s2, count, gamma, invstd, dgamma, dbeta, coef);
     else bn_finalize_one(c, s1, s2, count, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean_out, invstd);
   }
@@ -1125,12 +1129,16 @@ __global__ void scale_kernel(float* g, long n, const float* mul) {
 // fp32 split-K slabs [splits][nvox][C] -> sum in split order + bias, store T, BN partial
 // sums; 64 voxels per block row
 constexpr int kMaxSplitSlabs = 16;  // slabs loaded together (more: summed one by one after)
+// 16 voxel lanes x 64 channels per block: a thread owns 4 of the row's 64 voxels, so a voxel
+// row is 4 rounds of slab loads instead of 16 (deep levels have few rows: level 4 is 8 rows x
+// 16 channel blocks, and each round is a full memory latency)
+constexpr int kSeThreads = 1024;
 template <typename T>
-__global__ void __launch_bounds__(TPB) split_epilogue_kernel(const float* acc, int splits, const float* bias, T* y0,
-                                                             T* y1, int cy0, float* stats, int C, long nvox,
-                                                             int relu) {
+__global__ void __launch_bounds__(kSeThreads) split_epilogue_kernel(const float* acc, int splits, const float* bias,
+                                                                    T* y0, T* y1, int cy0, float* stats, int C,
+                                                                    long nvox, int relu) {
   // stats row = (sum, M2 about the row mean), count row after the [rows][C][2] block
-  constexpr int NV = TPB / 64, KPT = 64 / NV;
+  constexpr int NV = kSeThreads / 64, KPT = 64 / NV;
   __shared__ float red[NV][64][3];
   const int cl = threadIdx.x & 63, vl = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
@@ -1279,7 +1287,7 @@ int pcms_bn_finalize(const float* part, int rows, int C, double count, const flo
                      float* rmean, float* rvar, long long* nbt, float momentum, float eps,
                      float* scale, float* shift, float* mean, float* invstd, double* ws, hipStream_t s) {
   if (rows <= kSmallRows) {
-    hipLaunchKernelGGL(colsum_finalize_small_kernel<false>, dim3(cdiv(C, 64)), dim3(256), 0, s, part, rows, C,
+    hipLaunchKernelGGL(colsum_finalize_small_kernel<false>, dim3(cdiv(C, 64)), dim3(64 * kCfRL), 0, s, part, rows, C,
                        part + (long)rows * C * 2, count, gamma, beta, rmean, rvar, nbt, momentum, eps, scale, shift,
                        mean, invstd, nullptr, nullptr, nullptr);
     PCMS_CHECK_LAUNCH();
@@ -1364,7 +1372,7 @@ int pcms_bn_relu_bwd_finish(int dtype, const void* da, const void* y, const floa
   const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
   hipError_t e;
   if (rows <= kSmallRows) {
-    hipLaunchKernelGGL(colsum_finalize_small_kernel<true>, dim3(cdiv(C, 64)), dim3(256), 0, s, part, rows, C,
+    hipLaunchKernelGGL(colsum_finalize_small_kernel<true>, dim3(cdiv(C, 64)), dim3(64 * kCfRL), 0, s, part, rows, C,
                        (const float*)nullptr, (double)nvox, gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f,
                        nullptr, nullptr, nullptr, const_cast<float*>(invstd), dgamma, dbeta, coef);
   } else {
@@ -1643,8 +1651,8 @@ int pcms_split_epilogue(int dtype, const float* acc, int splits, const float* bi
   const int relu = flags & PCMS_CONV_RELU;
   if (y1 == nullptr) cy0 = C;
   dim3 grid(cdiv(nvox, 64), C / 64);
-  if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(TPB), 0, s, acc, splits, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox, relu);
-  else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(TPB), 0, s, acc, splits, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox, relu);
+  if (dtype == PCMS_BF16) hipLaunchKernelGGL(split_epilogue_kernel<bf16_t>, grid, dim3(kSeThreads), 0, s, acc, splits, bias, (bf16_t*)y0, (bf16_t*)y1, cy0, stats, C, nvox, relu);
+  else hipLaunchKernelGGL(split_epilogue_kernel<float>, grid, dim3(kSeThreads), 0, s, acc, splits, bias, (float*)y0, (float*)y1, cy0, stats, C, nvox, relu);
   PCMS_CHECK_LAUNCH();
 }
 
