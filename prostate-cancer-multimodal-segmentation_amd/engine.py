@@ -133,7 +133,7 @@ class UNetEngine:
         # slabs, BN partial rows, weight-gradient partial rows), so the recomputed tensors are
         # bit-identical to the forward's and two identical steps give identical results.
         self.act_ckpt = False
-        self.split_target = 384  # split-K conv launches (levels 2-4): workgroups aimed at
+        self.split_target = 512  # split-K conv launches (levels 2-4): workgroups aimed at
         self.wgrad_target = 256  # conv weight-gradient workgroups: one round of 1 WG per CU (fewer partial rows to reduce than 512)
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
         self.kernel_timer = None  # dict name -> [(start, end) events] (bench.py roofline timing)
