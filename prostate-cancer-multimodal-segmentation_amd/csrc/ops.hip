@@ -1342,7 +1342,10 @@ int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const fl
 int pcms_bn_bwd_rows(int dtype, int C, long nvox) {
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   const int VL = TPB / (C / VEC);
-  return grid_for(nvox, VL * 16, 2048);
+  // small (deep) grids: one trip of 4 rows per thread and 4x the blocks (a block's reduction
+  // is a chain of memory latencies), as long as the rows stay on the one-launch finalize
+  const int small = grid_for(nvox, VL * 4, 2048);
+  return small <= kSmallRows ? small : grid_for(nvox, VL * 16, 2048);
 }
 
 int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scale, const float* shift,
