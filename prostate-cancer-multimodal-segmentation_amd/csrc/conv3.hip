@@ -1399,7 +1399,10 @@ constexpr int kBgDummy = 1024;
 constexpr int kBgStage = 64 * 128;                                        // per-M-group store slice
 constexpr int kBgRed = 4 * 64 * 3 * 4;                                    // BN moments
 constexpr int kBgLds = 2 * kBgBuf + kBgDummy + 4 * kBgStage + kBgRed + 64 * 4;  // + bias
-constexpr int kBgDist = 2;                 // B prefetch distance (taps); (Dist + 1) | 27
+#ifndef BG_DIST
+#define BG_DIST 8  // 2: 1-1.5 % slower big-box launches (A/B, profiles/r4_bg_dist_ab.txt)
+#endif
+constexpr int kBgDist = BG_DIST;           // B prefetch distance (taps); (Dist + 1) | 27
 constexpr int kBgEpiStores = kBgMT * 2;    // 16-B stores per wave and box
 static_assert(27 % (kBgDist + 1) == 0, "B ring index must continue across chunks");
 static_assert(kBgLds <= 160 * 1024, "LDS");
