@@ -120,6 +120,7 @@ class UNetEngine:
         self._packed_version = -1
         self._dirty = True
         self._packs_fresh = False  # the fused Adam wrote every conv / ConvT pack (not the stem's)
+        self._stem_conv_stale = False  # the stem's general-kernel pack skipped by the fast path
         self._adam_plan = None
         self.bufs = None
         self.buf_key = None
@@ -389,14 +390,17 @@ class UNetEngine:
         if not self._dirty and v == self._packed_version:
             return
         if self._packs_fresh and v == self._packed_version:
-            # the fused Adam rewrote every conv / ConvT pack: only the stem's are left
+            # the fused Adam rewrote every conv / ConvT pack: only the stem's are left.  With
+            # the direct stem kernels its general-kernel pack is needed only by a shape they do
+            # not run (packed on first use there: _conv)
             cs = self.convs[0]
-            if cs.dgrad is None:
+            if self.stem_fast:
+                call("pcms_stem_pack", cs.mod.weight, self.stem_pack, self.nmod)
+                self._stem_conv_stale = True
+            elif cs.dgrad is None:
                 call("pcms_conv3_pack", cs.code, cs.mod.weight, cs.fwd, cs.cout, cs.cin, 0)
             else:
                 call("pcms_conv3_pack2", cs.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
-            if self.stem_fast:
-                call("pcms_stem_pack", cs.mod.weight, self.stem_pack, self.nmod)
             self._dirty = False
             self._packs_fresh = False
             return
@@ -428,6 +432,17 @@ class UNetEngine:
         self._packed_version = self.flat_p._version
         self._dirty = False
         self._packs_fresh = False
+        self._stem_conv_stale = False
+
+    def _stem_conv_pack(self):
+        """The stem conv's general-kernel weight pack, when the fast path skipped it."""
+        if self._stem_conv_stale:
+            cs = self.convs[0]
+            if cs.dgrad is None:
+                call("pcms_conv3_pack", cs.code, cs.mod.weight, cs.fwd, cs.cout, cs.cin, 0)
+            else:
+                call("pcms_conv3_pack2", cs.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
+            self._stem_conv_stale = False
 
     def _ensure_eval_packs(self):
         """Folded eval weights: w' = w * gamma / sqrt(rvar + eps), b' = b * sc + beta - rmean * sc
@@ -603,6 +618,8 @@ class UNetEngine:
         nvox = N * S[0] * S[1] * S[2]
         splits = self._splits(N, S, c0 + c1, cs.cout, cs.code)
         st = b["stats"] if training and not recompute else None
+        if cs is self.convs[0] and not self.stem_sup & 1:
+            self._stem_conv_pack()
         if bnin is not None:
             call("pcms_conv3_fwd_bnin", cs.code, x0, c0, bnin.scale, bnin.shift, cs.fwd, cs.mod.bias, y, st, N,
                  *S, cs.cout)
