@@ -1272,7 +1272,7 @@ extern "C" {
 
 int pcms_pack_input(int dtype, const float* in, void* out, int N, int Cin, long V, int Cp, hipStream_t s) {
   if (Cp == 8 && Cin <= 8 && V % 4 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0) {
-    const int grid = grid_for((long)N * V / 4, TPB, 4 * 256);
+    const int grid = grid_for((long)N * V / 4, TPB, 16 * 256);  // ~one quad per thread: every load in flight at once
     if (dtype == PCMS_BF16) hipLaunchKernelGGL(pack_input4_kernel<bf16_t>, dim3(grid), dim3(TPB), 0, s, in, (bf16_t*)out, N, Cin, V);
     else hipLaunchKernelGGL(pack_input4_kernel<float>, dim3(grid), dim3(TPB), 0, s, in, (float*)out, N, Cin, V);
     PCMS_CHECK_LAUNCH();

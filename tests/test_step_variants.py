@@ -179,6 +179,7 @@ def test_fused_adam_packs_match_flat_adam(gscale, precision):
         opt.step()
         eng = m.engine()
         eng._ensure_packs()
+        eng._stem_conv_pack()  # the stem's general-kernel pack is otherwise built on first use
         torch.cuda.synchronize()
         runs.append((eng, opt))
     (e0, o0), (e1, o1) = runs
