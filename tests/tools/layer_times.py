@@ -60,6 +60,7 @@ def main():
                     help="fp32: the conv MFMA fraction counts the bf16x6 work (6 bf16 MFMA products per product)")
     ap.add_argument("--wgrad-target", type=int, default=0, help="engine.wgrad_target override")
     ap.add_argument("--split-target", type=int, default=0, help="engine.split_target override")
+    ap.add_argument("--big-min-boxes", type=int, default=0, help="pcms_conv3_big_min_boxes override")
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
     from pcms_amd import engine as E
@@ -74,6 +75,9 @@ def main():
         tr.model.engine().wgrad_target = a.wgrad_target
     if a.split_target:
         tr.model.engine().split_target = a.split_target
+    if a.big_min_boxes:
+        from pcms_amd import _lib as L
+        L.query("pcms_conv3_big_min_boxes", a.big_min_boxes)
     b = make_batch(a.batch, spatial, seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
     for _ in range(3):
