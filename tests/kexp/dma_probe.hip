@@ -48,6 +48,7 @@ __global__ void __launch_bounds__((F & 4096) ? 1024 : 512, 1) probe_kernel(const
   constexpr int kT = (F & 4096) ? 1024 : 512;
   constexpr bool kMfma = F & 64, kLdsRd = F & 128, kNoStage = F & 256, kInter = F & 512, kZero = F & 1024, kSpec = F & 2048;
   constexpr bool kBlocked = F & 8192;
+  constexpr bool kHalfRd = F & 16384;  // LDS-fed: 3 fragments (6 tr reads) per 8 MFMAs instead of 6 (12)
   constexpr int XROWB = kWide ? 128 : 64;
   constexpr int XP = kHalo * XROWB / 16;
   constexpr int NP = (kXOnly ? 0 : kDyP) + (kDyOnly ? 0 : XP);
@@ -146,7 +147,14 @@ __global__ void __launch_bounds__((F & 4096) ? 1024 : 512, 1) probe_kernel(const
       s16x8_t f[6];
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
-        if constexpr (kLdsRd) {
+        if constexpr (kLdsRd && kHalfRd) {
+          if (j < 3) {
+            const s16x4_t lo = tr_read(rb, st * 2048 + j * 128), hi = tr_read(rb, st * 2048 + j * 128 + 512);
+            f[j] = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          } else {
+            f[j] = f[j - 3];
+          }
+        } else if constexpr (kLdsRd) {
           const s16x4_t lo = tr_read(rb, st * 2048 + j * 128), hi = tr_read(rb, st * 2048 + j * 128 + 512);
           f[j] = (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         } else {
@@ -222,7 +230,7 @@ extern "C" int probe_run(int flags, const void* x, const void* dy, int N, int D,
   switch (flags) {
     PROBE(0) PROBE(1) PROBE(2) PROBE(3) PROBE(4) PROBE(5) PROBE(8) PROBE(9) PROBE(16) PROBE(17) PROBE(32) PROBE(33)
     PROBE(20) PROBE(36) PROBE(64) PROBE(128) PROBE(192) PROBE(320) PROBE(384) PROBE(448) PROBE(576) PROBE(704) PROBE(66) PROBE(194) PROBE(1088) PROBE(1344) PROBE(1600) PROBE(2048) PROBE(2112) PROBE(2240) PROBE(2368) PROBE(2496) PROBE(4096) PROBE(4160) PROBE(4416) PROBE(4544) PROBE(4288)
-    PROBE(8192) PROBE(8193) PROBE(8224) PROBE(8228) PROBE(8256) PROBE(8384)
+    PROBE(8192) PROBE(8193) PROBE(8224) PROBE(8228) PROBE(8256) PROBE(8384) PROBE(16832) PROBE(16576)
     default: return -1;
   }
 #undef PROBE

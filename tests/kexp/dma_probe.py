@@ -23,7 +23,8 @@ NAMES = {0: "product shape, 1 box in flight", 1: "2 boxes in flight", 2: "regist
          4544: "16 waves: LDS-fed MFMA alone", 4288: "16 waves: staging + LDS-fed MFMA",
          8192: "blocked x: staging", 8193: "blocked x: 2 in flight", 8224: "blocked x: halo only",
          8228: "blocked x: halo only, L2-resident", 8256: "blocked x: staging + MFMA phase",
-         8384: "blocked x: staging + LDS-fed MFMAs"}
+         8384: "blocked x: staging + LDS-fed MFMAs",
+         16832: "LDS-fed MFMA alone, half the reads", 16576: "staging + LDS-fed MFMAs, half reads"}
 
 
 def main():
@@ -63,7 +64,7 @@ def main():
         wide = F & 8
         per_box = 0 if F & 256 else (0 if F & 32 else 256 * 128) + (0 if F & 16 else 600 * (128 if wide else 64))
         gbs = grid * 64 * per_box / (us * 1e-6) / 1e9
-        print(f"F={F:3d} {name:34s} {us:8.1f} us  {per_box / 1024:5.1f} KB/box  {gbs / 256:6.1f} GB/s/CU  "
+        print(f"F={F:5d} {name:36s} {us:8.1f} us  {per_box / 1024:5.1f} KB/box  {gbs / 256:6.1f} GB/s/CU  "
               f"{us / 64:5.2f} us/box  clock {mhz:6.0f} MHz", flush=True)
 
 
