@@ -214,6 +214,15 @@ int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Co
 int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
                      int target_wgs, hipStream_t s);
+/* pcms_convt_wgrad + the bias gradient db[co] += sum of dout over the ConvT output box
+ * (F.pad front offsets floor((Do - 2 Din) / 2), ...), taken from the weight gradient's own
+ * read of dout where the kernel allows it (bf16, Cin % 128 == 0), else by
+ * pcms_box_channel_sum after it (models/unet3d.py:118-122 ConvTranspose3d bias, autograd);
+ * bws: pcms_convt_wgrad_bias_ws_floats(...) fp32                                         */
+int pcms_convt_wgrad_bias_ws_floats(int dtype, int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs);
+int pcms_convt_wgrad_bias(int dtype, const void* x, const void* dout, float* dw, float* db, float* ws, float* bws,
+                          int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
+                          int target_wgs, hipStream_t s);
 /* out[c] += sum over the sub-box of x (ConvTranspose3d bias gradient); ws:
  * pcms_box_channel_sum_ws_floats(...) fp32 (per-block partial rows, fixed-order sum)     */
 int pcms_box_channel_sum_ws_floats(int dtype, int N, int C, int bd, int bh, int bw);

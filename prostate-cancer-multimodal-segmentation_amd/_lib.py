@@ -67,6 +67,8 @@ SIGNATURES = {
     "pcms_convt_dgrad_ws": "ippppiiiiiiiiis",
     "pcms_convt_wgrad_ws_floats": "iiiiiii",
     "pcms_convt_wgrad": "ippppiiiiiiiiiis",
+    "pcms_convt_wgrad_bias_ws_floats": "iiiiiiii",
+    "pcms_convt_wgrad_bias": "ippppppiiiiiiiiiis",
     "pcms_box_channel_sum_ws_floats": "iiiiii",
     "pcms_box_channel_sum": "ipppiiiiiiiiiiis",
     "pcms_head_fwd": "ippppliiifs",

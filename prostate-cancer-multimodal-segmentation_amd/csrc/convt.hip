@@ -687,9 +687,15 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad_kernel(const T* x, const T
 // [VB][64] halves; 8 waves = (ci quarter cq, co half), each all 8 taps (8 accumulators):
 // per 16 voxels one x fragment and 8 dout fragments feed 8 MFMAs.
 // NT: non-temporal loads (dout far larger than the Infinity Cache)
+// BIAS (bpart != nullptr; ci tile 0's workgroups): the bias gradient sum_v dout[v][co] from the
+// same read of dout -- a thread's dout pieces are always channels 8 (tid % 8) .. of its co
+// tile (the piece index steps by 512, a multiple of 8), summed in registers in piece order and
+// then over the 64 threads of each channel group in thread order: one [Cout] partial row per
+// voxel split (the ConvT bias-gradient pass over dout -- 268 MB at level 0 -- is gone)
 template <bool NT>
 __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout, float* ws,
-                                                               UpGeom g, int Cin, int Cout, int vox_per_split) {
+                                                               UpGeom g, int Cin, int Cout, int vox_per_split,
+                                                               float* bpart) {
   constexpr int VB = 64, ROW = 128, PPR = 8;
   constexpr int XP = VB * 2 * PPR;               // x pieces (two 64-ci halves)
   constexpr int NP = XP + 8 * VB * PPR;          // + 8 taps
@@ -713,6 +719,8 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
   const int gg = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
   const int ca = (cq & 1) * 32 + gg * 16 + pp * 4, cb = wq * 32 + gg * 16 + pp * 4;
   const char* Pq = P + (cq >> 1) * VB * ROW;
+  const bool bias = bpart != nullptr && blockIdx.z == 0;
+  float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (long vb = vbeg; vb < vend; vb += VB) {
     u32x4_t stg[PT];
 #pragma unroll
@@ -734,6 +742,15 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
       stg[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src))
                   : *reinterpret_cast<const u32x4_t*>(src);
       if (vb + v >= vend) stg[i] = (u32x4_t){0u, 0u, 0u, 0u};
+    }
+    if (bias) {
+#pragma unroll
+      for (int i = XP / 512; i < PT; ++i)  // the dout pieces (pc >= XP)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          bs[2 * k] += __uint_as_float(stg[i][k] << 16);
+          bs[2 * k + 1] += __uint_as_float(stg[i][k] & 0xffff0000u);
+        }
     }
     __syncthreads();  // every wave is done with the previous block's tiles
 #pragma unroll
@@ -768,6 +785,37 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
       const int co = co0 + wq * 32 + (lane & 31);
       prow[((long)ci * 8 + t) * Cout + co] = acc[t][e];
     }
+  if (bias) {
+    __syncthreads();  // every wave is done reading the tiles
+    float* red = reinterpret_cast<float*>(lds);  // [512][8]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bs[j];
+    __syncthreads();
+    if (tid < 64) {  // channel co0 + tid = group tid / 8, element tid % 8
+      const int q = tid >> 3, j = tid & 7;
+      float sum = 0.f;
+      for (int t = q; t < 512; t += 8) sum += red[t * 8 + j];
+      bpart[(long)blockIdx.x * Cout + co0 + tid] = sum;
+    }
+  }
+}
+
+// db[c] += sum of the R bias partial rows [R][C] in row order (8 columns x 32 row lanes per
+// block, the 32 lane sums added in lane order)
+__global__ void __launch_bounds__(256) convt_bias_reduce(const float* part, int R, int C, float* db) {
+  __shared__ float red[32][9];
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  float s = 0.f;
+  if (c < C)
+    for (int r = rl; r < R; r += 32) s += part[(long)r * C + c];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float t = 0.f;
+    for (int k = 0; k < 32; ++k) t += red[k][cl];
+    db[c] += t;
+  }
 }
 
 // split reduction, fixed order.  Stage 1 (S > 16): rows r*16 .. r*16+15 summed in place into
@@ -1139,9 +1187,9 @@ int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Co
 
 // dw (torch layout [Cin][Cout][2][2][2], fp32) += ...; ws: pcms_convt_wgrad_ws_floats(...)
 // floats (per-split partial rows summed in a fixed order: deterministic)
-int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
-                     int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
-                     int target_wgs, hipStream_t s) {
+static int convt_wgrad_any(int dtype, const void* x, const void* dout, float* dw, float* ws, float* bpart,
+                           float* db, int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
+                           int target_wgs, hipStream_t s) {
   if (Cin % 64 || Cout % 64) return -1;
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
   if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
@@ -1155,7 +1203,13 @@ int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, floa
     auto kern = nt ? convt_wgrad128_kernel<true> : convt_wgrad128_kernel<false>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, grid, dim3(512), lds, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g,
-                       Cin, Cout, vps);
+                       Cin, Cout, vps, bpart);
+    if (bpart != nullptr) {
+      hipError_t eb = hipGetLastError();
+      if (eb != hipSuccess) return (int)eb;
+      hipLaunchKernelGGL(convt_bias_reduce, dim3(cdiv(Cout, 8)), dim3(256), 0, s, (const float*)bpart, splits, Cout,
+                         db);
+    }
   } else if (dtype == PCMS_BF16) {
     constexpr int lds = 9 * CW<bf16_t>::VB * 128;
     (void)hipFuncSetAttribute((const void*)convt_wgrad_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1181,6 +1235,38 @@ int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, floa
   hipLaunchKernelGGL(convt_wgrad_reduce, dim3(Cin, Cout / 32), dim3(256), 0, s, (const float*)ws, R, stride, dw, Cin,
                      Cout);
   PCMS_CHECK_LAUNCH();
+}
+
+int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
+                     int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
+                     int target_wgs, hipStream_t s) {
+  return convt_wgrad_any(dtype, x, dout, dw, ws, nullptr, nullptr, N, Din, Hin, Win, Cin, Cout, Do, Ho, Wo,
+                         target_wgs, s);
+}
+
+// the bias-gradient workspace of pcms_convt_wgrad_bias: one [Cout] row per voxel split (fused
+// path) or pcms_box_channel_sum's rows (the other paths), whichever is larger
+int pcms_convt_wgrad_bias_ws_floats(int dtype, int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs) {
+  int vps;
+  const int fused = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps) * Cout;
+  const int box = pcms_box_channel_sum_ws_floats(dtype, N, Cout, 2 * Din, 2 * Hin, 2 * Win);
+  return std::max(fused, box);
+}
+
+// pcms_convt_wgrad + db[co] += the sum of dout over the ConvT output box (the bias gradient;
+// F.pad's front offsets floor((Do - 2 Din) / 2), ...): from the weight gradient's own read of
+// dout on the bf16 128-ci path, else pcms_box_channel_sum after it
+int pcms_convt_wgrad_bias(int dtype, const void* x, const void* dout, float* dw, float* db, float* ws, float* bws,
+                          int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
+                          int target_wgs, hipStream_t s) {
+  if (db == nullptr || bws == nullptr) return -2;
+  if (dtype == PCMS_BF16 && Cin % 128 == 0 && Cout % 64 == 0)
+    return convt_wgrad_any(dtype, x, dout, dw, ws, bws, db, N, Din, Hin, Win, Cin, Cout, Do, Ho, Wo, target_wgs, s);
+  const int rc = convt_wgrad_any(dtype, x, dout, dw, ws, nullptr, nullptr, N, Din, Hin, Win, Cin, Cout, Do, Ho, Wo,
+                                 target_wgs, s);
+  if (rc) return rc;
+  return pcms_box_channel_sum(dtype, dout, db, bws, N, Do, Ho, Wo, Cout, (Do - 2 * Din) / 2, (Ho - 2 * Hin) / 2,
+                              (Wo - 2 * Win) / 2, 2 * Din, 2 * Hin, 2 * Win, s);
 }
 
 }  // extern "C"

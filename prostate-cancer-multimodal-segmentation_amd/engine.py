@@ -574,7 +574,8 @@ class UNetEngine:
         red = [query("pcms_head_bwd_ws_floats", D * H * W, N, self.ncls)]
         for i, up in enumerate(self.ups):
             l = 3 - i
-            red.append(query("pcms_box_channel_sum_ws_floats", self.code, N, C[l], *[2 * v for v in S[l + 1]]))
+            red.append(query("pcms_convt_wgrad_bias_ws_floats", self.code, N, *S[l + 1], up.in_channels,
+                             up.out_channels, 512))
         b["redws"] = torch.empty(max(red), dtype=torch.float32, device=dev)
         # dedicated stem kernels where they support the shape (else the general conv kernels)
         self.stem_sup = query("pcms_stem_supported", N, D, H, W) if self.stem_fast else 0
@@ -860,13 +861,10 @@ class UNetEngine:
             up = self.ups[i]
             _, dpack = self.convt_packs[i]
             hin = b["e4_x"] if i == 0 else b[f"d{l + 1}_a2"]
-            call("pcms_convt_wgrad", self.code, hin, gu, up.weight.grad, b["ctws"], N, *S[l + 1], up.in_channels,
-                 up.out_channels, *S[l], 512)
-            dz = (S[l][0] - 2 * S[l + 1][0]) // 2
-            dy_ = (S[l][1] - 2 * S[l + 1][1]) // 2
-            dx_ = (S[l][2] - 2 * S[l + 1][2]) // 2
-            call("pcms_box_channel_sum", self.code, gu, up.bias.grad, b["redws"], N, *S[l], C[l], dz, dy_, dx_,
-                 2 * S[l + 1][0], 2 * S[l + 1][1], 2 * S[l + 1][2])
+            # weight and bias gradients in one pass over gu (the bias sum over the ConvT output
+            # box, F.pad's front offsets floor((S[l] - 2 S[l + 1]) / 2))
+            call("pcms_convt_wgrad_bias", self.code, hin, gu, up.weight.grad, up.bias.grad, b["ctws"], b["redws"], N,
+                 *S[l + 1], up.in_channels, up.out_channels, *S[l], 512)
             self._grads_done(f"up{i + 1}")
             gnext = b["gx4"] if i == 0 else b[f"gA{l + 1}"]
             call("pcms_convt_dgrad_ws", self.code, gu, dpack, gnext, b["ctws"], N, *S[l + 1], up.in_channels,

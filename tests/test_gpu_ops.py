@@ -547,12 +547,19 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
                       device=DEV)
     L.call("pcms_box_channel_sum", code, god, db, bws, N, *Sout, cout, dz // 2, dyy // 2, dxx // 2,
            2 * Sin[0], 2 * Sin[1], 2 * Sin[2])
+    # weight and bias gradients in one call (the bias from the weight gradient's own read of
+    # dout on the bf16 128-ci path, else the box sum after it)
+    dw2, db2 = torch.zeros_like(dw), torch.zeros_like(db)
+    bws2 = torch.empty(L.query("pcms_convt_wgrad_bias_ws_floats", code, N, *Sin, cin, cout, 64), device=DEV)
+    L.call("pcms_convt_wgrad_bias", code, ndhwc(x).to(DEV), god, dw2, db2, ws, bws2, N, *Sin, cin, cout, *Sout, 64)
     torch.cuda.synchronize()
     close(ncdhw(out.cpu()), up.detach(), tol, "convT fwd (+pad)")
     close(ncdhw(dx.cpu()), xr.grad, tol, "convT dgrad")
     close(ncdhw(dxs.cpu()), xr.grad, tol, "convT dgrad (K-split)")
     close(dw.cpu(), wr.grad, 1e-4 if code else 2e-5, "convT wgrad")
     close(db.cpu(), br.grad, 1e-4 if code else 1e-5, "convT bias grad")
+    assert torch.equal(dw2, dw), "fused wgrad + bias: the same weight gradient"
+    close(db2.cpu(), br.grad, 1e-4 if code else 1e-5, "convT bias grad (fused)")
 
 
 @pytest.mark.parametrize("Sin,Sout", [((32, 32, 24), (64, 64, 48)), ((24, 20, 12), (49, 41, 25))])
