@@ -231,15 +231,18 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_reduce_kernel(
       sgx[j] += g * ((yv[j] - mu[j]) * is[j]);
     }
   };
-  for (; v + 3 * stride < nvox; v += 4 * stride) {
-    float dv[4][VEC], yv[4][VEC];
+#ifndef BNR_U
+#define BNR_U 2  // voxel rows in flight per thread and trip (A/B: 1 / 4 / 8 slower, profiles/r4_bnr_unroll_ab.txt)
+#endif
+  for (; v + (BNR_U - 1) * stride < nvox; v += BNR_U * stride) {
+    float dv[BNR_U][VEC], yv[BNR_U][VEC];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < BNR_U; ++u) {
       ld16<NT>(da + (v + u * stride) * C + c0, dv[u]);
       ld16<NT>(y + (v + u * stride) * C + c0, yv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc1(dv[u], yv[u]);
+    for (int u = 0; u < BNR_U; ++u) acc1(dv[u], yv[u]);
   }
   for (; v < nvox; v += stride) {
     float dv[VEC], yv[VEC];
