@@ -838,7 +838,10 @@ __global__ void __launch_bounds__(TPB, (BN && NC > 2) ? 2 : 3) head_bwd_kernel(c
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
   VoxQR pv(v, nvox_per_n);
-  constexpr int U = NC > 2 ? 1 : (BN || NC > 1) ? 2 : kHU;  // (registers: the BN form holds 6 x 8 per-channel values)
+#ifndef HEADB_U
+#define HEADB_U 2
+#endif
+  constexpr int U = NC > 2 ? 1 : (BN || NC > 1) ? HEADB_U : kHU;  // (registers: the BN form holds 6 x 8 per-channel values)
 #pragma unroll 1
   for (; v + (U - 1) * stride < total; v += U * stride) {
     float x[U][8], dl[U][NC];
@@ -948,7 +951,10 @@ __global__ void __launch_bounds__(TPB, 2) head_bn_apply_kernel(const T* y, const
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
   VoxQR pv(v, nvox_per_n);
-  constexpr int U = NC > 1 ? 1 : 2;  // (registers: 5 x 8 per-channel values + NC x 8 weights held)
+#ifndef HEADA_U
+#define HEADA_U 2
+#endif
+  constexpr int U = NC > 1 ? 1 : HEADA_U;  // (registers: 5 x 8 per-channel values + NC x 8 weights held)
 #pragma unroll 1
   for (; v + (U - 1) * stride < total; v += U * stride) {
     float x[U][8], dl[U][NC];
