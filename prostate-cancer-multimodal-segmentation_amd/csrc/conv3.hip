@@ -1258,28 +1258,45 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
   const int local = blockIdx.x - (int)e[5];
   const int j0 = (local % (Cout / 32)) * 32, chunk = local / (Cout / 32);
   const float s = gmul ? c.gscale * gmul[0] : c.gscale;
-  for (int i = 0; i < 27; ++i) {
-    const int q4 = threadIdx.x + i * 256, run = q4 / 216, q = q4 % 216;
-    const long idx = off + ((long)(j0 + run) * Cin + chunk * 32) * 27 + 4 * q;
-    // the fp32 master / gradient / moment streams (1.4 GB per step) bypass the caches
-    f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(P + idx));
-    f32x4_t gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Gr + idx));
-    f32x4_t mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Mo + idx));
-    f32x4_t vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Vo + idx));
+  // ADAM_U iterations' four streams loaded before any is used: 4 x ADAM_U 16-B loads in flight
+  // per thread (the stores of an iteration could alias the next one's loads for the compiler,
+  // so without the explicit batch it keeps one iteration's loads in flight)
+#ifndef ADAM_U
+#define ADAM_U 3
+#endif
+  static_assert(27 % ADAM_U == 0, "ADAM_U divides the 27 iterations");
+  for (int i0 = 0; i0 < 27; i0 += ADAM_U) {
+    f32x4_t pv[ADAM_U], gv[ADAM_U], mv[ADAM_U], vv[ADAM_U];
+    long idx[ADAM_U];
+    int tbo[ADAM_U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float pk = pv[k], gk = gv[k], mk = mv[k], vk = vv[k];
-      adam_update(pk, gk, mk, vk, c, s);
-      pv[k] = pk; gv[k] = gk; mv[k] = mk; vv[k] = vk;
+    for (int u = 0; u < ADAM_U; ++u) {
+      const int q4 = threadIdx.x + (i0 + u) * 256, run = q4 / 216, q = q4 % 216;
+      idx[u] = off + ((long)(j0 + run) * Cin + chunk * 32) * 27 + 4 * q;
+      tbo[u] = run * 864 + 4 * q;
+      // the fp32 master / gradient / moment streams (1.4 GB per step) bypass the caches
+      pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(P + idx[u]));
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Gr + idx[u]));
+      mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Mo + idx[u]));
+      vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Vo + idx[u]));
     }
-    __builtin_nontemporal_store(pv, reinterpret_cast<f32x4_t*>(P + idx));
-    __builtin_nontemporal_store(mv, reinterpret_cast<f32x4_t*>(Mo + idx));
-    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4_t*>(Vo + idx));
-    if (s != 1.f) __builtin_nontemporal_store(gv, reinterpret_cast<f32x4_t*>(Gr + idx));
-    uint2 o;
-    o.x = pack_bf16x2(pv[0], pv[1]);
-    o.y = pack_bf16x2(pv[2], pv[3]);
-    *reinterpret_cast<uint2*>(tb + run * 864 + 4 * q) = o;
+#pragma unroll
+    for (int u = 0; u < ADAM_U; ++u) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float pk = pv[u][k], gk = gv[u][k], mk = mv[u][k], vk = vv[u][k];
+        adam_update(pk, gk, mk, vk, c, s);
+        pv[u][k] = pk; gv[u][k] = gk; mv[u][k] = mk; vv[u][k] = vk;
+      }
+      __builtin_nontemporal_store(pv[u], reinterpret_cast<f32x4_t*>(P + idx[u]));
+      __builtin_nontemporal_store(mv[u], reinterpret_cast<f32x4_t*>(Mo + idx[u]));
+      __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4_t*>(Vo + idx[u]));
+      if (s != 1.f) __builtin_nontemporal_store(gv[u], reinterpret_cast<f32x4_t*>(Gr + idx[u]));
+      uint2 o;
+      o.x = pack_bf16x2(pv[u][0], pv[u][1]);
+      o.y = pack_bf16x2(pv[u][2], pv[u][3]);
+      *reinterpret_cast<uint2*>(tb + tbo[u]) = o;
+    }
   }
   __syncthreads();
   for (int g = threadIdx.x; g < 27 * 128; g += 256) {
