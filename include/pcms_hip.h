@@ -211,6 +211,9 @@ int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* 
 /* dw += ConvTranspose3d weight gradient; ws: pcms_convt_wgrad_ws_floats(...) fp32 (one
  * [Cin][8][Cout] partial row per voxel split, summed in a fixed order)                   */
 int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs);
+/* A/B switch: taps per workgroup of the bf16 Cin % 128 == 0 weight gradient (8, 4 or 2; 0 =
+   chosen by shape); returns the previous setting.  Process-wide. */
+int pcms_convt_wgrad_taps(int tt);
 int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,
                      int target_wgs, hipStream_t s);

@@ -692,34 +692,42 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad_kernel(const T* x, const T
 // tile (the piece index steps by 512, a multiple of 8), summed in registers in piece order and
 // then over the 64 threads of each channel group in thread order: one [Cout] partial row per
 // voxel split (the ConvT bias-gradient pass over dout -- 268 MB at level 0 -- is gone)
-template <bool NT>
-__global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout, float* ws,
-                                                               UpGeom g, int Cin, int Cout, int vox_per_split,
-                                                               float* bpart) {
-  constexpr int VB = 64, ROW = 128, PPR = 8;
+// TT (taps per workgroup, 8 / 4 / 2): the deep levels' grids -- a few thousand input voxels,
+// 16-64 (ci, co) tiles -- fill the chip with voxel splits whose fp32 partial rows (67 MB per
+// launch at the engine's 512-workgroup target) cost more than the MFMAs; splitting the 8 taps
+// over G = 8 / TT workgroups instead cuts the splits (and the partial rows) by G, at G x the x
+// staging.  blockIdx.z = ci tile x G + tap group.  DIRECT (one split): dw += the tile itself
+// (torch layout [Cin][Cout][8], each element owned by one workgroup), no partial rows.
+// Bias (ci tile 0): one [Cout] row per (split, tap group).
+template <bool NT, int TT, bool DIRECT>
+__global__ void __launch_bounds__(512, TT <= 4 ? 2 : 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout,
+                                                                             float* ws, UpGeom g, int Cin, int Cout,
+                                                                             int vox_per_split, float* bpart) {
+  constexpr int VB = 64, ROW = 128, PPR = 8, G = 8 / TT;
   constexpr int XP = VB * 2 * PPR;               // x pieces (two 64-ci halves)
-  constexpr int NP = XP + 8 * VB * PPR;          // + 8 taps
-  constexpr int PT = NP / 512;                   // 10 per thread
+  constexpr int NP = XP + TT * VB * PPR;         // + TT taps
+  constexpr int PT = NP / 512;                   // 2 + TT per thread
   static_assert(NP % 512 == 0, "whole pieces per thread");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* P = lds;                                 // x tiles [2][VB][64]
-  char* Q = lds + 2 * VB * ROW;                  // dout tiles [8][VB][64]
+  char* Q = lds + 2 * VB * ROW;                  // dout tiles [TT][VB][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int cq = wave & 3, wq = wave >> 2;       // ci quarter, co half
-  const int p0 = blockIdx.z * 128;               // ci tile
+  const int tg = blockIdx.z % G, tb = tg * TT;   // tap group, its first tap
+  const int p0 = (blockIdx.z / G) * 128;         // ci tile
   const int co0 = blockIdx.y * 64;               // co tile
   const long M = (long)g.N * g.Din * g.Hin * g.Win;
   const long vbeg = (long)blockIdx.x * vox_per_split;
   const long vend = std::min<long>(M, vbeg + vox_per_split);
-  f32x16_t acc[8];
+  f32x16_t acc[TT];
 #pragma unroll
-  for (int t = 0; t < 8; ++t)
+  for (int t = 0; t < TT; ++t)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
   const int gg = (lane >> 4) & 1, qq = (lane & 15) >> 2, pp = lane & 3;
   const int ca = (cq & 1) * 32 + gg * 16 + pp * 4, cb = wq * 32 + gg * 16 + pp * 4;
   const char* Pq = P + (cq >> 1) * VB * ROW;
-  const bool bias = bpart != nullptr && blockIdx.z == 0;
+  const bool bias = bpart != nullptr && blockIdx.z < G;
   float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (long vb = vbeg; vb < vend; vb += VB) {
     u32x4_t stg[PT];
@@ -733,11 +741,11 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
         v = rem / PPR;
         const long m = std::min<long>(vb + v, vend - 1);
         src = x + m * Cin + p0 + hf * 64 + (rem % PPR) * 8;
-      } else {                                   // dout tap t
+      } else {                                   // dout tap tb + t
         const int t = (pc - XP) / (VB * PPR), rem = (pc - XP) % (VB * PPR);
         v = rem / PPR;
         const long m = std::min<long>(vb + v, vend - 1);
-        src = dout + child_vox(g, m, t) * Cout + co0 + (rem % PPR) * 8;
+        src = dout + child_vox(g, m, tb + t) * Cout + co0 + (rem % PPR) * 8;
       }
       stg[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src))
                   : *reinterpret_cast<const u32x4_t*>(src);
@@ -756,7 +764,7 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int pc = tid + i * 512;
-      const int tile = pc / (VB * PPR), rem = pc % (VB * PPR);  // tiles 0-1: x halves, 2-9: taps
+      const int tile = pc / (VB * PPR), rem = pc % (VB * PPR);  // tiles 0-1: x halves, 2..: taps
       const int v = rem / PPR, q = rem % PPR;
       *reinterpret_cast<u32x4_t*>(lds + tile * VB * ROW + half_swz(v, q * 8)) = stg[i];
     }
@@ -767,7 +775,7 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
       s16x4_t a0 = tr_read(Pq, half_swz(v, ca)), a1 = tr_read(Pq, half_swz(v + 4, ca));
       s16x8_t a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
+      for (int t = 0; t < TT; ++t) {
         const char* Qt = Q + t * VB * ROW;
         s16x4_t b0 = tr_read(Qt, half_swz(v, cb)), b1 = tr_read(Qt, half_swz(v + 4, cb));
         s16x8_t b = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
@@ -775,16 +783,38 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
       }
     }
   }
-  // C[row = ci][col = co] per tap -> this split's partial row ws[split][Cin][8][Cout]
-  float* prow = ws + (long)blockIdx.x * 8 * Cin * Cout;
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
+  const int co = co0 + wq * 32 + (lane & 31);
+  if constexpr (DIRECT) {
+    // dw[ci][co][tb .. tb + TT) += acc: TT contiguous floats per (ci, co), one owner
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int ci = p0 + cq * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      const int co = co0 + wq * 32 + (lane & 31);
-      prow[((long)ci * 8 + t) * Cout + co] = acc[t][e];
+      float* d = ws + ((long)ci * Cout + co) * 8 + tb;
+#pragma unroll
+      for (int t0 = 0; t0 < TT; t0 += (TT < 4 ? TT : 4)) {
+        if constexpr (TT == 2) {
+          float2 o = *reinterpret_cast<float2*>(d + t0);
+          o.x += acc[t0][e]; o.y += acc[t0 + 1][e];
+          *reinterpret_cast<float2*>(d + t0) = o;
+        } else {
+          f32x4_t o = *reinterpret_cast<f32x4_t*>(d + t0);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] += acc[t0 + k][e];
+          *reinterpret_cast<f32x4_t*>(d + t0) = o;
+        }
+      }
     }
+  } else {
+    // C[row = ci][col = co] per tap -> this split's partial row ws[split][Cin][8][Cout]
+    float* prow = ws + (long)blockIdx.x * 8 * Cin * Cout;
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int ci = p0 + cq * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        prow[((long)ci * 8 + tb + t) * Cout + co] = acc[t][e];
+      }
+  }
   if (bias) {
     __syncthreads();  // every wave is done reading the tiles
     float* red = reinterpret_cast<float*>(lds);  // [512][8]
@@ -795,7 +825,7 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad128_kernel(const bf16_t* x,
       const int q = tid >> 3, j = tid & 7;
       float sum = 0.f;
       for (int t = q; t < 512; t += 8) sum += red[t * 8 + j];
-      bpart[(long)blockIdx.x * Cout + co0 + tid] = sum;
+      bpart[((long)blockIdx.x * G + tg) * Cout + co0 + tid] = sum;
     }
   }
 }
@@ -1169,9 +1199,12 @@ int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* 
 
 // (the 128-ci bf16 kernel keeps the 64-ci split count: half the workgroups, the same
 // partial rows -- doubling the splits doubled the partial-row traffic: slower at levels 1-3)
-static int convt_wgrad_splits(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs, int* vps) {
+// G = 8 / TT tap groups divide the splits by G (the bf16 128-ci kernel's TT, see
+// convt_wgrad128_kernel)
+static int convt_wgrad_splits(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs, int* vps,
+                              int G = 1) {
   const long M = (long)N * Din * Hin * Win;
-  const int tiles = (Cout / 64) * (Cin / 64);
+  const int tiles = (Cout / 64) * (Cin / 64) * G;
   if (target_wgs <= 0) target_wgs = 512;
   const long nvb = (M + kVB - 1) / kVB;
   int splits = (int)std::max<long>(1, std::min<long>(nvb, cdiv(target_wgs, tiles)));
@@ -1179,11 +1212,59 @@ static int convt_wgrad_splits(int N, int Din, int Hin, int Win, int Cin, int Cou
   return (int)((M + *vps - 1) / *vps);
 }
 
-// fp32 workspace floats pcms_convt_wgrad needs: one [Cin][8][Cout] partial row per split
+static int g_convt_wg_tt = 0;  // taps per workgroup of the bf16 128-ci weight gradient (0: by shape)
+
+// The bf16 128-ci weight gradient's plan: taps per workgroup TT and the voxel splits.  By shape
+// (`tests/tools/convt_wgrad_sweep.py`, `profiles/r4_convt_wgrad_sweep*.txt`): TT = 2 for
+// Cin >= 256, 4 at Cin = 128, twice the workgroup target (the grids land at ~512 workgroups);
+// a plan of <= 2 splits runs as ONE split that writes dw directly (level 4: 49 -> 30 us; the
+// partial rows and their reduce launch cost more than the extra staging per workgroup).
+// pcms_convt_wgrad_taps(TT) pins TT at the plain target instead.  Other dtypes / Cin: TT = 8.
+static int convt_wgrad_plan(int dtype, int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs,
+                            int* tt, int* vps) {
+  if (dtype != PCMS_BF16 || Cin % 128) {
+    *tt = 8;
+    return convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, vps);
+  }
+  if (g_convt_wg_tt) {
+    *tt = g_convt_wg_tt;
+    return convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, vps, 8 / *tt);
+  }
+  if (target_wgs <= 0) target_wgs = 512;
+  *tt = Cin >= 256 ? 2 : 4;
+  const int splits = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, 2 * target_wgs, vps, 8 / *tt);
+  if (splits > 2) return splits;
+  const long M = (long)N * Din * Hin * Win;
+  *vps = (int)(cdiv(M, kVB) * kVB);
+  return 1;
+}
+
+// fp32 workspace floats pcms_convt_wgrad needs: one [Cin][8][Cout] partial row per split (the
+// one-tap-group split count: tap groups only ever lower it, whatever the dtype)
 int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs) {
   int vps;
   return convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps) * 8 * Cin * Cout;
 }
+
+// A/B switch: taps per workgroup of the bf16 128-ci weight gradient (8, 4, 2; 0 = by shape);
+// returns the previous value.  Set before the workspace queries.
+int pcms_convt_wgrad_taps(int tt) {
+  const int old = g_convt_wg_tt;
+  if (tt == 0 || tt == 2 || tt == 4 || tt == 8) g_convt_wg_tt = tt;
+  return old;
+}
+
+extern "C++" {
+template <int TT>
+static void launch_wgrad128(bool nt, bool direct, dim3 grid, hipStream_t s, const bf16_t* x, const bf16_t* dout,
+                            float* ws, UpGeom g, int Cin, int Cout, int vps, float* bpart) {
+  const int lds = (2 + TT) * 64 * 128;
+  auto kern = nt ? (direct ? convt_wgrad128_kernel<true, TT, true> : convt_wgrad128_kernel<true, TT, false>)
+                 : (direct ? convt_wgrad128_kernel<false, TT, true> : convt_wgrad128_kernel<false, TT, false>);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(kern, grid, dim3(512), lds, s, x, dout, ws, g, Cin, Cout, vps, bpart);
+}
+}  // extern "C++"
 
 // dw (torch layout [Cin][Cout][2][2][2], fp32) += ...; ws: pcms_convt_wgrad_ws_floats(...)
 // floats (per-split partial rows summed in a fixed order: deterministic)
@@ -1195,21 +1276,27 @@ static int convt_wgrad_any(int dtype, const void* x, const void* dout, float* dw
   if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
   int vps;
   const bool ci128 = dtype == PCMS_BF16 && Cin % 128 == 0;
-  const int splits = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps);
-  dim3 grid(splits, Cout / 64, Cin / (ci128 ? 128 : 64));
+  int TT;
+  const int splits = convt_wgrad_plan(dtype, N, Din, Hin, Win, Cin, Cout, target_wgs, &TT, &vps), G = 8 / TT;
   if (ci128) {
-    constexpr int lds = 10 * 64 * 128;
+    dim3 grid(splits, Cout / 64, (Cin / 128) * G);
     const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;
-    auto kern = nt ? convt_wgrad128_kernel<true> : convt_wgrad128_kernel<false>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(kern, grid, dim3(512), lds, s, (const bf16_t*)x, (const bf16_t*)dout, ws, g,
-                       Cin, Cout, vps, bpart);
+    const bool direct = splits == 1;
+    float* dst = direct ? dw : ws;
+    if (TT == 8) launch_wgrad128<8>(nt, direct, grid, s, (const bf16_t*)x, (const bf16_t*)dout, dst, g, Cin, Cout, vps, bpart);
+    else if (TT == 4) launch_wgrad128<4>(nt, direct, grid, s, (const bf16_t*)x, (const bf16_t*)dout, dst, g, Cin, Cout, vps, bpart);
+    else launch_wgrad128<2>(nt, direct, grid, s, (const bf16_t*)x, (const bf16_t*)dout, dst, g, Cin, Cout, vps, bpart);
     if (bpart != nullptr) {
       hipError_t eb = hipGetLastError();
       if (eb != hipSuccess) return (int)eb;
-      hipLaunchKernelGGL(convt_bias_reduce, dim3(cdiv(Cout, 8)), dim3(256), 0, s, (const float*)bpart, splits, Cout,
-                         db);
+      hipLaunchKernelGGL(convt_bias_reduce, dim3(cdiv(Cout, 8)), dim3(256), 0, s, (const float*)bpart, splits * G,
+                         Cout, db);
     }
+    if (direct) PCMS_CHECK_LAUNCH();
+  }
+  dim3 grid(splits, Cout / 64, Cin / 64);
+  if (ci128) {
+    // launched above
   } else if (dtype == PCMS_BF16) {
     constexpr int lds = 9 * CW<bf16_t>::VB * 128;
     (void)hipFuncSetAttribute((const void*)convt_wgrad_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1248,7 +1335,9 @@ int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, floa
 // path) or pcms_box_channel_sum's rows (the other paths), whichever is larger
 int pcms_convt_wgrad_bias_ws_floats(int dtype, int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs) {
   int vps;
-  const int fused = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, target_wgs, &vps) * Cout;
+  int TT;
+  const int splits = convt_wgrad_plan(dtype, N, Din, Hin, Win, Cin, Cout, target_wgs, &TT, &vps);
+  const int fused = splits * (8 / TT) * Cout;
   const int box = pcms_box_channel_sum_ws_floats(dtype, N, Cout, 2 * Din, 2 * Hin, 2 * Win);
   return std::max(fused, box);
 }

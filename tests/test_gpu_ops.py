@@ -562,6 +562,43 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     close(db2.cpu(), br.grad, 1e-4 if code else 1e-5, "convT bias grad (fused)")
 
 
+@pytest.mark.parametrize("tt", [0, 8, 4, 2])
+@pytest.mark.parametrize("Sin,Sout,cin,cout,target", [((8, 8, 4), (16, 16, 8), 1024, 512, 256),   # one split: dw direct
+                                                      ((8, 8, 4), (16, 16, 8), 1024, 512, 1024),
+                                                      ((5, 6, 3), (11, 12, 7), 256, 128, 2048),  # ragged, F.pad ring
+                                                      ((16, 16, 8), (32, 32, 16), 512, 256, 1024)])
+def test_convt_wgrad_taps(tt, Sin, Sout, cin, cout, target):
+    """The bf16 ConvTranspose weight + bias gradient with the 8 taps over 8 / TT workgroups
+    (fewer voxel splits; one split writes dw directly, += onto what it holds) against fp64."""
+    L = _lib()
+    g = torch.Generator().manual_seed(11)
+    N = 2
+    x = torch.randn(N, cin, *Sin, generator=g).bfloat16()
+    w = (torch.randn(cin, cout, 2, 2, 2, generator=g) / math.sqrt(cin)).bfloat16()
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    br = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    u = F.conv_transpose3d(xr, wr, br, stride=2)
+    dz, dyy, dxx = (Sout[i] - u.shape[2 + i] for i in range(3))
+    up = F.pad(u, [dxx // 2, dxx - dxx // 2, dyy // 2, dyy - dyy // 2, dz // 2, dz - dz // 2])
+    gout = torch.randn(up.shape, generator=g).bfloat16()
+    up.backward(gout.double())
+    w0 = torch.randn(cin, cout, 2, 2, 2, generator=g)  # the accumulation target's prior content
+    b0 = torch.randn(cout, generator=g)
+    old = L.query("pcms_convt_wgrad_taps", tt)
+    try:
+        ws = torch.empty(L.query("pcms_convt_wgrad_ws_floats", N, *Sin, cin, cout, target), device=DEV)
+        bws = torch.empty(L.query("pcms_convt_wgrad_bias_ws_floats", 1, N, *Sin, cin, cout, target), device=DEV)
+        dw, db = w0.to(DEV), b0.to(DEV)
+        L.call("pcms_convt_wgrad_bias", 1, ndhwc(x).to(DEV), ndhwc(gout).to(DEV), dw, db, ws, bws, N, *Sin, cin,
+               cout, *Sout, target)
+        torch.cuda.synchronize()
+    finally:
+        L.query("pcms_convt_wgrad_taps", old)
+    close(dw.cpu() - w0, wr.grad, 1e-4, f"convT wgrad TT={tt}")
+    close(db.cpu() - b0, br.grad, 1e-4, f"convT bias grad TT={tt}")
+
+
 @pytest.mark.parametrize("Sin,Sout", [((32, 32, 24), (64, 64, 48)), ((24, 20, 12), (49, 41, 25))])
 def test_convt_fwd_stream(Sin, Sout):
     """The persistent level-0 ConvTranspose forward (Cin 128, Cout 64; several 64-voxel tiles
