@@ -200,6 +200,11 @@ int pcms_convt_pack_elems(int dtype, int Cin, int Cout);
 int pcms_convt_pack(int dtype, const float* w, void* out, int Cin, int Cout, int dgrad, hipStream_t s);
 int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bias, void* out,
                    int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
+/* the same with a K-split workspace for small grids (bf16; fp32 partials summed in a fixed
+   order with the bias): ws = pcms_convt_fwd_ws_floats(...) floats (0: no split, ws may be NULL) */
+int pcms_convt_fwd_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout);
+int pcms_convt_fwd_ws(int dtype, const void* x, const void* wpack, const float* bias, void* out, float* ws,
+                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
 int pcms_convt_dgrad(int dtype, const void* dout, const void* wpack_d, void* dx,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s);
 /* the same with an fp32 workspace of pcms_convt_dgrad_ws_floats(...) floats (0: none needed):

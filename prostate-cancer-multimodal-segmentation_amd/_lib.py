@@ -62,6 +62,8 @@ SIGNATURES = {
     "pcms_convt_pack_elems": "iii",
     "pcms_convt_fwd_stream": "i",
     "pcms_convt_fwd": "ippppiiiiiiiiis",
+    "pcms_convt_fwd_ws_floats": "iiiiii",
+    "pcms_convt_fwd_ws": "ipppppiiiiiiiiis",
     "pcms_convt_dgrad": "ipppiiiiiiiiis",
     "pcms_convt_dgrad_ws_floats": "iiiiii",
     "pcms_convt_dgrad_ws": "ippppiiiiiiiiis",

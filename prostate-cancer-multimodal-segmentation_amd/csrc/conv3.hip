@@ -1015,9 +1015,15 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
 #pragma unroll
           for (int k = 0; k < kPer; ++k) {
             const int q4 = tid + k * kWThreads, row = q4 / 216, q = q4 % 216;
+#if defined(WGRAD_ABL) && (WGRAD_ABL & 1)  // ablation build: the flush's global stores dropped
+            const f32x4_t o = g[k] + *reinterpret_cast<const f32x4_t*>(tile + row * 864 + 4 * q);
+            if (q4 < kQ && o[0] == 1.2345e30f)
+              *reinterpret_cast<f32x4_t*>(p.dw + ((long)(co_base + ct * 32 + row) * p.cw + ci_base) * 27 + 4 * q) = o;
+#else
             if (q4 < kQ)
               *reinterpret_cast<f32x4_t*>(p.dw + ((long)(co_base + ct * 32 + row) * p.cw + ci_base) * 27 + 4 * q) =
                   g[k] + *reinterpret_cast<const f32x4_t*>(tile + row * 864 + 4 * q);
+#endif
           }
         } else {
           for (int i = tid; i < 32 * 32 * 27; i += kWThreads) {

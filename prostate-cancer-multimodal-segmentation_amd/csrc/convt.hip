@@ -493,7 +493,19 @@ __global__ void __launch_bounds__(512, 2) convt_lds_kernel(const bf16_t* a_src, 
     }
     __syncthreads();
   }
-  if constexpr (FWD) {
+  if constexpr (FWD && SPLIT) {
+    // fp32 partials ws[z][m][q] (q = GEMM column = tap x Cout + co), summed in z order with
+    // the bias by convt_fwd_reduce
+    const long Q = 8L * Cout;
+    float* part = ws + (long)blockIdx.z * M * Q + q0 + 2 * r_lane;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const long m = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
+      if (m >= M) continue;
+      *reinterpret_cast<f32x2_t*>(part + m * Q) = f32x2_t{acc[0][e], acc[1][e]};
+      *reinterpret_cast<f32x2_t*>(part + m * Q + 64) = f32x2_t{acc[2][e], acc[3][e]};
+    }
+  } else if constexpr (FWD) {
     long dq[2];
     int cq[2];
     float b0[2], b1[2];
@@ -562,6 +574,23 @@ __global__ void __launch_bounds__(256) convt_dgrad_reduce(const float* ws, int S
     d[0] = pack_bf16x2(a[0], a[1]);
     d[1] = pack_bf16x2(a[2], a[3]);
   }
+}
+
+// forward K splits: out[child(m, t)][co] = bf16(sum over z = 0..S-1 of ws[z][m][t Cout + co] +
+// bias[co]), z in order; 4 columns (one tap, Cout % 4 == 0) per thread
+__global__ void __launch_bounds__(256) convt_fwd_reduce(const float* ws, int S, long M, int Cout,
+                                                        const float* bias, bf16_t* out, UpGeom g) {
+  const long Q = 8L * Cout, E = M * Q;
+  const long i = (blockIdx.x * 256L + threadIdx.x) * 4;
+  if (i >= E) return;
+  f32x4_t a = *reinterpret_cast<const f32x4_t*>(ws + i);
+  for (int z = 1; z < S; ++z) a += *reinterpret_cast<const f32x4_t*>(ws + (long)z * E + i);
+  const long m = i / Q;
+  const int q = (int)(i % Q), t = q / Cout, co = q % Cout;
+  uint2 o;
+  o.x = pack_bf16x2(a[0] + bias[co], a[1] + bias[co + 1]);
+  o.y = pack_bf16x2(a[2] + bias[co + 2], a[3] + bias[co + 3]);
+  *reinterpret_cast<uint2*>(out + child_vox(g, m, t) * Cout + co) = o;
 }
 
 // ---- weight gradient: C[p = ci][q = (t, co)] over K = input voxels ----
@@ -1087,8 +1116,30 @@ int pcms_convt_pack_elems(int dtype, int Cin, int Cout) {
 constexpr int kX6MT = 4;
 static bool x6_mt4(long M, long colblocks) { return cdiv(M, 128 * kX6MT) * colblocks >= device_cus(); }
 
+// K splits of the bf16 LDS forward: doubled while the grid is under 256 workgroups (level 4:
+// 64 workgroups x 16 stages -> 256 x 4), each a power of two dividing the Cin / 64 stages
+static int convt_fwd_splits(long M, int Cin, int Cout) {
+  if (Cin % 64 || (8 * Cout) % kCDN) return 1;
+  const long wgs = cdiv(M, kCDM) * (8 * Cout / kCDN);
+  const int nst = Cin / 64;
+  int S = 1;
+  while (wgs * S < 256 && S < 16 && nst % (2 * S) == 0) S *= 2;
+  return S;
+}
+
+int pcms_convt_fwd_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout) {
+  const long M = (long)N * Din * Hin * Win, S = convt_fwd_splits(M, Cin, Cout);
+  const long f = S > 1 ? S * M * 8 * Cout : 0;
+  return f >= (1L << 31) ? -7 : (int)f;
+}
+
 int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bias, void* out,
                    int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
+  return pcms_convt_fwd_ws(dtype, x, wpack, bias, out, nullptr, N, Din, Hin, Win, Cin, Cout, Do, Ho, Wo, s);
+}
+
+int pcms_convt_fwd_ws(int dtype, const void* x, const void* wpack, const float* bias, void* out, float* ws,
+                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo, hipStream_t s) {
   if (Cin % 16 || Cout % 64) return -1;
   UpGeom g = make_geom(N, Din, Hin, Win, Do, Ho, Wo);
   if ((long)N * Do * Ho * Wo >= (1L << 31)) return -7;  // 32-bit voxel index math
@@ -1105,6 +1156,17 @@ int pcms_convt_fwd(int dtype, const void* x, const void* wpack, const float* bia
     PCMS_CHECK_LAUNCH();
   }
   if (dtype == PCMS_BF16 && Cin % 64 == 0 && (8 * Cout) % kCDN == 0) {
+    const int S = ws ? convt_fwd_splits(M, Cin, Cout) : 1;
+    if (S > 1) {
+      auto kern = convt_lds_kernel<true, false, true>;
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);
+      hipLaunchKernelGGL(kern, dim3(cdiv(M, kCDM), 8 * Cout / kCDN, S), dim3(512), kCDStage, s,
+                         (const bf16_t*)x, (const bf16_t*)wpack, bias, (bf16_t*)out, g, Cin, Cout, ws);
+      const long E = M * 8 * Cout;
+      hipLaunchKernelGGL(convt_fwd_reduce, dim3((unsigned)cdiv(E / 4, 256)), dim3(256), 0, s, (const float*)ws, S, M,
+                         Cout, bias, (bf16_t*)out, g);
+      PCMS_CHECK_LAUNCH();
+    }
     const bool nt = 2L * N * Do * Ho * Wo * Cout >= kNtBytes;
     auto kern = nt ? convt_lds_kernel<true, true> : convt_lds_kernel<true, false>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kCDStage);

@@ -584,6 +584,9 @@ class UNetEngine:
         # the ConvT dgrad's K slabs share it (the weight gradient has reduced it by then)
         ctws += [query("pcms_convt_dgrad_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels)
                  for i, up in enumerate(self.ups)]
+        # and the forward's K slabs (free in the forward pass)
+        ctws += [query("pcms_convt_fwd_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels)
+                 for i, up in enumerate(self.ups)]
         b["ctws"] = torch.empty(max(ctws), dtype=torch.float32, device=dev)
         self.bufs = b
         self.buf_key = key
@@ -732,8 +735,8 @@ class UNetEngine:
             l = 3 - i
             up = self.ups[i]
             fpack, _ = self.convt_packs[i]
-            call("pcms_convt_fwd", self.code, h, fpack, up.bias, b[f"d{l}_u"], N, *S[l + 1], up.in_channels,
-                 up.out_channels, *S[l])
+            call("pcms_convt_fwd_ws", self.code, h, fpack, up.bias, b[f"d{l}_u"], b["ctws"], N, *S[l + 1],
+                 up.in_channels, up.out_channels, *S[l])
             self._block_fwd(self.dec[i], b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], self._dec_acts(l), N, S[l],
                             training)
             h = b[f"d{l}_a2"]

@@ -530,6 +530,11 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     L.call("pcms_convt_pack", code, wdev, dp, cin, cout, 1)
     out = torch.full((N, *Sout, cout), float("nan"), dtype=dt, device=DEV)
     L.call("pcms_convt_fwd", code, ndhwc(x).to(DEV), fp, b.to(DEV), out, N, *Sin, cin, cout, *Sout)
+    # K-split forward (fp32 slabs summed in a fixed order with the bias) where the grid is small
+    nfs = L.query("pcms_convt_fwd_ws_floats", N, *Sin, cin, cout)
+    outs = torch.full_like(out, float("nan"))
+    fws = torch.full((max(nfs, 1),), float("nan"), device=DEV)
+    L.call("pcms_convt_fwd_ws", code, ndhwc(x).to(DEV), fp, b.to(DEV), outs, fws, N, *Sin, cin, cout, *Sout)
     god = ndhwc(gout).to(DEV)
     dx = torch.empty(N, *Sin, cin, dtype=dt, device=DEV)
     L.call("pcms_convt_dgrad", code, god, dp, dx, N, *Sin, cin, cout, *Sout)
@@ -554,6 +559,8 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
     L.call("pcms_convt_wgrad_bias", code, ndhwc(x).to(DEV), god, dw2, db2, ws, bws2, N, *Sin, cin, cout, *Sout, 64)
     torch.cuda.synchronize()
     close(ncdhw(out.cpu()), up.detach(), tol, "convT fwd (+pad)")
+    close(ncdhw(outs.cpu()), up.detach(), tol, "convT fwd (+pad, K-split)")
+    assert nfs > 0 or not code or (Sin, cin) not in (((8, 8, 4), 1024), ((2, 2, 3), 128)), "small grids split"
     close(ncdhw(dx.cpu()), xr.grad, tol, "convT dgrad")
     close(ncdhw(dxs.cpu()), xr.grad, tol, "convT dgrad (K-split)")
     close(dw.cpu(), wr.grad, 1e-4 if code else 2e-5, "convT wgrad")

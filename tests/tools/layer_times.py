@@ -31,6 +31,10 @@ def flops(name, a):
         return 2 * 8 * a[9] * a[10] * a[5] * a[6] * a[7] * a[8]
     if name == "pcms_convt_dgrad":
         return 2 * 8 * a[8] * a[9] * a[4] * a[5] * a[6] * a[7]
+    if name == "pcms_convt_fwd_ws":
+        return 2 * 8 * a[10] * a[11] * a[6] * a[7] * a[8] * a[9]
+    if name == "pcms_convt_wgrad_bias":
+        return 2 * 8 * a[11] * a[12] * a[7] * a[8] * a[9] * a[10]
     return 0
 
 
@@ -47,6 +51,10 @@ def desc(name, a):
         return f"bn({a[2]})->{a[12]} {a[9]}x{a[10]}x{a[11]}"
     if name in ("pcms_convt_fwd", "pcms_convt_wgrad", "pcms_convt_dgrad_ws"):
         return f"{a[9]}->{a[10]} {a[6]}x{a[7]}x{a[8]}"
+    if name == "pcms_convt_fwd_ws":
+        return f"{a[10]}->{a[11]} {a[7]}x{a[8]}x{a[9]}"
+    if name == "pcms_convt_wgrad_bias":
+        return f"{a[11]}->{a[12]} {a[8]}x{a[9]}x{a[10]}"
     return ""
 
 
