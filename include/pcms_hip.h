@@ -55,11 +55,13 @@ int pcms_conv3_mblocks(int N, int D, int H, int W);/* general-kernel M blocks (a
  * pcms_conv3_mblocks rows                                                               */
 int pcms_conv3_fwd_rows(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout);
 int pcms_conv3_big_min_boxes(int v);               /* set (v > 0) / query; returns old */
-int pcms_conv3_big_max_wgs(int v);
+int pcms_conv3_big_max_wgs(int v);                 /* persistent grid cap: set (v >= 0,
+                                                      0 = one per CU) / query; old      */
 /* general-kernel boxes of <= 256 voxels (level 4) on four waves of 2 M-tiles (1, default)
  * or two waves of 4 (0); v < 0 queries; returns the previous setting                   */
-int pcms_conv3_small_box_mtw2(int v);                 /* persistent grid cap: set (v >= 0,
-                                                      0 = one per CU) / query; old      */
+int pcms_conv3_small_box_mtw2(int v);
+/* A/B switch: general forward / dgrad box volume, 512 or 256 voxels (v <= 0 queries) */
+int pcms_conv3_fwd_box_vol(int v);
 /* master W [Cout][Cin][3][3][3] fp32 -> kernel pack; flip=1 builds the dgrad pack      */
 int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int flip, hipStream_t s);
 // Both packs of one conv (forward and dgrad, as pcms_conv3_pack flip 0 / 1) from one read of w.

@@ -23,6 +23,7 @@ SIGNATURES = {
     "pcms_conv3_fwd_rows": "iiiiiiii",
     "pcms_conv3_big_min_boxes": "i",
     "pcms_conv3_big_max_wgs": "i",
+    "pcms_conv3_fwd_box_vol": "i",
     "pcms_conv3_small_box_mtw2": "i",
     "pcms_conv3_pack": "ippiiis",
     "pcms_conv3_pack2": "ipppiis",

@@ -1770,6 +1770,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 // to give every CU one (pcms_conv3_big_min_boxes), every byte offset inside a 32-bit voffset
 static int g_big_min_boxes = 256;
 static int g_conv_mtw2 = 1;  // boxes of <= 256 voxels on 2 M-tiles per wave (A/B switch)
+static int g_fwd_box_vol = 512;  // general forward / dgrad box volume (512 or 256; A/B switch)
 static int g_big_max_wgs = 0;  // persistent grid cap (0: one workgroup per CU)
 static bool big_fwd_ok(int dtype, int N, int D, int H, int W, int c0, int c1) {
   if (dtype != PCMS_BF16 || D % kBgBD || H % 8 || W % 16 || c0 % 16 || c1 % 16 || c0 < 16) return false;
@@ -1791,7 +1792,7 @@ extern "C" {
 // Returns the m-block count (workgroups along M) of the general fwd kernel for a grid
 // (an upper bound on every fwd path's BatchNorm row count; sizes the split decision).
 int pcms_conv3_mblocks(int N, int D, int H, int W) {
-  Box b = fwd_box(D, H, W);
+  Box b = fwd_box(D, H, W, g_fwd_box_vol);
   return N * cdiv(D, 1 << b.lbd) * cdiv(H, 1 << b.lbh) * cdiv(W, 1 << b.lbw);
 }
 
@@ -1820,6 +1821,14 @@ int pcms_conv3_big_max_wgs(int v) {
 
 // general-kernel boxes of <= 256 voxels on four waves of 2 M-tiles (1) or two of 4 (0);
 // v < 0 queries; returns the previous setting
+// general-kernel forward / dgrad box volume: 512 or 256 voxels; v <= 0 queries; returns the
+// previous setting (A/B switch: set before any workspace query)
+int pcms_conv3_fwd_box_vol(int v) {
+  const int old = g_fwd_box_vol;
+  if (v == 256 || v == 512) g_fwd_box_vol = v;
+  return old;
+}
+
 int pcms_conv3_small_box_mtw2(int v) {
   const int old = g_conv_mtw2;
   if (v >= 0) g_conv_mtw2 = v;
@@ -1938,7 +1947,7 @@ static int conv3_fwd_any(int dtype, const void* x0, int c0, const void* x1, int 
   if (flags & ~(PCMS_CONV_ACCUMULATE | PCMS_CONV_RELU)) return -8;
   if (y1 == nullptr) cy0 = Cout;
   if (cy0 % 64 != 0 && cy0 != Cout) return -2;
-  Box b = fwd_box(D, H, W);
+  Box b = fwd_box(D, H, W, g_fwd_box_vol);
   Conv3Params p;
   p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1;
   p.isc = isc; p.ish = ish;

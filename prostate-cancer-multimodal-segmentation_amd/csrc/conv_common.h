@@ -157,13 +157,15 @@ Box choose_box(int D, int H, int W, int maxvol, int maxhalo, int minw, int minvo
   return best;
 }
 
-// Forward/dgrad box: 512 voxels; width 16 whenever the grid is that wide (perm32 layout).
-Box fwd_box(int D, int H, int W) {
+// Forward/dgrad box: `vol` (512 or 256) voxels; width 16 whenever the grid is that wide
+// (perm32 layout).
+Box fwd_box(int D, int H, int W, int vol = 512) {
+  const int lv = vol >= 512 ? 5 : 4;  // log2(bd * bh) at width 16
   if (W >= 16) {
     Box best{0, 0, 4};
     double bc = 1e30;
-    for (int a = 0; a <= 5; ++a) {
-      const int b = 5 - a;  // bd * bh = 32
+    for (int a = 0; a <= lv; ++a) {
+      const int b = lv - a;  // bd * bh = vol / 16
       const int bd = 1 << a, bh = 1 << b;
       if ((bd + 2) * (bh + 2) * 18 > kHaloMax) continue;
       const double cost = (double)cdiv(D, bd) * bd * cdiv(H, bh) * bh +
@@ -172,7 +174,7 @@ Box fwd_box(int D, int H, int W) {
     }
     return best;
   }
-  return choose_box(D, H, W, 512, kHaloMax, 4, 32);
+  return choose_box(D, H, W, vol >= 512 ? 512 : 256, kHaloMax, 4, 32);
 }
 
 // compute units of the current device (persistent-grid sizing)

@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--wgrad-target", type=int, default=0, help="engine.wgrad_target override")
     ap.add_argument("--split-target", type=int, default=0, help="engine.split_target override")
     ap.add_argument("--big-min-boxes", type=int, default=0, help="pcms_conv3_big_min_boxes override")
+    ap.add_argument("--fwd-box-vol", type=int, default=0, help="pcms_conv3_fwd_box_vol override (256)")
     ap.add_argument("--convt-taps", type=int, default=0, help="pcms_convt_wgrad_taps override (8 / 4 / 2)")
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
@@ -84,6 +85,9 @@ def main():
         tr.model.engine().wgrad_target = a.wgrad_target
     if a.split_target:
         tr.model.engine().split_target = a.split_target
+    if a.fwd_box_vol:
+        from pcms_amd import _lib as L
+        L.query("pcms_conv3_fwd_box_vol", a.fwd_box_vol)
     if a.convt_taps:
         from pcms_amd import _lib as L
         L.query("pcms_convt_wgrad_taps", a.convt_taps)
