@@ -573,7 +573,8 @@ def test_convt(dt, code, tol, Sin, Sout, cin, cout):
 @pytest.mark.parametrize("Sin,Sout,cin,cout,target", [((8, 8, 4), (16, 16, 8), 1024, 512, 256),   # one split: dw direct
                                                       ((8, 8, 4), (16, 16, 8), 1024, 512, 1024),
                                                       ((5, 6, 3), (11, 12, 7), 256, 128, 2048),  # ragged, F.pad ring
-                                                      ((16, 16, 8), (32, 32, 16), 512, 256, 1024)])
+                                                      ((16, 16, 8), (32, 32, 16), 512, 256, 1024),
+                                                      ((2, 2, 3), (5, 4, 7), 128, 64, 512)])  # one block: direct, every TT
 def test_convt_wgrad_taps(tt, Sin, Sout, cin, cout, target):
     """The bf16 ConvTranspose weight + bias gradient with the 8 taps over 8 / TT workgroups
     (fewer voxel splits; one split writes dw directly, += onto what it holds) against fp64."""
