@@ -728,8 +728,11 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad_kernel(const T* x, const T
 // staging.  blockIdx.z = ci tile x G + tap group.  DIRECT (one split): dw += the tile itself
 // (torch layout [Cin][Cout][8], each element owned by one workgroup), no partial rows.
 // Bias (ci tile 0): one [Cout] row per (split, tap group).
+#ifndef CTW_PF
+#define CTW_PF 1
+#endif
 template <bool NT, int TT, bool DIRECT>
-__global__ void __launch_bounds__(512, TT <= 4 ? 2 : 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout,
+__global__ void __launch_bounds__(512, (TT <= 4 && !CTW_PF) ? 2 : 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout,
                                                                              float* ws, UpGeom g, int Cin, int Cout,
                                                                              int vox_per_split, float* bpart) {
   constexpr int VB = 64, ROW = 128, PPR = 8, G = 8 / TT;
@@ -758,8 +761,11 @@ __global__ void __launch_bounds__(512, TT <= 4 ? 2 : 1) convt_wgrad128_kernel(co
   const char* Pq = P + (cq >> 1) * VB * ROW;
   const bool bias = bpart != nullptr && blockIdx.z < G;
   float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (long vb = vbeg; vb < vend; vb += VB) {
-    u32x4_t stg[PT];
+  // CTW_PF: the next block's pieces are loaded into registers right after this block's are
+  // written to LDS, so their latency runs under this block's MFMAs (without it each block's
+  // loads -> LDS -> MFMAs run in series)
+  u32x4_t stg[PT];
+  auto load_block = [&](long vb) {
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int pc = tid + i * 512;
@@ -780,6 +786,14 @@ __global__ void __launch_bounds__(512, TT <= 4 ? 2 : 1) convt_wgrad128_kernel(co
                   : *reinterpret_cast<const u32x4_t*>(src);
       if (vb + v >= vend) stg[i] = (u32x4_t){0u, 0u, 0u, 0u};
     }
+  };
+#if CTW_PF
+  if (vbeg < vend) load_block(vbeg);
+#endif
+  for (long vb = vbeg; vb < vend; vb += VB) {
+#if !CTW_PF
+    load_block(vb);
+#endif
     if (bias) {
 #pragma unroll
       for (int i = XP / 512; i < PT; ++i)  // the dout pieces (pc >= XP)
@@ -798,6 +812,9 @@ __global__ void __launch_bounds__(512, TT <= 4 ? 2 : 1) convt_wgrad128_kernel(co
       *reinterpret_cast<u32x4_t*>(lds + tile * VB * ROW + half_swz(v, q * 8)) = stg[i];
     }
     __syncthreads();
+#if CTW_PF
+    if (vb + VB < vend) load_block(vb + VB);
+#endif
 #pragma unroll
     for (int k0 = 0; k0 < VB; k0 += 16) {
       const int v = k0 + 8 * h + qq;
@@ -1278,7 +1295,9 @@ static int g_convt_wg_tt = 0;  // taps per workgroup of the bf16 128-ci weight g
 
 // The bf16 128-ci weight gradient's plan: taps per workgroup TT and the voxel splits.  By shape
 // (`tests/tools/convt_wgrad_sweep.py`, `profiles/r4_convt_wgrad_sweep*.txt`): TT = 2 for
-// Cin >= 256, 4 at Cin = 128, twice the workgroup target (the grids land at ~512 workgroups);
+// Cin >= 256 at twice the workgroup target (the grids land at ~512 workgroups), TT = 4 at
+// Cin = 128 at the target itself (103-107 us on both boxes measured; at twice the target 93
+// on one box but 124-127 on another, `r4_convt_wgrad_l1_boxes.txt`);
 // a plan of <= 2 splits runs as ONE split that writes dw directly (level 4: 49 -> 30 us; the
 // partial rows and their reduce launch cost more than the extra staging per workgroup).
 // pcms_convt_wgrad_taps(TT) pins TT at the plain target instead.  Other dtypes / Cin: TT = 8.
@@ -1294,7 +1313,8 @@ static int convt_wgrad_plan(int dtype, int N, int Din, int Hin, int Win, int Cin
   }
   if (target_wgs <= 0) target_wgs = 512;
   *tt = Cin >= 256 ? 2 : 4;
-  const int splits = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, 2 * target_wgs, vps, 8 / *tt);
+  const int splits = convt_wgrad_splits(N, Din, Hin, Win, Cin, Cout, Cin >= 256 ? 2 * target_wgs : target_wgs, vps,
+                                        8 / *tt);
   if (splits > 2) return splits;
   const long M = (long)N * Din * Hin * Win;
   *vps = (int)(cdiv(M, kVB) * kVB);
