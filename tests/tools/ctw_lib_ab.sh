@@ -1,6 +1,8 @@
 # ConvTranspose weight-gradient variants alternated on one box (test tooling):
 # convt_wgrad_sweep.py (auto plan) and layer_times with the product library, the depth-1
 # prefetch build (libpcms_hip_d1.so) and the no-prefetch build (libpcms_hip_nopf.so).
+# Build the variants first: tests/tools/ab_build.sh nopf -DCTW_PF=0; d1 = a library built
+# from the depth-1 revision of convt.hip (git show) with the other sources.
 cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 L=$PWD/prostate-cancer-multimodal-segmentation_amd
