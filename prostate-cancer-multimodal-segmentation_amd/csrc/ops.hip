@@ -471,7 +471,10 @@ __global__ void __launch_bounds__(TPB) bn_relu_pool_kernel(const T* y, T* a, T* 
       const int d = 2 * dc + (k >> 2), h = 2 * hc + ((k >> 1) & 1), w = 2 * wc + (k & 1);
       in[k] = d < D && h < H && w < W;
       vin[k] = ((n * D + d) * H + h) * W + w;
-      if (in[k]) ld16<NT>(y + vin[k] * C + cv * VEC, v[k]);
+#ifndef BRP_NTLOAD
+#define BRP_NTLOAD 1  // A/B: y loads non-temporal with the stores (1) or cached (0)
+#endif
+      if (in[k]) ld16<NT && BRP_NTLOAD>(y + vin[k] * C + cv * VEC, v[k]);
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
