@@ -151,7 +151,18 @@ template <typename T> __device__ __forceinline__ float round_st(float v) {
 }
 
 // streams this large bypass the caches (non-temporal loads / stores)
-constexpr long kNtBytes = 128L << 20;
+#ifndef PCMS_NT_MB
+#define PCMS_NT_MB 128  // A/B switch (build-time)
+#endif
+constexpr long kNtBytes = (long)PCMS_NT_MB << 20;
+// the BatchNorm / ReLU / pool passes stream level-1-sized tensors (67 MB) past the caches too:
+// their inputs were written a full conv earlier and their outputs are read a conv later
+// (A/B: BN rows -12..-15 us per step, the ConvTranspose forward +3 us at 64 MB: kept at 128
+// there, profiles/r4_nt_threshold_ab.txt)
+#ifndef PCMS_BN_NT_MB
+#define PCMS_BN_NT_MB 64
+#endif
+constexpr long kNtBytesBn = (long)PCMS_BN_NT_MB << 20;
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -1340,7 +1340,7 @@ int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const fl
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || TPB % (C / VEC)) return -1;
   const int grid = ew_grid(dtype, C, nvox);
-  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytesBn;
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL((nt ? bn_relu_kernel<bf16_t, true> : bn_relu_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0, s,
                        (const bf16_t*)y, (bf16_t*)a, scale, shift, C, nvox);
@@ -1384,7 +1384,7 @@ int pcms_bn_relu_bwd_finish(int dtype, const void* da, const void* y, const floa
                             hipStream_t s) {
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   if (C % VEC || (TPB % (C / VEC)) != 0) return -1;
-  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  const bool nt = nvox * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytesBn;
   hipError_t e;
   if (rows <= kSmallRows) {
     hipLaunchKernelGGL(colsum_finalize_small_kernel<true>, dim3(cdiv(C, 64)), dim3(64 * kCfRL), 0, s, part, rows, C,
@@ -1423,7 +1423,7 @@ int pcms_bn_relu_pool(int dtype, const void* y, void* a, void* p, const float* s
   if (cells * 8 >= (1L << 31)) return -7;  // 32-bit index math in the kernel
   const int CV = C / VEC;
   const int grid = cell_grid(cells * CV, CV, 8192);
-  const bool nt = (long)N * D * H * W * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytes;
+  const bool nt = (long)N * D * H * W * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytesBn;
   if (dtype == PCMS_BF16)
     hipLaunchKernelGGL((nt ? bn_relu_pool_kernel<bf16_t, true> : bn_relu_pool_kernel<bf16_t, false>), dim3(grid),
                        dim3(TPB), 0, s, (const bf16_t*)y, (bf16_t*)a, (bf16_t*)p, scale, shift, N, D, H, W, C);
