@@ -191,13 +191,117 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
                       f"{reps} back-to-back launches, median of 3"}
 
 
+class ClockProbe:
+    """Shader clock over a stretch of device work (pcms_clock_probe): a stamp is one tiny
+    launch of single-wave workgroups that record (s_memtime, s_memrealtime, CU location);
+    between two stamps a CU's average clock is d(memtime) / d(memrealtime) x 100 MHz.  The
+    cycle counters of different CUs carry different offsets, so only stamps written by the
+    same CU are paired (1024 workgroups per stamp: every CU appears in both).  Stamps are
+    enqueued on the current stream, outside the per-step events."""
+
+    def __init__(self, nblocks: int = 1024):
+        self.nblocks = nblocks
+
+    def stamp(self):
+        from pcms_amd import _lib as L
+        buf = torch.zeros(3 * self.nblocks, dtype=torch.int64, device="cuda")
+        L.call("pcms_clock_probe", buf, self.nblocks)
+        return buf
+
+    @staticmethod
+    def mhz(a, b):
+        """Per-XCD clock (MHz) between stamps a and b: the median over that XCD's CUs seen in
+        both stamps (first stamp of a CU in a, last in b)."""
+        first, last = {}, {}
+        for t, r, loc in a.view(-1, 3).cpu().tolist():
+            if loc not in first or r < first[loc][1]:
+                first[loc] = (t, r)
+        for t, r, loc in b.view(-1, 3).cpu().tolist():
+            if loc not in last or r > last[loc][1]:
+                last[loc] = (t, r)
+        per = {}
+        for loc, (ta, ra) in first.items():
+            if loc in last and last[loc][1] > ra:
+                tb, rb = last[loc]
+                per.setdefault(int(loc) & 0xff, []).append((tb - ta) / (rb - ra) * 100.0)
+        return {x: round(statistics.median(v), 1) for x, v in sorted(per.items())}
+
+    @staticmethod
+    def summary(per):
+        vals = list(per.values())
+        if not vals:
+            return None
+        return {"sclk_mhz": round(statistics.median(vals), 1), "sclk_mhz_min": min(vals), "sclk_mhz_max": max(vals),
+                "per_xcd": per}
+
+
+def stem_clock(tr, N, spatial, reps=30):
+    """The shader clock over `reps` back-to-back launches of each stem kernel (the product's
+    calls, on the training buffers, after the timed steps): the figure the stem roofline can
+    be normalised with.  Returns {"fwd": {...}, "wgrad": {...}} or None."""
+    from pcms_amd import _lib as L
+    eng = tr.model.engine()
+    if not (eng.stem_sup & 3) == 3 or eng.bufs is None:
+        return None
+    b = eng.bufs
+    D, H, W = spatial
+    cs = eng.convs[0]
+    bn = eng.enc[0].b0
+    dw = torch.zeros(64 * 5 * 27, device="cuda")
+    calls = {
+        "fwd": lambda: L.call("pcms_stem_fwd", b["xin"], eng.stem_pack, cs.mod.bias, b["e0_y1"], b["stats"], N, D, H,
+                              W, eng.stem_dense),
+        "wgrad": lambda: L.call("pcms_stem_wgrad_bn", b["xin"], b["gA0"], b["e0_y1"], bn.scale, bn.shift, bn.mean,
+                                bn.invstd, b["coef"], dw, b["dwt"], 5, N, D, H, W),
+    }
+    probe = ClockProbe()
+    out = {}
+    for name, fn in calls.items():
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a = probe.stamp()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        z = probe.stamp()
+        torch.cuda.synchronize()
+        s = ClockProbe.summary(ClockProbe.mhz(a, z)) or {}
+        s.pop("per_xcd", None)
+        s["us_per_launch"] = round(e0.elapsed_time(e1) / reps * 1e3, 1)
+        out[name] = s
+    return out
+
+
 def cpu_baseline(n, spatial):
     """The CPU oracle (a restatement of utils/trainer.py:179-195 on torch CPU fp32) timed on
     this host at the config batch: 1 warm-up + 3 timed BCEDice train steps, median."""
     from oracle import unet3d_cpu as ref
     from pcms_amd.synthetic import make_batch, step_seed
-    cores = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    # every core this process may run on (SURVEY §8d: torch.set_num_threads(len(affinity))),
+    # capped only by a cgroup CPU quota if one is set (threads beyond it would only time-slice)
+    affinity = max(1, len(os.sched_getaffinity(0)))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, math.ceil(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    cores = min(affinity, quota) if quota else affinity
     torch.set_num_threads(cores)
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     torch.manual_seed(0)
     sd = ref.init_params(5, 1)
     step = ref.RefStep(sd, lr=1e-4, loss="bce_dice")
@@ -208,7 +312,8 @@ def cpu_baseline(n, spatial):
         step.step(b["image"], b["label"])
         times.append(time.perf_counter() - t0)
     med = statistics.median(times[1:])
-    return {"value": round(n / med, 4), "unit": "volumes/s", "cores": cores, "kind": "port",
+    return {"value": round(n / med, 4), "unit": "volumes/s", "cores": cores, "kind": "port", "cpu_model": model,
+            "threads": torch.get_num_threads(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
             "sample": f"1 warm-up + 3 timed train steps (fwd+BCEDice+bwd+Adam), batch {n} x "
                       f"5x{'x'.join(map(str, spatial))}, torch CPU fp32, median {med:.1f} s/step"}
 
@@ -227,7 +332,7 @@ def timed_steps(tr, host_batches, warmup, steps, world):
     host enqueues ahead of the GPU, as a training loop without per-step host syncs does).
     Per-step times come from HIP events recorded on the compute stream at every step
     boundary; returns (per-step seconds, max over ranks), the wall time of the K steps, and
-    the last loss."""
+    the last loss, and the shader clock over the K steps (ClockProbe.summary, this rank)."""
     def loader():
         while True:
             yield from host_batches
@@ -239,15 +344,18 @@ def timed_steps(tr, host_batches, warmup, steps, world):
     if timer is not None:
         timer.clear()  # only the timed steps' launches count
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    probe = ClockProbe()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ck0 = probe.stamp()  # shader clock over the K steps: a stamp on each side, outside the step events
     evs[0].record()
     last = None
     for i in range(steps):
         last = tr.step_async(next(it))
         evs[i + 1].record()
+    ck1 = probe.stamp()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -257,7 +365,7 @@ def timed_steps(tr, host_batches, warmup, steps, world):
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     tt = tt.cpu().tolist()
-    return tt[:-1], tt[-1], last
+    return tt[:-1], tt[-1], last, ClockProbe.summary(ClockProbe.mhz(ck0, ck1))
 
 
 def main():
@@ -292,7 +400,7 @@ def main():
     if world > 1:
         sync = tr._grad_sync()[1]
         sync.exposed_events = []
-    ts, wall, last = timed_steps(tr, host, a.warmup, a.steps, world)
+    ts, wall, last, clock = timed_steps(tr, host, a.warmup, a.steps, world)
     timer = tr.model.engine().kernel_timer
     tr.model.engine().kernel_timer = None
     if world > 1:
@@ -322,6 +430,8 @@ def main():
     value = vols_step / med
     roof = stem_roofline(tr, a.batch, spatial, a.kernel_reps, in_step if len(in_step) == 2 else None) \
         if rank == 0 else None
+    if roof is not None and rank == 0:
+        roof["clock_standalone"] = stem_clock(tr, a.batch, spatial)
     # the fp32 parity build (the one that meets the 1e-3 logit bar) on the same batches
     fp32 = None
     if a.fp32_steps > 0 and a.precision != "fp32":
@@ -329,7 +439,7 @@ def main():
         torch.cuda.empty_cache()
         torch.manual_seed(0)
         tr32 = Trainer(dict(cfg, precision="fp32"))
-        ts32, _, _ = timed_steps(tr32, host, 2, a.fp32_steps, world)
+        ts32, _, _, _ = timed_steps(tr32, host, 2, a.fp32_steps, world)
         fp32 = round(vols_step / statistics.median(ts32), 3)
         del tr32
     cpu = None
@@ -357,6 +467,9 @@ def main():
                         "timing": "HIP events on the compute stream at every step boundary, K steps "
                                   "back to back between a barrier + synchronize on both sides"},
             "fp32_parity_build_value": fp32,
+            # the shader clock the XCDs held over the K timed steps (pcms_clock_probe stamps
+            # on both sides of them; rank 0): normalises the line against other boxes
+            "clock": clock,
         }
         if dp_info is not None:
             out["dp"] = dp_info

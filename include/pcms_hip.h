@@ -114,8 +114,8 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
  * does (other shapes: the general pcms_conv3_fwd / pcms_conv3_wgrad).                   */
 int pcms_stem_supported(int N, int D, int H, int W);
 int pcms_stem_pack_elems(void);
-/* the stem weight gradient's MFMA columns: 1 (default) dense tap rows x 16 for cin_w <= 5,
- * 0 taps x 8 channels; v < 0 queries; returns the previous setting                        */
+/* the stem weight gradient's MFMA columns: 0 (default) taps x 8 channels, 1 dense tap rows
+ * x 16 for cin_w <= 5; v < 0 queries; returns the previous setting                        */
 int pcms_stem_wgrad_dense(int v);
 int pcms_stem_pack(const float* w, void* out, int cin_w, hipStream_t s);
 /* y = stem conv(x) + bias; BatchNorm partial moments into stats, laid out as pcms_conv3_fwd
@@ -322,6 +322,15 @@ int pcms_add(int dtype, void* dst, const void* src, long n, hipStream_t s);
 /* NDHWC (Cs stored channels) -> NCDHW fp32 (first C channels): the sub-module outputs
  * (DoubleConv3D / Down3D / Up3D called on their own, models/unet3d.py:42-158)          */
 int pcms_unpack_output(int dtype, const void* in, float* out, int N, int C, int Cs, long V, hipStream_t s);
+
+/* ---- measurement (bench.py, not a training path) ----------------------------------- */
+/* One launch of nblocks single-wave workgroups; block b writes {s_memtime, s_memrealtime,
+ * XCC id} to out[3b .. 3b+2] (uint64).  Two probes around a stretch of work give each XCD's
+ * average shader clock over it: d(memtime) / d(memrealtime) x 100 MHz.                    */
+int pcms_clock_probe(void* out, int nblocks, hipStream_t s);
+/* check of the probe: every block spins `cycles` shader cycles and writes its own {t0, r0,
+ * t1, r1, XCC id} to out[5b ..] (tests/tools/clock_check.py)                              */
+int pcms_clock_spin(void* out, int nblocks, long cycles, hipStream_t s);
 
 #ifdef __cplusplus
 }

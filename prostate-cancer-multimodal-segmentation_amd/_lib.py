@@ -95,6 +95,8 @@ SIGNATURES = {
     "pcms_grad_clip": "plffippps",
     "pcms_add": "ippls",
     "pcms_unpack_output": "ippiiils",
+    "pcms_clock_probe": "pis",
+    "pcms_clock_spin": "pils",
 }
 
 _CT = {"i": ctypes.c_int, "l": ctypes.c_long, "d": ctypes.c_double, "f": ctypes.c_float,

@@ -1422,13 +1422,17 @@ constexpr int kBgDummy = 1024;
 constexpr int kBgStage = 64 * 128;                                        // per-M-group store slice
 constexpr int kBgRed = 4 * 64 * 3 * 4;                                    // BN moments
 constexpr int kBgLds = 2 * kBgBuf + kBgDummy + 4 * kBgStage + kBgRed + 64 * 4;  // + bias
+// BNIN: the input BatchNorm's scale / shift table [2][kBgBnMax] floats after that
+constexpr int kBgBnMax = 128;
+constexpr int kBgBnOff = kBgLds;
+constexpr int kBgLdsBn = kBgLds + 2 * kBgBnMax * 4;
 #ifndef BG_DIST
 #define BG_DIST 8  // 2: 1-1.5 % slower big-box launches (A/B, profiles/r4_bg_dist_ab.txt)
 #endif
 constexpr int kBgDist = BG_DIST;           // B prefetch distance (taps); (Dist + 1) | 27
 constexpr int kBgEpiStores = kBgMT * 2;    // 16-B stores per wave and box
 static_assert(27 % (kBgDist + 1) == 0, "B ring index must continue across chunks");
-static_assert(kBgLds <= 160 * 1024, "LDS");
+static_assert(kBgLdsBn <= 160 * 1024, "LDS");
 
 // hidden 16-B global load (the compiler's waitcnt pass does not count it): retired by
 // vm_wait2<N>, which also orders the register's readers after the wait
@@ -1460,7 +1464,6 @@ template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_wai
 // a separate HBM pass.  At a chunk's end each thread rewrites the pieces it staged for the
 // next chunk in LDS (their DMA has landed by the chunk-end vmcnt wait; out-of-range pieces,
 // the zero padding, are left zero), before the barrier that publishes the buffer.
-constexpr int kBgBnMax = 128;
 template <bool BNIN = false>
 __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Params p, uint32_t x0bytes,
                                                                      uint32_t x1bytes) {
@@ -1517,7 +1520,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     return (!dummy && voff != kOOB ? 1u << j : 0u) | ((uint32_t)((pc & 1) ^ ((hw_ >> 3) & 1)) << (8 + j));
   };
   // BNIN: the staged pieces of buffer `buf` (chunk `chunk`) -> relu(x sc + sh) in place
-  float* bnt = reinterpret_cast<float*>(lds + 2 * kBgBuf + kBgDummy + 4 * kBgStage + 4 * 64 * 3 * 4 + 64 * 4);
+  float* bnt = reinterpret_cast<float*>(lds + kBgBnOff);  // reserved by kBgLdsBn (BNIN launches)
   auto bn_apply = [&](int buf, int chunk, uint32_t pm) {
 #pragma unroll
     for (int j = 0; j < kBgPieces; ++j) {
@@ -1971,8 +1974,9 @@ static int conv3_fwd_any(int dtype, const void* x0, int c0, const void* x1, int 
     const long nvox = (long)N * D * H * W;
     const int nslot = big_slots(N, D, H, W, Cout);
     auto kern = p.isc ? conv3_fwd_big_kernel<true> : conv3_fwd_big_kernel<false>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kBgLds);
-    hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64)), dim3(kBgThreads), kBgLds, s, p,
+    const int ldsb = p.isc ? kBgLdsBn : kBgLds;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldsb);
+    hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64)), dim3(kBgThreads), ldsb, s, p,
                        (uint32_t)(nvox * c0 * 2), (uint32_t)(nvox * c1 * 2));
     PCMS_CHECK_LAUNCH();
   }

@@ -115,6 +115,9 @@ class UNetEngine:
         # pair (same arithmetic and rounding).  False: the a1 pass (A/B)
         self.fuse_bnin = True
         self._bnin_cache = {}
+        # the blocks whose training forward ran fused (id(BlockSpec)): the backward and the
+        # checkpointed recompute follow the forward's decision, not the current settings
+        self._fwd_bnin = set()
         self.stem_pack = None
         self._flat_ptrs = None
         self._packed_version = -1
@@ -677,7 +680,13 @@ class UNetEngine:
                 call("pcms_maxpool_fwd", self.code, a2, pool_out, N, *S, blk.c1.cout)
             return
         self._conv(blk.c0, x0, c0, x1, c1, out["y1"], N, S, True, training, blk.b0, recompute)
-        if self._bnin(blk, N, S):  # a1 is never stored: the second conv applies BN0 + ReLU itself
+        if recompute:
+            bnin = id(blk) in self._fwd_bnin
+        else:
+            bnin = self._bnin(blk, N, S)
+            if training:
+                (self._fwd_bnin.add if bnin else self._fwd_bnin.discard)(id(blk))
+        if bnin:  # a1 is never stored: the second conv applies BN0 + ReLU itself
             self._conv(blk.c1, out["y1"], blk.c0.cout, None, 0, out["y2"], N, S, True, training, blk.b1, recompute,
                        bnin=blk.b0)
         else:
@@ -775,7 +784,7 @@ class UNetEngine:
         elif ga2 is not None:
             self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         with self._side():
-            if self._bnin(blk, N, S):  # x = relu(bn0(y1)), applied in the kernel's staging
+            if id(blk) in self._fwd_bnin:  # x = relu(bn0(y1)), applied in the kernel's staging (as the forward)
                 call("pcms_conv3_wgrad_bnin", blk.c1.code, acts["y1"], blk.c0.cout, blk.b0.scale, blk.b0.shift, gY,
                      blk.c1.mod.weight.grad, b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target,
                      int(self._gstore))
