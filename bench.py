@@ -205,7 +205,10 @@ class ClockProbe:
     def stamp(self):
         from pcms_amd import _lib as L
         buf = torch.zeros(3 * self.nblocks, dtype=torch.int64, device="cuda")
-        L.call("pcms_clock_probe", buf, self.nblocks)
+        # the raw entry point (tools may wrap _lib.call to time every library call)
+        rc = L.load().pcms_clock_probe(buf.data_ptr(), self.nblocks, L.stream())
+        if rc != 0:
+            raise L.HipError(f"pcms_clock_probe failed with status {rc}")
         return buf
 
     @staticmethod

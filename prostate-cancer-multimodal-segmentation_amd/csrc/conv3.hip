@@ -154,11 +154,21 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
     const bf16_t* wchunk = wp + (long)chunk * 27 * p.Cout * Tr::WK;
     Frag bset[2][2][Tr::KS];
     auto load_b = [&](Frag (&dst)[2][Tr::KS], int tap) {
-      const bf16_t* wt = wchunk + ((long)tap * p.Cout + co_base + r_lane) * Tr::WK;
+      if constexpr (std::is_same<T, bf16_t>::value) {
+        // fragment-major pack (pack_bf16_off): block (row tile, ks) = one contiguous 1 KiB
+        const bf16_t* wt = wchunk + ((long)tap * p.Cout + co_base) * 32 + lane * 8;
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int ks = 0; ks < Tr::KS; ++ks) dst[nt][ks] = gl_b(wt + nt * 32 * Tr::WK, ks, hsel);
+          for (int ks = 0; ks < Tr::KS; ++ks)
+            dst[nt][ks] = *reinterpret_cast<const s16x8_t*>(wt + nt * 1024 + ks * 512);
+      } else {
+        const bf16_t* wt = wchunk + ((long)tap * p.Cout + co_base + r_lane) * Tr::WK;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int ks = 0; ks < Tr::KS; ++ks) dst[nt][ks] = gl_b(wt + nt * 32 * Tr::WK, ks, hsel);
+      }
     };
     load_b(bset[0], 0);
     // The A fragments roll through one register set: right after M-tile mt's MFMAs of tap t
@@ -1156,6 +1166,8 @@ __global__ void __launch_bounds__(256) pack_conv3_kernel(const float* w, T* out,
       o[k] = h; o[CK + k] = h;
       o[2 * CK + k] = m; o[3 * CK + k] = h;
       o[4 * CK + k] = l; o[5 * CK + k] = m;
+    } else if constexpr (std::is_same<T, bf16_t>::value) {
+      out[pack_bf16_off(chunk, t, j0 + jj, k, J)] = Elem<T>::cvt(v);
     } else {
       out[(((long)chunk * 27 + t) * J + j0 + jj) * CK + k] = Elem<T>::cvt(v);
     }
@@ -1195,16 +1207,16 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_kernel(const float* w, bf
     u32x4_t o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(tile[jj][k8 + 2 * i][ts], tile[jj][k8 + 2 * i + 1][ts]);
-    *reinterpret_cast<u32x4_t*>(out + (((long)chunk * 27 + t) * J + j0 + jj) * 32 + k8) = o;
+    *reinterpret_cast<u32x4_t*>(out + pack_bf16_off(chunk, t, j0 + jj, k8, J)) = o;
   }
 }
 
 // Both bf16 packs of one conv from ONE read of the fp32 weight (Cin % 32 == Cout % 32 == 0).
 // Block (co j0 .. j0+32, ci c*32 .. +32): the 32 contiguous 864-float runs w[co][c*32..][27]
 // are converted to bf16 once into LDS (same rounding as pack_bf16x2), then both packs are
-// written as whole 64-B rows:
-//   fwd   [ci/32][t][co][ci%32] = w[co][ci][t]
-//   dgrad [co/32][t][ci][co%32] = w[co][ci][26 - t]
+// written as 16-B pieces of the fragment-major layout (pack_bf16_off):
+//   fwd   (c = ci/32, t, j = co, k = ci%32) = w[co][ci][t]
+//   dgrad (c = co/32, t, j = ci, k = co%32) = w[co][ci][26 - t]
 __global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* w, bf16_t* fwd, bf16_t* dgr,
                                                                    int Cout, int Cin) {
   __shared__ __attribute__((aligned(16))) uint16_t tb[32 * 864];
@@ -1232,7 +1244,7 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       o[i] = (uint32_t)tb[co * 864 + (k8 + 2 * i) * 27 + t] | ((uint32_t)tb[co * 864 + (k8 + 2 * i + 1) * 27 + t] << 16);
-    *reinterpret_cast<u32x4_t*>(fwd + (((long)chunk * 27 + t) * Cout + j0 + co) * 32 + k8) = o;
+    *reinterpret_cast<u32x4_t*>(fwd + pack_bf16_off(chunk, t, j0 + co, k8, Cout)) = o;
   }
   for (int g = threadIdx.x; g < 27 * 128; g += 256) {
     const int t = g >> 7, ci = (g >> 2) & 31, k8 = (g & 3) * 8, ts = 26 - t;
@@ -1240,7 +1252,7 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       o[i] = (uint32_t)tb[(k8 + 2 * i) * 864 + ci * 27 + ts] | ((uint32_t)tb[(k8 + 2 * i + 1) * 864 + ci * 27 + ts] << 16);
-    *reinterpret_cast<u32x4_t*>(dgr + (((long)(j0 >> 5) * 27 + t) * Cin + chunk * 32 + ci) * 32 + k8) = o;
+    *reinterpret_cast<u32x4_t*>(dgr + pack_bf16_off(j0 >> 5, t, chunk * 32 + ci, k8, Cin)) = o;
   }
 }
 
@@ -1311,7 +1323,7 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       o[i] = (uint32_t)tb[co * 864 + (k8 + 2 * i) * 27 + t] | ((uint32_t)tb[co * 864 + (k8 + 2 * i + 1) * 27 + t] << 16);
-    *reinterpret_cast<u32x4_t*>(fwd + (((long)chunk * 27 + t) * Cout + j0 + co) * 32 + k8) = o;
+    *reinterpret_cast<u32x4_t*>(fwd + pack_bf16_off(chunk, t, j0 + co, k8, Cout)) = o;
   }
   for (int g = threadIdx.x; g < 27 * 128; g += 256) {
     const int t = g >> 7, ci = (g >> 2) & 31, k8 = (g & 3) * 8, ts = 26 - t;
@@ -1319,7 +1331,7 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       o[i] = (uint32_t)tb[(k8 + 2 * i) * 864 + ci * 27 + ts] | ((uint32_t)tb[(k8 + 2 * i + 1) * 864 + ci * 27 + ts] << 16);
-    *reinterpret_cast<u32x4_t*>(dgr + (((long)(j0 >> 5) * 27 + t) * Cin + chunk * 32 + ci) * 32 + k8) = o;
+    *reinterpret_cast<u32x4_t*>(dgr + pack_bf16_off(j0 >> 5, t, chunk * 32 + ci, k8, Cin)) = o;
   }
 }
 
@@ -1392,9 +1404,10 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_x6_kernel(float* P, float
 // input channels in 16-channel chunks), PERSISTENT: one 8-wave workgroup per CU, one grid of
 // at most #CU workgroups; workgroup (slot, cob) computes 8 x 8 x 16 = 1024-voxel boxes
 // slot, slot + nslot, ... for its 64 output channels.  Wave w = (M-group mg = w & 3, N-tile
-// nt = w >> 2) owns voxel rows [256 mg, 256 mg + 256) = 8 M-tiles and the output channels of
-// parity nt, so every B fragment (weights, L2-resident) feeds 8 MFMAs and the two waves of a
-// SIMD overlap one's operand waits with the other's MFMAs.
+// nt = w >> 2) owns voxel rows [256 mg, 256 mg + 256) = 8 M-tiles and output channels
+// [32 nt, 32 nt + 32), so every B fragment (weights, L2-resident; one contiguous 1 KiB load
+// from the fragment-major pack, round 5) feeds 8 MFMAs and the two waves of a SIMD overlap
+// one's operand waits with the other's MFMAs.
 // The 10 x 10 x 18 halo of a chunk (32-B rows; the two 16-B halves swapped on odd row octets,
 // so 16 consecutive rows hit 16 distinct bank groups) is double-buffered: the next chunk's
 // halo -- the NEXT BOX's first chunk during a box's last chunk -- streams in by buffer
@@ -1402,7 +1415,7 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_x6_kernel(float* P, float
 // are read while tap t's 8 MFMAs run; B loads run Dist taps ahead across chunk and box
 // boundaries.  So only the first box of a workgroup waits for its operands; every later box
 // starts on a landed halo.  Epilogue per box: + bias, bf16 channels staged through the
-// M-group's 8 KiB LDS slice (two M-tiles at a time, the pair's even / odd channels) and
+// M-group's 8 KiB LDS slice (two M-tiles at a time, the pair's channel halves) and
 // written back as 16-B stores of whole 128-B channel rows (16 store instructions per wave and
 // box, issued without waiting: the B waits of the next box's first taps count them).
 // BatchNorm partials: per (M-group, channel) a running Chan merge over the boxes (count,
@@ -1428,6 +1441,12 @@ constexpr int kBgBnOff = kBgLds;
 constexpr int kBgLdsBn = kBgLds + 2 * kBgBnMax * 4;
 #ifndef BG_DIST
 #define BG_DIST 8  // 2: 1-1.5 % slower big-box launches (A/B, profiles/r4_bg_dist_ab.txt)
+#endif
+// ablation builds only (tests/tools/big_abl.py; 0 in the product): 1 halo DMA reads nothing
+// (out-of-range source, the same instructions), 2 no output stores, 4 no MFMAs (operands still
+// read), 8 no weight loads after the prologue, 16 no A-fragment LDS reads
+#ifndef BG_ABL
+#define BG_ABL 0
 #endif
 constexpr int kBgDist = BG_DIST;           // B prefetch distance (taps); (Dist + 1) | 27
 constexpr int kBgEpiStores = kBgMT * 2;    // 16-B stores per wave and box
@@ -1472,7 +1491,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r_lane = lane & 31, hsel = lane >> 5;
-  // wave = (M-group mg: box voxel rows 256 mg ..; N-tile nt: the output channels of parity nt)
+  // wave = (M-group mg: box voxel rows 256 mg ..; N-tile nt: output channels 32 nt .. 32 nt + 31)
   const int mg = wave & 3, nt = wave >> 2;
   const int Cout = p.Cout, ncob = Cout >> 6;
   // logical workgroup id: consecutive ids on one XCD (dispatch is round-robin over 8), output
@@ -1509,7 +1528,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
     uint32_t voff = kOOB;
     if (live && hv < kBgHalo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
-        (unsigned)gw < (unsigned)p.W)
+        (unsigned)gw < (unsigned)p.W && !(BG_ABL & 1))
       voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs +
               (uint32_t)((pc & 1) ^ ((hw_ >> 3) & 1)) * 8u) * 2u;
     const bool dummy = j == kBgPieces - 1 && wave > 0;  // wave-uniform
@@ -1561,13 +1580,17 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   const int nchunk = p.Cin >> 4;
   const uint32_t tap_bytes = (uint32_t)Cout * 64u;
   const i32x4_t wr = buffer_desc(p.w, (uint32_t)(p.Cin >> 5) * 27u * tap_bytes);
+  bool bl_prologue = true;  // BG_ABL & 8: only the prologue's weight loads run
   auto load_b = [&](s16x8_t& dst, int chunk, int tap, uint32_t boff) {
-    const uint32_t off = boff + (uint32_t)((chunk >> 1) * 27 + tap) * tap_bytes + (uint32_t)(chunk & 1) * 32u;
+    if ((BG_ABL & 8) && !bl_prologue) return;
+    // fragment-major pack (pack_bf16_off): the (32-chunk, tap) rows, boff = this wave's row
+    // tile and lane, then the k-step (chunk & 1): one contiguous 1 KiB per wave
+    const uint32_t off = boff + (uint32_t)((chunk >> 1) * 27 + tap) * tap_bytes + (uint32_t)(chunk & 1) * 1024u;
     bload16<0>(dst, wr, off);
   };
 
-  // epilogue constants: output columns are channel pairs (column j of N-tile nt = channel
-  // 2 j + nt); two-pointer output split at cy0 (workgroup-uniform)
+  // epilogue constants: column j of N-tile nt = channel 32 nt + j; two-pointer output split at
+  // cy0 (workgroup-uniform)
   // (bias and the running BatchNorm moments live in LDS between boxes, not in registers)
   float* red = reinterpret_cast<float*>(lds + 2 * kBgBuf + kBgDummy + 4 * kBgStage);  // [mg][64][3]
   float* bls = red + 4 * 64 * 3;                                           // [64]
@@ -1597,8 +1620,9 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 #pragma unroll
   for (int j = 0; j < kBgPieces; ++j) pmask |= stage_piece(n, d0, h0, w0, 0, 0, j, true);
 #pragma unroll
-  for (int t = 0; t < kBgDist; ++t) load_b(bset[t], 0, t, (uint32_t)((co_base + 2 * r_lane + nt) * 64 + hsel * 16));
+  for (int t = 0; t < kBgDist; ++t) load_b(bset[t], 0, t, (uint32_t)(((co_base >> 5) + nt) * 2048 + lane * 16));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bl_prologue = false;
   if constexpr (BNIN) bn_apply(0, 0, pmask);
   __syncthreads();
   int buf = 0;
@@ -1627,8 +1651,9 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
       int swk[3];
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) swk[kw] = hbase + kw * 32 + ((hs ^ ((((prow & 15) + kw) >> 3) & 1)) << 4);
-      const uint32_t boff = (uint32_t)((co_base + 2 * (lo & 31) + nt) * 64 + hs * 16);
+      const uint32_t boff = (uint32_t)(((co_base >> 5) + nt) * 2048 + lo * 16);
       auto read_a1 = [&](int tap, int mt) {
+        if constexpr ((BG_ABL & 16) != 0) tap = 0;
         const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
         return *reinterpret_cast<const s16x8_t*>(hl + swk[kw] + (kd * kBgHH + kh) * kBgHW * 32 +
                                                  ((mt >> 2) * kBgHH + 2 * (mt & 3)) * kBgHW * 32);
@@ -1654,8 +1679,9 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
         vm_wait1<bg_wait<kBgPieces, kBgDist>(tap) + extra>(b);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          acc[mt] = mfma(a[mt], b, acc[mt]);
-          if constexpr (tap + 1 < 27) a[mt] = read_a1(tap + 1, mt);
+          if constexpr ((BG_ABL & 4) != 0) asm volatile("" ::"v"(a[mt]), "v"(b));
+          else acc[mt] = mfma(a[mt], b, acc[mt]);
+          if constexpr (tap + 1 < 27 && (BG_ABL & 16) == 0) a[mt] = read_a1(tap + 1, mt);
         }
       });
       // the next chunk's halo has landed (the newest piece is followed by the B loads of the
@@ -1674,7 +1700,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 
     // ---- epilogue of this box, two M-tiles at a time: + bias, bf16 channels into the
     // M-group's LDS slice (row = 32 mm + C row, 128 B of 64 channels; the two waves of the
-    // group write the even / odd channels), read back as 4 x 16 B per lane and wave = whole
+    // group write channels 0-31 / 32-63), read back as 4 x 16 B per lane and wave = whole
     // 128-B channel rows, 16-B stores.  BatchNorm moments in the same pass, shifted by K
     // (the running mean; the bias before the first box): box mean K + S1 / n, M2 = S2 -
     // S1^2 / n, Chan-merged into the running moments.
@@ -1683,9 +1709,9 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     const int lane_o = opaque(lane);
     const long plane = (long)p.H * p.W;
     const long vbase = (((long)n * p.D + d0) * p.H + h0) * p.W + w0;
-    char* wst = stg + (lane_o & 31) * 4 + nt * 2 + (lane_o >> 5) * 512;
-    float* rme = red + (mg * 64 + 2 * (lane_o & 31) + nt) * 3;  // [ch][mean, M2, n] of this wave's channel
-    const float bias0 = bls[2 * (lane_o & 31) + nt];
+    char* wst = stg + (lane_o & 31) * 2 + nt * 64 + (lane_o >> 5) * 512;
+    float* rme = red + (mg * 64 + 32 * nt + (lane_o & 31)) * 3;  // [ch][mean, M2, n] of this wave's channel
+    const float bias0 = bls[32 * nt + (lane_o & 31)];
     const bool relu = p.accumulate & PCMS_CONV_RELU;  // eval: BatchNorm folded (no stats then)
     const float rn = (float)nbdone * (32.f * MT);
     const float K0 = nbdone ? rme[0] : bias0;
@@ -1715,7 +1741,10 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
         const int mt = 2 * pass + (row >> 5), pr = perm32(row & 31);
         const int rd = 2 * mg + (mt >> 2), rh = 2 * (mt & 3) + (pr >> 4), rw = pr & 15;
         const long vox = vbase + (long)rd * plane + (long)rh * p.W + rw;
-        __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0, 0);
+        if constexpr ((BG_ABL & 2) == 0)
+          __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0, 0);
+        else
+          asm volatile("" ::"v"(v), "v"((int)vox));
       }
       // both waves are done reading the slice before the next pass rewrites it
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1888,6 +1917,7 @@ int pcms_conv3_pack(int dtype, const float* w, void* out, int Cout, int Cin, int
   const int CK = pcms_conv3_chunk(dtype);
   const int J = flip ? Cin : Cout;
   const int Kdim = flip ? Cout : Cin;
+  if (dtype == PCMS_BF16 && J % 32) return -1;  // fragment-major rows come in 32-row tiles
   dim3 grid(cdiv(J, 8), cdiv(Kdim, CK));
   if (dtype == PCMS_BF16 && Kdim % 32 == 0 && J % 8 == 0)
     hipLaunchKernelGGL(pack_conv3_bf16_kernel, grid, dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin, flip);

@@ -85,9 +85,19 @@ __device__ __forceinline__ s16x8_t lds_a(const char* lds, int row, int ks, int h
 __device__ __forceinline__ s16x8_t lds_slot(const char* lds, int row, int s) {
   return *reinterpret_cast<const s16x8_t*>(lds + row * kRowBytes + (s ^ swz(row)) * 16);
 }
-// B fragment (weights) straight from global: packed [chunk][27][Cout][WK] bf16.
+// B fragment (weights) straight from global: packed [chunk][27][Cout][WK] (fp32-data builds).
 __device__ __forceinline__ s16x8_t gl_b(const bf16_t* wrow, int ks, int h) {
   return *reinterpret_cast<const s16x8_t*>(wrow + ks * 16 + h * 8);
+}
+// bf16 weight pack, fragment-major (round 5): element (chunk c = k / 32, tap t, row j, k % 32)
+// of a J-row pack (J % 32 == 0) sits in the 1 KiB block (c, t, row tile j / 32, k-step
+// ks = (k / 16) % 2) at lane (j % 32) + 32 ((k / 8) % 2), element k % 8 -- exactly the
+// v_mfma_f32_32x32x16_bf16 B operand of that (32-row tile, k-step), so one B fragment is ONE
+// contiguous 1 KiB wave load (8 whole 128-B lines) instead of 16-32 lines touched in part,
+// and a row tile's two k-steps are adjacent (constant offsets from one address).
+__device__ __forceinline__ long pack_bf16_off(int c, int t, int j, int k, int J) {
+  return (((long)c * 27 + t) * (J >> 5) + (j >> 5)) * 1024 + (k >> 4 & 1) * 512 +
+         ((j & 31) + (k >> 3 & 1) * 32) * 8 + (k & 7);
 }
 
 struct Conv3Params {

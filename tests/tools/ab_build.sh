@@ -4,7 +4,7 @@ set -e
 cd "$(dirname "$0")/../../prostate-cancer-multimodal-segmentation_amd/csrc"
 SUF=$1; shift
 mkdir -p build_$SUF
-for f in conv3 stem convt ops; do
+for f in conv3 stem convt ops probe; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -Wno-unused-function "$@" -c $f.hip -o build_$SUF/$f.o &
 done
 wait

@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--big-min-boxes", type=int, default=0, help="pcms_conv3_big_min_boxes override")
     ap.add_argument("--fwd-box-vol", type=int, default=0, help="pcms_conv3_fwd_box_vol override (256)")
     ap.add_argument("--convt-taps", type=int, default=0, help="pcms_convt_wgrad_taps override (8 / 4 / 2)")
+    ap.add_argument("--clock", action="store_true",
+                    help="bracket every launch with bench.ClockProbe stamps: the shader clock per launch and the MFMA "
+                         "fraction at that clock (the stamps add a few us of launches between layers)")
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
     from pcms_amd import engine as E
@@ -102,30 +105,49 @@ def main():
     orig = E.call
     rec = []
 
+    probe = None
+    if a.clock:
+        import bench
+        probe = bench.ClockProbe()
+
     def timed(name, *args):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0 = probe.stamp() if probe else None
         s.record()
         r = orig(name, *args)
         e.record()
-        rec.append((name, args, s, e))
+        c1 = probe.stamp() if probe else None
+        rec.append((name, args, s, e, c0, c1))
         return r
     mods = [m for k, m in sys.modules.items() if k.startswith("pcms_amd") and getattr(m, "call", None) is orig]
     for m in mods:
         m.call = timed
+    def clk(c0, c1):
+        if c0 is None:
+            return None
+        import bench
+        v = list(bench.ClockProbe.mhz(c0, c1).values())
+        return statistics.median(v) if v else None
+
     per = []
     for _ in range(a.steps):
         rec.clear()
         tr.step(batch)
         torch.cuda.synchronize()
-        per.append([(n, ar, s.elapsed_time(e) * 1e3) for n, ar, s, e in rec])
+        per.append([(n, ar, s.elapsed_time(e) * 1e3, clk(c0, c1)) for n, ar, s, e, c0, c1 in rec])
     for m in mods:
         m.call = orig
     rows = []
-    for i, (n, ar, _) in enumerate(per[0]):
+    for i, (n, ar, _, _) in enumerate(per[0]):
         us = statistics.median(p[i][2] for p in per)
         f = flops(n, ar) * (xf if n.startswith("pcms_conv3") else 1)
-        rows.append({"i": i, "name": n, "desc": desc(n, ar), "us": round(us, 1), "gflop": round(f / 1e9, 2),
-                     "mfma_frac": round(f / (us * 1e-6) / PEAK, 3) if f else None})
+        row = {"i": i, "name": n, "desc": desc(n, ar), "us": round(us, 1), "gflop": round(f / 1e9, 2),
+               "mfma_frac": round(f / (us * 1e-6) / PEAK, 3) if f else None}
+        if probe:
+            mhz = statistics.median(p[i][3] for p in per if p[i][3] is not None)
+            row["mhz"] = round(mhz)
+            row["mfma_frac_at_clock"] = round(f / (us * 1e-6) / (PEAK * mhz / 2400.0), 3) if f else None
+        rows.append(row)
     tot = sum(r["us"] for r in rows)
     by = {}
     for r in rows:
@@ -134,7 +156,8 @@ def main():
     for k, v in sorted(by.items(), key=lambda kv: -kv[1]):
         print(f"  {k:28s} {v / 1e3:7.3f} ms")
     for r in sorted(rows, key=lambda r: -r["us"])[:60]:
-        print(f"{r['i']:4d} {r['name']:22s} {r['desc']:34s} {r['us']:8.1f} us  {r['gflop']:8.1f} GF  {r['mfma_frac']}")
+        print(f"{r['i']:4d} {r['name']:22s} {r['desc']:34s} {r['us']:8.1f} us  {r['gflop']:8.1f} GF  {r['mfma_frac']}"
+              + (f"  {r['mhz']} MHz  {r['mfma_frac_at_clock']}" if probe else ""))
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"batch": a.batch, "size": spatial, "rows": rows}, f, indent=1)
