@@ -106,6 +106,20 @@ int pcms_conv3_wgrad_tg_maxbox(int v);
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, int flags, hipStream_t s);
+/* The big-box convs on v_mfma_f32_16x16x32_bf16 (round 5): K = a pair of taps x 16 channels,
+ * 8 M-tiles x 4 N-tiles per wave; the same boxes, halo pipeline and outputs (y, BN partial
+ * rows: pcms_conv3_fwd_rows) as the 32x32x16 big-box path of pcms_conv3_fwd.  Weights in the
+ * pack16 layout: pcms_conv3_pack16 writes both directions of the convs of a table (int64 rows
+ * {fp32 weight ptr, Cout, Cin, fwd16 ptr or 0, dgrad16 ptr or 0, first tile, 0, 0}, one tile
+ * per 32 x 32 channels; fwd16 = rows Cout, k Cin; dgrad16 = rows Cin, k Cout, taps mirrored).
+ * pcms_conv3_fwd16 takes isc / ish (the input's BatchNorm + ReLU, as pcms_conv3_fwd_bnin) or
+ * NULL; flags 0 or PCMS_CONV_RELU; -5 where pcms_conv3_big16_ok is 0.                      */
+int pcms_conv3_big16_ok(int N, int D, int H, int W, int c0, int c1, int Cout);
+int pcms_conv3_pack16_elems(int J, int Kdim);
+int pcms_conv3_pack16(const long long* table, int ntab, int ntiles, hipStream_t s);
+int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float* isc, const float* ish,
+                     const void* wpack16, const float* bias, void* y0, void* y1, int cy0, float* stats, int flags,
+                     int N, int D, int H, int W, int Cout, hipStream_t s);
 /* Stem (inc.conv.0, bf16 build): input stored with 8 channels (n_modalities <= 8).
  * K packs two taps per MFMA k-step (14 x 16 = 224 instead of 27 x 32), or, with
  * PCMS_STEM_DENSE (cin_w <= 5), one (kd, kh) tap row of 3 kw x 5 channels per k-step (9 x 16);

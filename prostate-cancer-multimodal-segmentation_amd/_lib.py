@@ -35,6 +35,10 @@ SIGNATURES = {
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiiis",
     "pcms_conv3_wgrad_tg_maxbox": "i",
+    "pcms_conv3_big16_ok": "iiiiiii",
+    "pcms_conv3_pack16_elems": "ii",
+    "pcms_conv3_pack16": "piis",
+    "pcms_conv3_fwd16": "pipippppppipiiiiiis",
     "pcms_stem_pack_elems": "",
     "pcms_stem_wgrad_dense": "i",
     "pcms_stem_pack": "ppis",

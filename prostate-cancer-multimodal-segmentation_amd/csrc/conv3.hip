@@ -1490,7 +1490,6 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r_lane = lane & 31, hsel = lane >> 5;
   // wave = (M-group mg: box voxel rows 256 mg ..; N-tile nt: output channels 32 nt .. 32 nt + 31)
   const int mg = wave & 3, nt = wave >> 2;
   const int Cout = p.Cout, ncob = Cout >> 6;
@@ -1500,6 +1499,9 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
   const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const int cob = lg % ncob, slot = lg / ncob, nslot = G / ncob;
   const int nbox = p.N * p.nbd * p.nbh * p.nbw;
+  // box walk: slot, slot + nslot, ... (a d-column walk and sc1 / nt output stores measured
+  // no different, profiles/r5_big_walk_storepolicy_ab.txt)
+  const int box_step = nslot, box_end = nbox, box0 = slot;
   const int co_base = cob * 64;
   auto origin = [&](int box, int& n, int& d0, int& h0, int& w0) {
     int q = box;
@@ -1607,7 +1609,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 
   f32x16_t acc[MT];
   s16x8_t bset[kBgDist + 1];
-  int box = slot;
+  int box = box0;
   int n, d0, h0, w0;
   origin(box, n, d0, h0, w0);
   // Short boxes (4 chunks): every CU would reach its box boundary -- the vmcnt(0), the 128 KiB
@@ -1631,8 +1633,8 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-    const int nbx = box + nslot;
-    const bool has_next = nbx < nbox;
+    const int nbx = box + box_step;
+    const bool has_next = nbx < box_end;
     int nn = n, nd0 = d0, nh0 = h0, nw0 = w0;
     if (has_next) origin(nbx, nn, nd0, nh0, nw0);
     // one chunk: 27 taps.  Chunk 0 (peeled, Slack): B(t < Dist) were issued before the
@@ -1793,6 +1795,399 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
     st[0] = S;
     st[1] = M2;
     if (tid == 0 && cob == 0) p.stats[(long)nslot * Cout * 2 + slot] = Nn;
+  }
+}
+
+
+// ------------------------------------------------------------------------------------
+// Big-box forward / dgrad on v_mfma_f32_16x16x32_bf16 (round 5; pcms_conv3_fwd16).  The same
+// persistent 8-wave workgroup, 8 x 8 x 16 boxes, 16-channel chunks and LDS-DMA halo pipeline
+// as conv3_fwd_big_kernel, with the MFMA shape changed: K = 32 = a PAIR of taps x 16 channels
+// (lanes 0-31 of a fragment hold tap 2 s, lanes 32-63 tap 2 s + 1; 14 k-steps per chunk, the
+// 28th tap a zero weight), wave w = box d-plane w: 8 M-tiles (its 8 h-rows of 16 voxels) x 4
+// N-tiles (all 64 output channels), so per k-step 8 A reads + 4 B loads feed 32 MFMAs -- half
+// the A bytes per FLOP of the 32x32x16 kernel.  Why: the big-box convs run power-capped
+// (1.4-1.9 GHz in step, profiles/r5_layer_times_clock.json), and this inner loop does the same
+// FLOPs for ~11 % less time on every CU at once (tests/kexp/mfma_shape.hip:
+// profiles/r5_mfma_shape_probe.txt: 1505-1529 vs 1358-1370 TFLOP/s, at 2.00-2.06 vs 1.90-1.94
+// GHz).  Halo rows stay 32 B (16 channels) without a swizzle: a 16-lane ds_read_b128 group reads
+// rows {0-3, 12-15} of one half and {4-11} of the other, all 64 banks once.  B fragments come
+// from the pack16 layout (pack16_off: one contiguous 1 KiB per (chunk, tap pair, 16-channel
+// tile)).  Epilogue: each wave stages one M-tile at a time (16 voxels x 64 channels, 144-B rows)
+// in its own LDS slice -- no cross-wave barrier -- and writes whole 128-B channel rows.
+// ------------------------------------------------------------------------------------
+constexpr int kB6Steps = 14;                       // tap pairs per chunk
+constexpr int kB6Dist = 1;                         // B prefetch distance (k-steps)
+static_assert(kB6Steps % (kB6Dist + 1) == 0, "B ring index must continue across chunks");
+constexpr int kB6Row = 144;                        // epilogue slice row (64 ch bf16 + pad: conflict-free writes)
+constexpr int kB6Slice = 16 * kB6Row;
+constexpr int kB6Red = 8 * 64 * 3 * 4;
+constexpr int kB6SliceOff = 2 * kBgBuf + kBgDummy;
+constexpr int kB6RedOff = kB6SliceOff + 8 * kB6Slice;
+constexpr int kB6Lds = kB6RedOff + kB6Red + 64 * 4;  // + bias
+constexpr int kB6BnOff = kB6Lds;
+constexpr int kB6LdsBn = kB6Lds + 2 * kBgBnMax * 4;
+static_assert(kB6LdsBn <= 160 * 1024, "LDS");
+constexpr int kB6EpiStores = 16;                   // 16-B stores per wave and box
+
+__device__ __forceinline__ f32x4_t mfma16(s16x8_t a, s16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+// halo row offset of tap t (10 x 18 rows per plane); the zero-weight 28th tap reads tap 26's rows
+__host__ __device__ constexpr int b6_tapoff(int t) {
+  return t > 26 ? b6_tapoff(26) : ((t / 9) * kBgHH + (t / 3) % 3) * kBgHW + t % 3;
+}
+// retire the hidden loads of the four B fragments of a step (and everything issued before)
+template <int N> __device__ __forceinline__ void vm_wait4(s16x8_t (&b)[4]) {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : "n"(N) : "memory");
+}
+template <int P> constexpr int b6_piece(int s) { return ((s % kB6Steps) + kB6Steps) % kB6Steps < P ? 1 : 0; }
+// vector-memory ops issued after the last of B(t)'s 4 loads by the time step t waits for it:
+// every step u issues B(u + D) (4 loads) then piece(u) (u < P)
+template <int P, int Dist> constexpr int b6_wait(int t) {
+  int n = b6_piece<P>(t - Dist);
+  for (int u = t - Dist + 1; u <= t; ++u) n += 4 + b6_piece<P>(u);
+  return n;
+}
+
+template <bool BNIN = false>
+__global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Params p, uint32_t x0bytes,
+                                                                     uint32_t x1bytes) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Cout = p.Cout, ncob = Cout >> 6;
+  const int G = gridDim.x;
+  const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int cob = lg % ncob, slot = lg / ncob, nslot = G / ncob;
+  const int nbox = p.N * p.nbd * p.nbh * p.nbw;
+  const int co_base = cob * 64;
+  auto origin = [&](int box, int& n, int& d0, int& h0, int& w0) {
+    int q = box;
+    const int bwi = q % p.nbw; q /= p.nbw;
+    const int bhi = q % p.nbh; q /= p.nbh;
+    const int bdi = q % p.nbd;
+    n = q / p.nbd;
+    d0 = bdi * kBgBD; h0 = bhi * 8; w0 = bwi * 16;
+  };
+  const i32x4_t xr0 = buffer_desc(p.x0, x0bytes);
+  const i32x4_t xr1 = buffer_desc(p.x1 ? p.x1 : p.x0, x1bytes);
+  const uint32_t lds0 = lds_addr(lds);
+  // halo piece j of this thread: row pc / 2 (32 B), 16-B half pc & 1 (channels 8 half ..),
+  // no swizzle; live = false: still issued (the vmcnt arithmetic), reads out of range = zeros
+  auto stage_piece = [&](int n, int d0, int h0, int w0, int chunk, int buf, int j, bool live) {
+    const int c = chunk * 16;
+    const bool first = c < p.c0;
+    const uint32_t stride = first ? p.c0 : p.c1;
+    const uint32_t cofs = first ? c : c - p.c0;
+    const int pc = opaque(tid) + j * kBgThreads;
+    const int hv = pc >> 1;
+    const int hw_ = hv % kBgHW, t_ = hv / kBgHW, hh_ = t_ % kBgHH, hd_ = t_ / kBgHH;
+    const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+    uint32_t voff = kOOB;
+    if (live && hv < kBgHalo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
+        (unsigned)gw < (unsigned)p.W)
+      voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs + (uint32_t)(pc & 1) * 8u) * 2u;
+    const bool dummy = j == kBgPieces - 1 && wave > 0;
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(
+        dummy ? lds0 + 2 * kBgBuf : lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
+    dma16(first ? xr0 : xr1, lb, dummy ? kOOB : voff, 0);
+    return (!dummy && voff != kOOB ? 1u << j : 0u) | ((uint32_t)(pc & 1) << (8 + j));
+  };
+  float* bnt = reinterpret_cast<float*>(lds + kB6BnOff);
+  auto bn_apply = [&](int buf, int chunk, uint32_t pm) {
+#pragma unroll
+    for (int j = 0; j < kBgPieces; ++j) {
+      if (!((pm >> j) & 1)) continue;
+      const int pc = tid + j * kBgThreads;
+      u32x4_t* q = reinterpret_cast<u32x4_t*>(lds + buf * kBgBuf + pc * 16);
+      const int c = chunk * 16 + ((pm >> (8 + j)) & 1) * 8;
+      const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(bnt + c), s1 = *reinterpret_cast<const f32x4_t*>(bnt + c + 4);
+      const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(bnt + kBgBnMax + c);
+      const f32x4_t h1 = *reinterpret_cast<const f32x4_t*>(bnt + kBgBnMax + c + 4);
+      const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      u32x4_t v = *q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        v[i] = pack_bf16x2(bn_relu1(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]),
+                           bn_relu1(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]));
+      *q = v;
+    }
+  };
+  if constexpr (BNIN) {
+    if (tid < p.Cin) { bnt[tid] = p.isc[tid]; bnt[kBgBnMax + tid] = p.ish[tid]; }
+    __syncthreads();
+  }
+
+  // B: pack16, (16-chunk c, step s) rows of Cout / 16 fragments of 1 KiB; this wave's four
+  // N-tiles are the workgroup's 64 channels: one base + immediates 0 / 1 / 2 / 3 KiB
+  const int nchunk = p.Cin >> 4;
+  const uint32_t step_bytes = (uint32_t)Cout * 64u;
+  const i32x4_t wr = buffer_desc(p.w, (uint32_t)nchunk * kB6Steps * step_bytes);
+  auto load_b = [&](s16x8_t (&dst)[4], int chunk, int st, uint32_t boff) {
+    const uint32_t off = boff + (uint32_t)(chunk * kB6Steps + st) * step_bytes;
+    bload16<0>(dst[0], wr, off);
+    bload16<1024>(dst[1], wr, off);
+    bload16<2048>(dst[2], wr, off);
+    bload16<3072>(dst[3], wr, off);
+  };
+
+  float* red = reinterpret_cast<float*>(lds + kB6RedOff);  // [wave][64][mean, M2, n]
+  float* bls = red + 8 * 64 * 3;
+  if (tid < 64) bls[tid] = p.bias ? p.bias[co_base + tid] : 0.f;
+  const bool to0 = co_base < p.cy0;
+  const long ys = to0 ? p.cy0 : Cout - p.cy0;
+  const int yc0 = to0 ? co_base : co_base - p.cy0;
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+      to0 ? p.y0 : p.y1, (short)0, (int)(p.nvox * ys * 2), 0x00020000);
+  char* slice = lds + kB6SliceOff + wave * kB6Slice;
+  int nbdone = 0;
+
+  f32x4_t acc[8][4];
+  s16x8_t bset[kB6Dist + 1][4];
+  int box = slot;
+  int n, d0, h0, w0;
+  origin(box, n, d0, h0, w0);
+  if (nchunk <= 4)
+    for (int i = 0; i < 2 * (slot & 3); ++i) __builtin_amdgcn_s_sleep(127);
+  uint32_t pmask = 0;
+#pragma unroll
+  for (int j = 0; j < kBgPieces; ++j) pmask |= stage_piece(n, d0, h0, w0, 0, 0, j, true);
+  {
+    const uint32_t boff0 = (uint32_t)(cob * 4096 + lane * 16);
+#pragma unroll
+    for (int t = 0; t < kB6Dist; ++t) load_b(bset[t], 0, t, boff0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (BNIN) bn_apply(0, 0, pmask);
+  __syncthreads();
+  int buf = 0;
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int nbx = box + nslot;
+    const bool has_next = nbx < nbox;
+    int nn = n, nd0 = d0, nh0 = h0, nw0 = w0;
+    if (has_next) origin(nbx, nn, nd0, nh0, nw0);
+    auto run_chunk = [&](int chunk, auto slack_tag) {
+      constexpr bool Slack = decltype(slack_tag)::value;
+      const bool last = chunk + 1 == nchunk;
+      const bool live = !last || has_next;
+      const int sn = last ? nn : n, sd = last ? nd0 : d0, sh = last ? nh0 : h0, sw = last ? nw0 : w0;
+      const int schunk = last ? 0 : chunk + 1;
+      const int lo = opaque(lane);
+      const uint32_t boff = (uint32_t)(cob * 4096 + lo * 16);
+      // A: this lane's halo row base -- box voxel (d = wave, h = 0, w = r16), its channel half
+      // (g4 & 1) -- plus the row offset of its tap of the pair (g4 >> 1); M-tile mt = h-row mt
+      // is an immediate (mt x 18 rows)
+      const uint32_t abase = lds0 + buf * kBgBuf +
+                             (uint32_t)(((wave * kBgHH) * kBgHW + (lo & 15)) * 32 + ((lo >> 4) & 1) * 16);
+      const bool hi_tap = (lo >> 5) & 1;
+      // A fragment of (step st, M-tile mt); fragments are read two M-tiles ahead of their four
+      // MFMAs through a 3-register rotation, across step boundaries (a deeper, per-step rolling
+      // set made the compiler double-buffer it into spills)
+      auto rd = [&](int st, int mt) {
+        const uint32_t ad = abase + (uint32_t)(hi_tap ? b6_tapoff(2 * st + 1) : b6_tapoff(2 * st)) * 32u;
+        return *reinterpret_cast<const LDS_AS s16x8_t*>((const LDS_AS char*)(uintptr_t)ad + mt * kBgHW * 32);
+      };
+      s16x8_t ar[3];
+      ar[0] = rd(0, 0);
+      ar[1] = rd(0, 1);
+      static_for<kB6Steps>([&](auto sc) {
+        constexpr int st = decltype(sc)::value;
+        constexpr int sn_ = st + kB6Dist;
+        if constexpr (sn_ < kB6Steps) load_b(bset[sn_ % (kB6Dist + 1)], chunk, sn_, boff);
+        else load_b(bset[sn_ % (kB6Dist + 1)], schunk, sn_ - kB6Steps, boff);
+        if constexpr (st < kBgPieces) {
+          const uint32_t bits = stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, st, live);
+          if constexpr (BNIN) pmask = (st == 0 ? 0u : pmask) | bits;
+        }
+        s16x8_t (&b)[4] = bset[st % (kB6Dist + 1)];
+        constexpr int extra = (Slack && st < kB6Dist) ? kB6EpiStores : 0;
+        vm_wait4<b6_wait<kBgPieces, kB6Dist>(st) + extra>(b);
+        static_for<8>([&](auto mc) {
+          constexpr int mt = decltype(mc)::value;
+          constexpr int q = st * 8 + mt + 2;  // the fragment read now: position q (two ahead)
+          if constexpr (q < kB6Steps * 8) ar[q % 3] = rd(q / 8, q % 8);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[mt][j] = mfma16(ar[(st * 8 + mt) % 3], b[j], acc[mt][j]);
+        });
+        // keep the order (1 read, 4 MFMAs per M-tile) and every step's work in its step
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          if (st * 8 + mt + 2 < kB6Steps * 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      if (!last) vm_wait<4 * (kB6Steps - kBgPieces)>();
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (BNIN) bn_apply(buf ^ 1, schunk, pmask);
+      __syncthreads();
+      buf ^= 1;
+    };
+    run_chunk(0, std::true_type{});
+    for (int chunk = 1; chunk < nchunk; ++chunk) run_chunk(chunk, std::false_type{});
+
+    // ---- epilogue of this box: lane (g4, r16) holds, per (M-tile mt, N-tile j), voxels w =
+    // 4 g4 + i (i < 4) of h-row mt, channel 16 j + r16.  One M-tile at a time through the wave's
+    // own slice (16 rows of 144 B): + bias, bf16; read back as whole 128-B rows (2 x 16 B per
+    // lane), 16-B stores.  BatchNorm moments shifted by K (the running mean; the bias before
+    // the first box), per channel over the wave's 128 voxels, Chan-merged per (wave, channel).
+    const int lane_o = opaque(lane);
+    const int rr = lane_o & 15, gg = lane_o >> 4;
+    const long plane = (long)p.H * p.W;
+    const long vbase = (((long)n * p.D + d0 + wave) * p.H + h0) * p.W + w0;
+    const bool relu = p.accumulate & PCMS_CONV_RELU;
+    float bias_j[4], K0[4], c0s[4], S1[4], S2[4];
+    const float rn = (float)nbdone * 128.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bias_j[j] = bls[16 * j + rr];
+      K0[j] = nbdone ? red[(wave * 64 + 16 * j + rr) * 3] : bias_j[j];
+      c0s[j] = bias_j[j] - K0[j];
+      S1[j] = 0.f;
+      S2[j] = 0.f;
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v0 = acc[mt][j][i];
+          *reinterpret_cast<bf16_t*>(slice + (4 * gg + i) * kB6Row + (16 * j + rr) * 2) =
+              f2bf(relu ? fmaxf(v0 + bias_j[j], 0.f) : v0 + bias_j[j]);
+          const float e0 = v0 + c0s[j];
+          S1[j] += e0;
+          S2[j] = fmaf(e0, e0, S2[j]);
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int q = lane_o + 64 * k, vw = q >> 3, c16 = q & 7;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(slice + vw * kB6Row + c16 * 16);
+        const long vox = vbase + (long)mt * p.W + vw;
+        if constexpr ((BG_ABL & 2) == 0)
+          __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0, 0);
+        else
+          asm volatile("" ::"v"(v), "v"((int)vox));
+      }
+      (void)plane;
+    }
+    {
+      constexpr float nb = 128.f;  // voxels per wave and box
+      const float nnew = rn + nb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s1 = S1[j], s2 = S2[j];
+        s1 += __shfl_xor(s1, 16, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        const float mbox = K0[j] + s1 / nb;
+        const float m2b = fmaxf(s2 - s1 * s1 / nb, 0.f);
+        float* rme = red + (wave * 64 + 16 * j + rr) * 3;
+        const float rmean = nbdone ? rme[0] : 0.f, rm2 = nbdone ? rme[1] : 0.f;
+        const float delta = mbox - rmean;
+        if (gg == 0) {
+          rme[0] = rmean + delta * (nb / nnew);
+          rme[1] = rm2 + m2b + delta * delta * (rn * nb / nnew);
+          rme[2] = nnew;
+        }
+      }
+      ++nbdone;
+    }
+    if (!has_next) break;
+    box = nbx;
+    n = nn; d0 = nd0; h0 = nh0; w0 = nw0;
+  }
+
+  if (!p.stats) return;
+  __syncthreads();
+  if (tid < 64) {
+    float S = 0.f, Nn = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      S += red[(w * 64 + tid) * 3] * red[(w * 64 + tid) * 3 + 2];
+      Nn += red[(w * 64 + tid) * 3 + 2];
+    }
+    const float m = S / Nn;
+    float M2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const float c = red[(w * 64 + tid) * 3 + 2];
+      const float d = red[(w * 64 + tid) * 3] - m;
+      M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+    }
+    float* st = p.stats + ((long)slot * Cout + co_base + tid) * 2;
+    st[0] = S;
+    st[1] = M2;
+    if (tid == 0 && cob == 0) p.stats[(long)nslot * Cout * 2 + slot] = Nn;
+  }
+}
+
+// pack16 layout (conv3_fwd_b16_kernel's B operand): element (16-chunk c, tap pair s, row j,
+// lane group g, element e) = w[j][16 c + 8 (g & 1) + e][tap 2 s + (g >> 1)] (tap 27: zero), in
+// 1 KiB blocks (c, s, j / 16) of lanes l = 16 g + j % 16 -- the v_mfma_f32_16x16x32_bf16 B
+// fragment of that (tap pair, 16-row tile).  J % 16 == 0, Kdim % 16 == 0.
+__host__ __device__ inline long pack16_off(int c, int s, int j, int g, int J) {
+  return (((long)c * kB6Steps + s) * (J >> 4) + (j >> 4)) * 512 + (g * 16 + (j & 15)) * 8;
+}
+// Both pack16 forms of the convs of a table, from the fp32 master (one block per 32 co x 32 ci
+// tile, as pack_conv3_bf16_both_kernel): rows int64[8] = {weight ptr, Cout, Cin, fwd16 ptr (or
+// 0), dgrad16 ptr (or 0), first tile, 0, 0}.  fwd16: J = Cout rows, k = Cin; dgrad16: J = Cin
+// rows, k = Cout, taps mirrored (the dgrad conv is the transposed, flipped forward).
+__global__ void __launch_bounds__(256) pack16_conv3_kernel(const long long* tab, int ntab) {
+  __shared__ __attribute__((aligned(16))) uint16_t tb[32 * 864];
+  int ei = 0;
+  while (ei + 1 < ntab && tab[8 * (ei + 1) + 5] <= (long long)blockIdx.x) ++ei;
+  const long long* e = tab + 8 * ei;
+  const float* w = reinterpret_cast<const float*>(e[0]);
+  const int Cout = (int)e[1], Cin = (int)e[2];
+  bf16_t* fwd = reinterpret_cast<bf16_t*>(e[3]);
+  bf16_t* dgr = reinterpret_cast<bf16_t*>(e[4]);
+  const int local = blockIdx.x - (int)e[5];
+  const int j0 = (local % (Cout / 32)) * 32, ci0 = (local / (Cout / 32)) * 32;
+  for (int i = threadIdx.x; i < 32 * 216; i += 256) {
+    const int run = i / 216, q = i % 216;
+    const f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(w + ((long)(j0 + run) * Cin + ci0) * 27) + q);
+    uint2 o;
+    o.x = pack_bf16x2(v[0], v[1]);
+    o.y = pack_bf16x2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(tb + run * 864 + 4 * q) = o;
+  }
+  __syncthreads();
+  // 2 chunks x 14 steps x 2 row tiles x 64 lanes = 3584 16-B pieces per direction
+  for (int it = threadIdx.x; it < 2 * 3584; it += 256) {
+    const int dir = it / 3584, q = it % 3584;
+    bf16_t* out = dir ? dgr : fwd;
+    if (!out) continue;
+    const int l = q & 63, rt = (q >> 6) & 1, st = (q >> 7) % kB6Steps, cc = (q >> 7) / kB6Steps;
+    const int g = l >> 4, jl = rt * 16 + (l & 15);             // row within the 32-row tile
+    const int tap = 2 * st + (g >> 1);
+    uint32_t o[4];
+#pragma unroll
+    for (int ee = 0; ee < 4; ++ee) {
+      uint32_t v2 = 0;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int kl = cc * 16 + 8 * (g & 1) + 2 * ee + hh;  // k within the 32-wide tile
+        uint16_t v = 0;
+        if (tap < 27) v = dir ? tb[kl * 864 + jl * 27 + (26 - tap)] : tb[jl * 864 + kl * 27 + tap];
+        v2 |= (uint32_t)v << (16 * hh);
+      }
+      o[ee] = v2;
+    }
+    const int J = dir ? Cin : Cout;
+    const int jg = (dir ? ci0 : j0) + jl;                      // global row
+    const int cg = ((dir ? j0 : ci0) >> 4) + cc;               // global 16-chunk
+    *reinterpret_cast<u32x4_t*>(out + pack16_off(cg, st, jg, g, J)) = (u32x4_t){o[0], o[1], o[2], o[3]};
   }
 }
 
@@ -1963,6 +2358,52 @@ int pcms_conv3_fwd_bnin(int dtype, const void* x, int cin, const float* isc, con
   if (!isc || !ish || cin > kBgBnMax || dtype != PCMS_BF16) return -1;
   return conv3_fwd_any(dtype, x, cin, nullptr, 0, isc, ish, wpack, bias, y, nullptr, Cout, nullptr, stats, 0, N, D,
                        H, W, Cout, 1, s);
+}
+
+// ---- 16x16x32 big-box path (conv3_fwd_b16_kernel) ----
+// 1 when pcms_conv3_fwd16 runs this conv (bf16, the big-box shapes, one split); the engine
+// keeps a pack16 for such convs
+int pcms_conv3_big16_ok(int N, int D, int H, int W, int c0, int c1, int Cout) {
+  return Cout % 64 == 0 && big_fwd_ok(PCMS_BF16, N, D, H, W, c0, c1) && (long)N * D * H * W * Cout * 2 < (long)kOOB;
+}
+int pcms_conv3_pack16_elems(int J, int Kdim) { return (J % 16 || Kdim % 16) ? -1 : (Kdim / 16) * kB6Steps * J * 32; }
+// pack16 forms (fwd16: rows = Cout, k = Cin; dgrad16: rows = Cin, k = Cout, taps mirrored) of the
+// convs of a table: int64 rows {weight ptr, Cout, Cin, fwd16 ptr or 0, dgrad16 ptr or 0, first
+// tile, 0, 0}, one tile per 32 co x 32 ci (ntiles = sum of Cout / 32 x Cin / 32)
+int pcms_conv3_pack16(const long long* table, int ntab, int ntiles, hipStream_t s) {
+  if (ntab <= 0 || ntiles <= 0) return 0;
+  hipLaunchKernelGGL(pack16_conv3_kernel, dim3(ntiles), dim3(256), 0, s, table, ntab);
+  PCMS_CHECK_LAUNCH();
+}
+// y = conv(x) + bias on the 16x16x32 big-box kernel (wpack16 = a pcms_conv3_pack16 form);
+// arguments as pcms_conv3_fwd with splits = 1; isc / ish != NULL: the input's BatchNorm + ReLU
+// applied in the staging (as pcms_conv3_fwd_bnin; one source of <= 128 channels).  -5 when
+// pcms_conv3_big16_ok is 0.
+int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float* isc, const float* ish,
+                     const void* wpack16, const float* bias, void* y0, void* y1, int cy0, float* stats, int flags,
+                     int N, int D, int H, int W, int Cout, hipStream_t s) {
+  if (!pcms_conv3_big16_ok(N, D, H, W, c0, c1, Cout) || (c1 > 0 && x1 == nullptr)) return -5;
+  if (isc && (c1 != 0 || c0 > kBgBnMax || !ish)) return -1;
+  if (stats && flags) return -6;
+  if (flags & ~PCMS_CONV_RELU) return -8;
+  if (y1 == nullptr) cy0 = Cout;
+  if (cy0 % 64 != 0 && cy0 != Cout) return -2;
+  Conv3Params p;
+  p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1;
+  p.isc = isc; p.ish = ish;
+  p.w = wpack16; p.bias = bias; p.y0 = y0; p.y1 = y1; p.cy0 = cy0;
+  p.yacc = nullptr; p.stats = stats; p.accumulate = flags;
+  p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = c0 + c1; p.Cout = Cout;
+  p.nvox = (long)N * D * H * W;
+  p.nchunk = p.Cin / 16; p.chunks_per_split = p.nchunk;
+  p.nbd = D / kBgBD; p.nbh = H / 8; p.nbw = W / 16;
+  const int nslot = big_slots(N, D, H, W, Cout);
+  auto kern = isc ? conv3_fwd_b16_kernel<true> : conv3_fwd_b16_kernel<false>;
+  const int ldsb = isc ? kB6LdsBn : kB6Lds;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldsb);
+  hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64)), dim3(kBgThreads), ldsb, s, p,
+                     (uint32_t)(p.nvox * c0 * 2), (uint32_t)(p.nvox * c1 * 2));
+  PCMS_CHECK_LAUNCH();
 }
 
 }  // extern "C"

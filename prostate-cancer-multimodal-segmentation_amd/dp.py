@@ -13,10 +13,16 @@ The reference has no multi-GPU code.  The semantics chosen are those
 * the flat fp32 gradient is summed over ranks; the 1/world mean is folded into Adam.
 
 The gradient all-reduce is bucketed and overlapped with the backward: the engine reports
-each module's gradient range as soon as its backward has written it (decoder first, the
-stem last) and a bucket is launched asynchronously (``async_op=True``: the RCCL kernel is
-ordered after the producing kernels of the compute stream, then runs beside the rest of
-the backward).  ``finish()`` makes the compute stream wait for every bucket before Adam,
+each LAYER's gradient range (a conv's weight + bias, a BatchNorm's gamma + beta, the
+ConvTranspose, the head) as soon as the kernel that writes it is enqueued -- descending flat
+order, the head first and the stem last (``readiness_groups``) -- and a bucket is launched
+asynchronously (``async_op=True``: the RCCL kernel is ordered after the producing kernels of
+the compute stream, then runs beside the rest of the backward).  A bucket goes out once it
+holds ``bucket_elems`` elements, or once it holds ``min_bucket_elems`` and at most as many
+elements remain to come as it holds: near the end of the backward the buckets shrink with
+the remaining gradient, so the one bucket nothing overlaps (what ``finish`` launches) is the
+last layers' (the stem and down1: ~0.3 M elements at the UNet3D sizes, not the ~14 M of the
+four encoder modules it was with per-module readiness).  ``finish()`` makes the compute stream wait for every bucket before Adam,
 which applies the 1/world mean in its single pass over the gradient and writes the mean
 back, so ``param.grad`` holds the DDP mean after ``optimizer.step()``.
 Buckets are contiguous slices of the flat gradient, so every collective is one large
@@ -31,6 +37,45 @@ import torch.distributed as dist
 
 # top-level modules in the order the engine's backward finishes their gradients
 BACKWARD_ORDER = ("outc", "up4", "up3", "up2", "up1", "down4", "down3", "down2", "down1", "inc")
+
+
+def readiness_groups(named) -> List[Tuple[str, int, int]]:
+    """The (layer, lo, hi) flat ranges in the order the engine's backward reports them: one
+    group per layer (parameters sharing a module prefix, e.g. ``down2.maxpool_conv.1.conv.3``
+    = that conv's weight and bias), in descending flat order -- outc, up4's second BatchNorm,
+    its second conv, ..., up4's ConvTranspose, up3 ..., down4 ..., inc's first conv.  ``named``:
+    (name, tensor) pairs in parameter order (``model.named_parameters()``)."""
+    groups: List[List] = []
+    off = 0
+    for name, p in named:
+        layer = name.rsplit(".", 1)[0]
+        if groups and groups[-1][0] == layer:
+            groups[-1][2] = off + p.numel()
+        else:
+            groups.append([layer, off, off + p.numel()])
+        off += p.numel()
+    return [(g[0], g[1], g[2]) for g in reversed(groups)]
+
+
+def plan_buckets(ranges, total: int, bucket_elems: int, min_bucket_elems: int) -> List[Tuple[int, int]]:
+    """The buckets GradSync launches for ready ranges reported in this order (descending,
+    tiling [0, total)), ending with the remainder finish() launches: the launch rule in one
+    place for the tests."""
+    out, lo, hi = [], None, None
+    for a, b in ranges:
+        if hi is None:
+            hi = b
+        lo = a
+        if _due(hi - lo, lo, bucket_elems, min_bucket_elems):
+            out.append((lo, hi))
+            lo = hi = None
+    if hi is not None and hi > lo:
+        out.append((lo, hi))
+    return out
+
+
+def _due(pending: int, remaining: int, bucket_elems: int, min_bucket_elems: int) -> bool:
+    return pending >= bucket_elems or (pending >= min_bucket_elems and remaining <= pending)
 
 
 def module_grad_ranges(model) -> Dict[str, Tuple[int, int]]:
@@ -56,15 +101,18 @@ class GradSync:
     ``ready(lo, hi)`` declares flat_g[lo:hi] final.  Ranges arrive in descending order
     and tile the buffer (hi == the previous range's lo), as the U-Net backward produces
     them (outc and up4 sit at the end of the buffer, inc at offset 0).  Pending ranges are
-    launched once they reach ``bucket_elems`` (default 16 Mi elements = 64 MB fp32);
-    ``finish()`` launches the rest, waits, and returns the 1/world scale Adam applies.
+    launched once they reach ``bucket_elems`` (default 16 Mi elements = 64 MB fp32), or
+    ``min_bucket_elems`` (default 1 Mi) when no more than that many elements remain below
+    them; ``finish()`` launches the rest, waits, and returns the 1/world scale Adam applies.
     """
 
-    def __init__(self, flat_g: torch.Tensor, group=None, bucket_elems: int = 16 << 20, overlap: bool = True):
+    def __init__(self, flat_g: torch.Tensor, group=None, bucket_elems: int = 16 << 20, overlap: bool = True,
+                 min_bucket_elems: int = 1 << 20):
         self.flat_g = flat_g
         self.group = group
         self.world = dist.get_world_size(group)
         self.bucket_elems = int(bucket_elems)
+        self.min_bucket_elems = int(min(min_bucket_elems, bucket_elems))
         self.overlap = overlap
         self._works: List = []
         self._lo: Optional[int] = None   # pending range [lo, hi)
@@ -102,7 +150,7 @@ class GradSync:
         if self._hi is None:
             self._hi = hi
         self._lo = lo
-        if self.overlap and self._hi - self._lo >= self.bucket_elems:
+        if self.overlap and _due(self._hi - self._lo, self._lo, self.bucket_elems, self.min_bucket_elems):
             self._launch()
 
     def _launch(self):

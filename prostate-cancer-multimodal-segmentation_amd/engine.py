@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -34,12 +35,16 @@ _DT = {"bf16": (torch.bfloat16, BF16), "fp32": (torch.float32, F32)}
 
 
 class ConvSpec:
-    __slots__ = ("mod", "cin", "cout", "cin_store", "fwd", "dgrad", "code")
+    __slots__ = ("mod", "cin", "cout", "cin_store", "fwd", "dgrad", "code", "fwd16", "dgrad16")
 
     def __init__(self, mod, cin, cout, cin_store):
         self.mod, self.cin, self.cout, self.cin_store = mod, cin, cout, cin_store
         self.fwd = None
         self.dgrad = None
+        # pcms_conv3_pack16 forms for the 16x16x32 big-box kernel (pcms_conv3_fwd16), set by
+        # UNetEngine._alloc for the convs whose forward / dgrad run on it at the allocated shape
+        self.fwd16 = None
+        self.dgrad16 = None
         # conv-kernel dtype code: BF16, or for fp32 data F32 (bf16x6 arithmetic, fp32-grade)
         # / F32X3 (bf16x3, faster, ~10x the fp32 rounding error)
         self.code = None
@@ -115,6 +120,11 @@ class UNetEngine:
         # pair (same arithmetic and rounding).  False: the a1 pass (A/B)
         self.fuse_bnin = True
         self._bnin_cache = {}
+        # the level-0/1 convs (forward and dgrad) on the 16x16x32 big-box kernel
+        # (pcms_conv3_fwd16, pack16 weights rebuilt with the other packs); PCMS_B16=0 keeps the
+        # 32x32x16 big-box kernel (A/B)
+        self.use_b16 = os.environ.get("PCMS_B16", "1") != "0"
+        self._p16 = None  # pcms_conv3_pack16 table for the allocated shape
         # the blocks whose training forward ran fused (id(BlockSpec)): the backward and the
         # checkpointed recompute follow the forward's decision, not the current settings
         self._fwd_bnin = set()
@@ -215,7 +225,14 @@ class UNetEngine:
         self._wgen = getattr(self, "_wgen", 0) + 1
         self._adam_plan = None
         self._store_ranges = None  # offsets into the new flat buffer
+        self._p16 = None           # weight pointers of the pack16 table
         self.grad_ranges = module_grad_ranges(self.model)
+        # [lo, hi) of every parameter in the flat gradient (per-layer readiness for dp.GradSync)
+        self.param_span = {}
+        off = 0
+        for p in params:
+            self.param_span[id(p)] = (off, off + p.numel())
+            off += p.numel()
 
     @contextlib.contextmanager
     def _timed(self, name: str):
@@ -231,13 +248,17 @@ class UNetEngine:
         e1.record()
         t.setdefault(name, []).append((e0, e1))
 
-    def _grads_done(self, module: str):
-        """A module's backward is complete: join the weight-gradient stream (its dW kernels and
-        the gradient buffers they read are then safe for the all-reduce and for reuse), and
-        report the module's flat range to the data-parallel hook (dp.GradSync)."""
+    def _grads_done(self, *params):
+        """The gradients of ``params`` (adjacent in the flat buffer) are final: join the
+        weight-gradient stream (its dW kernels are then ordered before any consumer), and report
+        their flat range to the data-parallel hook (dp.GradSync) -- per layer, as each
+        weight-gradient / BatchNorm-backward kernel is enqueued, in descending flat order
+        (dp.readiness_groups lists the sequence), so the all-reduce buckets start while the
+        backward still runs and only the last layers' bucket waits at the end."""
         self._join_side()
         if self.grad_ready is not None:
-            self.grad_ready(*self.grad_ranges[module])
+            spans = [self.param_span[id(p)] for p in params]
+            self.grad_ready(min(a for a, _ in spans), max(b for _, b in spans))
 
     # weight gradients run on a side stream beside the data-gradient chain (dgrad -> BN ->
     # dgrad ...): they only read activations and the dY buffer of their layer, which the main
@@ -406,6 +427,7 @@ class UNetEngine:
                 call("pcms_conv3_pack2", cs.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
             self._dirty = False
             self._packs_fresh = False
+            self._pack16()
             return
         for i, cs in enumerate(self.convs):
             w = cs.mod.weight
@@ -436,6 +458,25 @@ class UNetEngine:
         self._dirty = False
         self._packs_fresh = False
         self._stem_conv_stale = False
+        self._pack16()
+
+    def _pack16(self):
+        """The pack16 forms of the convs running on the 16x16x32 big-box kernel at the allocated
+        shape: one batched pcms_conv3_pack16 launch from the fp32 master (its table is rebuilt
+        when the buffers or the flat parameters move)."""
+        if self._p16 is None:
+            rows, tiles = [], 0
+            for cs in self.convs:
+                if cs.fwd16 is None and cs.dgrad16 is None:
+                    continue
+                rows.append([cs.mod.weight.data_ptr(), cs.cout, cs.cin, 0 if cs.fwd16 is None else cs.fwd16.data_ptr(),
+                             0 if cs.dgrad16 is None else cs.dgrad16.data_ptr(), tiles, 0, 0])
+                tiles += (cs.cout // 32) * (cs.cin // 32)
+            self._p16 = (torch.tensor(rows if rows else [[0] * 8], dtype=torch.int64, device=self.device), len(rows),
+                         tiles)
+        tab, n, tiles = self._p16
+        if n:
+            call("pcms_conv3_pack16", tab, n, tiles)
 
     def _stem_conv_pack(self):
         """The stem conv's general-kernel weight pack, when the fast path skipped it."""
@@ -591,6 +632,21 @@ class UNetEngine:
         ctws += [query("pcms_convt_fwd_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels)
                  for i, up in enumerate(self.ups)]
         b["ctws"] = torch.empty(max(ctws), dtype=torch.float32, device=dev)
+        # the 16x16x32 big-box kernel: forward (sources as the block feeds them) and dgrad
+        for cs in self.convs:
+            cs.fwd16 = cs.dgrad16 = None
+        if self.use_b16 and self.code == BF16:
+            for blk, l in [(bk, i) for i, bk in enumerate(self.enc)] + [(bk, 3 - i) for i, bk in enumerate(self.dec)]:
+                for cs, c1 in ((blk.c0, C[l] if blk in self.dec else 0), (blk.c1, 0)):
+                    if cs is self.convs[0]:
+                        continue  # the stem runs on its own kernels
+                    c0 = cs.cin_store - c1
+                    if query("pcms_conv3_big16_ok", N, *S[l], c0, c1, cs.cout):
+                        cs.fwd16 = torch.empty(query("pcms_conv3_pack16_elems", cs.cout, cs.cin), dtype=T, device=dev)
+                    if query("pcms_conv3_big16_ok", N, *S[l], cs.cout, 0, cs.cin):
+                        cs.dgrad16 = torch.empty(query("pcms_conv3_pack16_elems", cs.cin, cs.cout), dtype=T, device=dev)
+        self._p16 = None
+        self._dirty = True  # build the new pack16 forms before the next conv
         self.bufs = b
         self.buf_key = key
 
@@ -627,7 +683,11 @@ class UNetEngine:
         st = b["stats"] if training and not recompute else None
         if cs is self.convs[0] and not self.stem_sup & 1:
             self._stem_conv_pack()
-        if bnin is not None:
+        if bnin is not None and cs.fwd16 is not None:
+            call("pcms_conv3_fwd16", x0, c0, None, 0, bnin.scale, bnin.shift, cs.fwd16, cs.mod.bias, y, None, cs.cout,
+                 st, 0, N, *S, cs.cout)
+            rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, 0, cs.cout)
+        elif bnin is not None:
             call("pcms_conv3_fwd_bnin", cs.code, x0, c0, bnin.scale, bnin.shift, cs.fwd, cs.mod.bias, y, st, N,
                  *S, cs.cout)
             rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, 0, cs.cout)
@@ -635,6 +695,10 @@ class UNetEngine:
             with self._timed("stem_fwd"):
                 call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2], self.stem_dense)
             rows = query("pcms_stem_fwd_rows", N, *S)
+        elif splits == 1 and cs.fwd16 is not None:
+            call("pcms_conv3_fwd16", x0, c0, x1, c1, None, None, cs.fwd16, cs.mod.bias, y, None, cs.cout, st, 0,
+                 N, S[0], S[1], S[2], cs.cout)
+            rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, c1, cs.cout)
         elif splits == 1:
             call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
@@ -720,13 +784,15 @@ class UNetEngine:
         if x.dtype != torch.float32:
             x = x.float()
         N, _, D, H, W = x.shape
+        # buffers first: a (re)allocation decides which convs run on the 16x16x32 kernel and
+        # marks the packs dirty, so their pack16 forms are built by the _ensure_packs below
+        self._alloc(N, D, H, W)
         self._ensure_packs()
         folded = not training and self.fold_bn_eval
         if folded:
             self._ensure_eval_packs()
         else:
             self._bn_epoch += training
-        self._alloc(N, D, H, W)
         b = self.bufs
         S, C = b["S"], b["C"]
         call("pcms_pack_input", self.code, x, b["xin"], N, self.nmod, D * H * W, self.cp)
@@ -783,6 +849,8 @@ class UNetEngine:
                  nvox, b["bnws"])
         elif ga2 is not None:
             self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
+        if ga2 is not None:
+            self._grads_done(blk.b1.mod.weight, blk.b1.mod.bias)
         with self._side():
             if id(blk) in self._fwd_bnin:  # x = relu(bn0(y1)), applied in the kernel's staging (as the forward)
                 call("pcms_conv3_wgrad_bnin", blk.c1.code, acts["y1"], blk.c0.cout, blk.b0.scale, blk.b0.shift, gY,
@@ -791,6 +859,7 @@ class UNetEngine:
             else:
                 call("pcms_conv3_wgrad", blk.c1.code, acts["a1"], blk.c0.cout, None, 0, gY, blk.c1.mod.weight.grad,
                      b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target, int(self._gstore))
+        self._grads_done(blk.c1.mod.weight, blk.c1.mod.bias)
         # dgrad conv1 -> grad of a1
         self._dgrad(blk.c1, gY, gA, None, blk.c1.cin, N, S)
         # BN0/ReLU backward -> dy1 (a second buffer: the side stream may still read gY)
@@ -800,11 +869,14 @@ class UNetEngine:
             m = bn.mod
             call("pcms_bn_relu_bwd", self.code, gA, acts["y1"], bn.scale, bn.shift, bn.mean, bn.invstd, m.weight,
                  b["stats"], b["coef"], m.weight.grad, m.bias.grad, None, bn.c, nvox, b["bnws"])
+            self._grads_done(m.weight, m.bias)
             with self._side(), self._timed("stem_wgrad"):
                 call("pcms_stem_wgrad_bn", x0, gA, acts["y1"], bn.scale, bn.shift, bn.mean, bn.invstd, b["coef"],
                      blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
+            self._grads_done(blk.c0.mod.weight, blk.c0.mod.bias)
             return
         self._bn_bwd(blk.b0, gA, acts["y1"], gZ, nvox)
+        self._grads_done(blk.b0.mod.weight, blk.b0.mod.bias)
         with self._side():
             if blk is self.enc[0] and self.stem_sup & 2:
                 with self._timed("stem_wgrad"):
@@ -812,6 +884,7 @@ class UNetEngine:
             else:
                 call("pcms_conv3_wgrad", blk.c0.code, x0, c0, x1, c1, gZ, blk.c0.mod.weight.grad, b["dwt"], N,
                      *S, blk.c0.cout, blk.c0.cin, self.wgrad_target, int(self._gstore))
+        self._grads_done(blk.c0.mod.weight, blk.c0.mod.bias)
         if gx_out0 is not None:
             self._dgrad(blk.c0, gZ, gx_out0, gx_out1, cy0, N, S)
 
@@ -825,7 +898,10 @@ class UNetEngine:
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
         splits = self._splits(N, S, cs.cout, cs.cin, cs.code)
-        if splits == 1:
+        if splits == 1 and cs.dgrad16 is not None:
+            call("pcms_conv3_fwd16", gy, cs.cout, None, 0, None, None, cs.dgrad16, None, out0, out1, cy0, None, 0,
+                 N, *S, cs.cin)
+        elif splits == 1:
             call("pcms_conv3_fwd", cs.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  None, None, 0, N, *S, cs.cin, 1)
         else:
@@ -858,7 +934,8 @@ class UNetEngine:
         call("pcms_head_bn_bwd", self.code, self._dec_acts(0)["y2"], bn.scale, bn.shift, bn.mean, bn.invstd, m.weight,
              dlogits, oc.weight, oc.weight.grad, oc.bias.grad, b["redws"], b["stats"], b["coef"], m.weight.grad,
              m.bias.grad, b["gY0"], D * H * W, N, self.ncls, b["bnws"])
-        self._grads_done("outc")
+        self._grads_done(oc.weight, oc.bias)
+        self._grads_done(m.weight, m.bias)  # the last decoder block's second BatchNorm (fused above)
         g = None
         # decoder, last block first
         for i in reversed(range(4)):
@@ -877,7 +954,7 @@ class UNetEngine:
             # box, F.pad's front offsets floor((S[l] - 2 S[l + 1]) / 2))
             call("pcms_convt_wgrad_bias", self.code, hin, gu, up.weight.grad, up.bias.grad, b["ctws"], b["redws"], N,
                  *S[l + 1], up.in_channels, up.out_channels, *S[l], 512)
-            self._grads_done(f"up{i + 1}")
+            self._grads_done(up.weight, up.bias)
             gnext = b["gx4"] if i == 0 else b[f"gA{l + 1}"]
             call("pcms_convt_dgrad_ws", self.code, gu, dpack, gnext, b["ctws"], N, *S[l + 1], up.in_channels,
                  up.out_channels, *S[l])
@@ -890,12 +967,10 @@ class UNetEngine:
             if l == 0:
                 self._block_bwd(blk, b["gx0"], acts, b["xin"], self.cp, None, 0, None, None, 0, N, S[0], 0,
                                 bn1_rows=rows)
-                self._grads_done("inc")
             else:
                 gp = b[f"gU{l}"]
                 self._block_bwd(blk, b[f"gx{l}"], acts, b[f"pool{l}"], C[l - 1], None, 0, gp, None, C[l - 1], N,
                                 S[l], l, bn1_rows=rows)
-                self._grads_done(f"down{l}")
                 # MaxPool3d backward + the next block's second BN-backward reduction, one pass
                 bn = self.enc[l - 1].b1
                 call("pcms_maxpool_bwd_bn", self.code, b[f"e{l - 1}_y2"], bn.scale, bn.shift, bn.mean, bn.invstd, gp,

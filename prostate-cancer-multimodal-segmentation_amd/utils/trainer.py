@@ -124,7 +124,8 @@ class BaseTrainer:
         eng = self.model.engine()
         if self._sync is None or self._sync.flat_g is not eng.flat_g:
             self._sync = GradSync(eng.flat_g, bucket_elems=self.config.get("dp_bucket_elems", 16 << 20),
-                                  overlap=self.config.get("dp_overlap", True))
+                                  overlap=self.config.get("dp_overlap", True),
+                                  min_bucket_elems=self.config.get("dp_min_bucket_elems", 1 << 20))
         return eng, self._sync
 
     def _clip_buffers(self):

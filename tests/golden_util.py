@@ -134,3 +134,74 @@ def check_step_against_oracle(m, grads, r, lr=1e-4, grad_rl2=5e-3, report=None, 
         report.update(worst_grad_rl2=worst, confident=nconf / max(ntot, 1))
     # most weights must actually be held to the tight bar
     assert nconf >= min_confident * ntot, (nconf, ntot)
+
+
+# ---- full-size fixtures (tests/golden/make_golden_full.py: the reference itself at configs 2,
+# 4 and 5; gradients / parameters stored at flat[::stride__<key>], masks as packed bits)
+
+FULL_CFGS = {"cfg2": (2, (128, 128, 64), False), "cfg4": (2, (128, 128, 64), True),
+             "cfg5": (1, (256, 256, 96), False)}
+FULL_SEED = 1234
+
+
+def full_fixture(cfg: str) -> dict:
+    return load(f"full_{cfg}")
+
+
+def full_batch(cfg: str):
+    n, spatial, zf = FULL_CFGS[cfg]
+    b = synthetic().make_batch(n, spatial, seed=FULL_SEED, zero_fill=zf)
+    return b["image"], b["label"]
+
+
+def unpack_bits(bits: np.ndarray, n: int) -> torch.Tensor:
+    return torch.from_numpy(np.unpackbits(bits)[:n].astype(bool))
+
+
+def fixture_sampled(t: torch.Tensor, fx: dict, key: str) -> torch.Tensor:
+    """t (a full parameter-shaped tensor) at the fixture's sample positions of ``key``."""
+    return t.detach().reshape(-1).cpu()[::int(fx["stride__" + key])].double()
+
+
+def check_step_against_fixture(params: dict, grads: dict, p0: dict, buffers: dict, fx: dict, lr=1e-4,
+                               grad_rl2=5e-3, report=None, min_confident=0.5):
+    """check_step_against_oracle's bars on the fixture's sample positions: gradients' relative
+    L2 distance to the reference's fp64 gradient within max(``grad_rl2``, 10x the reference's
+    fp32 distance to it) (pre-BN conv biases: |g| < 1e-4); post-Adam parameters within 2.01 lr
+    everywhere and within 1e-5 relative on confident elements (|g + wd p| of the reference
+    above 8x that element's gradient gap); BatchNorm running statistics within 1e-4 relative
+    (full buffers).  ``params`` / ``grads`` / ``p0``: {name: full tensor} of the GPU step
+    (after Adam / its gradients / before the step); ``buffers``: the GPU model's state dict."""
+    nconf = ntot = 0
+    worst = (0.0, "")
+    for k in params:
+        got = fixture_sampled(grads[k], fx, k)
+        exp = torch.from_numpy(fx["g32__" + k]).double()
+        t = torch.from_numpy(fx["g64__" + k]).double()
+        if k.endswith(PRE_BN_BIAS):
+            assert got.abs().max() < 1e-4, k
+        else:
+            nrm = max(float(t.norm()), 1e-30)
+            rl = float((got - t).norm()) / nrm
+            rl_ref = float((exp - t).norm()) / nrm
+            worst = max(worst, (rl, k))
+            assert rl <= max(grad_rl2, 10 * rl_ref), (k, rl, rl_ref)
+        pk = fixture_sampled(params[k], fx, k)
+        pe = torch.from_numpy(fx["post__" + k]).double()
+        d = (pk - pe).abs()
+        assert float(d.max()) <= 2.01 * lr + 1e-6, (k, float(d.max()))
+        if k.endswith(PRE_BN_BIAS):
+            continue
+        conf = (exp + 1e-5 * fixture_sampled(p0[k], fx, k)).abs() > torch.clamp(8 * (got - exp).abs(), min=1e-6)
+        nconf += int(conf.sum())
+        ntot += conf.numel()
+        if conf.any():
+            assert bool(torch.all(d[conf] <= 1e-5 * pe[conf].abs() + 2e-6)), (k, float(d[conf].max()))
+    for k, v in buffers.items():
+        if k.endswith(("running_mean", "running_var")):
+            torch.testing.assert_close(v.detach().cpu(), torch.from_numpy(fx["b__" + k]), rtol=1e-4, atol=1e-5, msg=k)
+        elif k.endswith("num_batches_tracked"):
+            assert int(v) == int(fx["b__" + k]), k
+    if report is not None:
+        report.update(worst_grad_rl2=worst, confident=nconf / max(ntot, 1))
+    assert nconf >= min_confident * ntot, (nconf, ntot)

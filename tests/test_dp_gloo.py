@@ -33,7 +33,7 @@ def _bn_keys(sd):
     return [k for k in sd if k.endswith(("running_mean", "running_var"))]
 
 
-def _worker(rank, world, port, q, bucket=1 << 20, spatial=SPATIAL):
+def _worker(rank, world, port, q, bucket=1 << 20, spatial=SPATIAL, min_bucket=1 << 18):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -41,18 +41,18 @@ def _worker(rank, world, port, q, bucket=1 << 20, spatial=SPATIAL):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import pcms_amd  # noqa: F401
         from oracle import unet3d_cpu as ref
-        from pcms_amd.dp import BACKWARD_ORDER, GradSync, module_grad_ranges
+        from pcms_amd.dp import GradSync, plan_buckets, readiness_groups
         from pcms_amd.synthetic import make_batch, step_seed
 
         torch.manual_seed(0)
         sd = ref.init_params(5, 1)
         keys = ref.param_keys(sd)
-        ranges = module_grad_ranges((k, sd[k]) for k in keys)
+        groups = readiness_groups((k, sd[k]) for k in keys)   # the engine's per-layer report order
         total = sum(sd[k].numel() for k in keys)
         flat_g = torch.zeros(total)
         bn_keys = _bn_keys(sd)
         flat_bn = torch.cat([sd[k].reshape(-1) for k in bn_keys])
-        sync = GradSync(flat_g, bucket_elems=bucket)
+        sync = GradSync(flat_g, bucket_elems=bucket, min_bucket_elems=min_bucket)
         for k in keys:
             sd[k].requires_grad_(True)
         opt = torch.optim.Adam([sd[k] for k in keys], lr=1e-4, weight_decay=1e-5)
@@ -76,8 +76,8 @@ def _worker(rank, world, port, q, bucket=1 << 20, spatial=SPATIAL):
                 flat_g[off:off + n].copy_(sd[k].grad.reshape(-1))
                 off += n
             mine = flat_g.clone()         # this rank's gradient (buckets reduce in place)
-            for name in BACKWARD_ORDER:   # the engine's completion order
-                sync.ready(*ranges[name])
+            for _, lo, hi in groups:      # the engine's completion order, layer by layer
+                sync.ready(lo, hi)
             scale = sync.finish()
             assert scale == 1.0 / world
             if world > 2:
@@ -90,14 +90,16 @@ def _worker(rank, world, port, q, bucket=1 << 20, spatial=SPATIAL):
                 assert bool(((flat_g - stack.sum(0)).abs() <= bound).all()), "all-reduce != sum of rank gradients"
             assert len(sync.launched) >= 3, sync.launched   # bucketed, not one message
             # the buckets tile the flat buffer from its end down to 0, each one launched once
-            # it reached the bucket size (the module ranges make them ragged), the last one
-            # the remainder finish() launches
+            # it reached the bucket size (the layer ranges make them ragged) or, near the end,
+            # min_bucket with no more than that remaining; the last one is the remainder
+            # finish() launches
             hi = total
             for lo_b, hi_b in sync.launched:
                 assert hi_b == hi and lo_b < hi_b, sync.launched
                 hi = lo_b
             assert hi == 0, sync.launched
-            assert all(h - l >= bucket for l, h in sync.launched[:-1]), sync.launched
+            assert sync.launched == plan_buckets([(lo, hi) for _, lo, hi in groups], total, bucket, min_bucket)
+            assert all(h - l >= min_bucket for l, h in sync.launched[:-1]), sync.launched
             off = 0
             for k in keys:
                 n = sd[k].numel()
@@ -197,6 +199,41 @@ def test_backward_order_tiles_the_flat_buffer():
         assert h == hi, name
         hi = lo
     assert hi == 0
+
+
+def test_layer_readiness_groups_and_tail_bucket():
+    """Per-layer readiness (the engine's _grads_done calls): the groups tile the flat buffer
+    in descending order, the head first and the stem's first conv last, and with the product
+    bucket sizes (64 MB buckets, 4 MB minimum) the one bucket finish() launches after the
+    backward (nothing left to overlap it) is small -- the stem and down1's first conv, not the
+    ~14 M elements of down3 + down2 + down1 + inc that per-module readiness left exposed."""
+    import pcms_amd  # noqa: F401
+    from oracle import unet3d_cpu as ref
+    from pcms_amd.dp import module_grad_ranges, plan_buckets, readiness_groups
+
+    sd = ref.init_params(5, 1)
+    keys = ref.param_keys(sd)
+    groups = readiness_groups((k, sd[k]) for k in keys)
+    total = sum(sd[k].numel() for k in keys)
+    assert groups[0][0] == "outc" and groups[-1][0] == "inc.conv.0"
+    assert groups[1][0] == "up4.conv.conv.4" and groups[5][0] == "up4.up"
+    hi = total
+    for name, lo, h in groups:
+        assert h == hi and lo < h, name
+        hi = lo
+    assert hi == 0
+    # every layer group lies inside one module range (the engine reports finer, same order)
+    mods = module_grad_ranges((k, sd[k]) for k in keys)
+    for name, lo, h in groups:
+        mlo, mhi = mods[name.split(".", 1)[0]]
+        assert mlo <= lo < h <= mhi, name
+    buckets = plan_buckets([(lo, h) for _, lo, h in groups], total, 16 << 20, 1 << 20)
+    tail = buckets[-1][1] - buckets[-1][0]
+    old_tail = plan_buckets([mods[m] for m in ("outc", "up4", "up3", "up2", "up1", "down4", "down3", "down2",
+                                               "down1", "inc")], total, 16 << 20, 16 << 20)[-1]
+    assert tail <= (1 << 20), buckets           # <= 4 MB exposed
+    assert old_tail[1] - old_tail[0] > 13_000_000, old_tail
+    assert len(buckets) <= 12, buckets          # still few, large messages
 
 
 def test_gradsync_rejects_out_of_order_ranges():

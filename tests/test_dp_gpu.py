@@ -31,10 +31,10 @@ def _port():
     return p
 
 
-def _run(tmp_path, world, clip=0.0):
+def _run(tmp_path, world, clip=0.0, spatial="32,32,16"):
     out = str(tmp_path / "dp.pt")
     port = str(_port())
-    env = dict(os.environ, CLIP=str(clip), PCMS_DP_STEPS="1")
+    env = dict(os.environ, CLIP=str(clip), PCMS_DP_STEPS="1", PCMS_DP_SPATIAL=spatial)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "tools", "dp_worker.py"), str(r), str(world), port,
                                out], env=env) for r in range(world)]
     rcs = [p.wait(timeout=240) for p in procs]
@@ -122,6 +122,45 @@ def test_dp_trainer_step_two_ranks(tmp_path, clip):
         assert nconf >= 0.2 * ntot, (nconf, ntot)
         bn = torch.cat([sd[k].reshape(-1) for k in sd if k.endswith(("running_mean", "running_var"))])
         np.testing.assert_allclose(r["bn"].numpy(), bn.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_dp_trainer_step_config3_shape(tmp_path):
+    """Config 3's per-rank workload (2 x 5x128x128x64 per rank, BASELINE configs[2]) through the
+    real distributed Trainer.step (two ranks on cuda:0 over gloo, fp32 build, per-layer
+    gradient readiness driving the bucketed all-reduce) against the REFERENCE's data-parallel
+    step at that size (tests/golden/full_dp3.npz: the reference's UNet3D / BCEDiceLoss on each
+    rank's shard, gradients averaged, one Adam step, rank 0's BatchNorm buffers; fp64 mean
+    gradient as the truth).  Bars as the small two-rank test: per-replica losses within 1e-5,
+    the mean gradient left in param.grad within max(5e-3, 10x the reference fp32 distance) of
+    the fp64 mean (relative L2, at the fixture's sample positions; pre-BN conv biases < 1e-4),
+    parameters within 2.01 lr and 1e-5 relative on confident elements, BatchNorm buffers =
+    rank 0's."""
+    import pcms_amd  # noqa: F401
+    from pcms_amd.models.unet3d import UNet3D
+    fx = gu.full_fixture("dp3")
+    r = _run(tmp_path, 2, 0.0, "128,128,64")
+    for rk in range(2):
+        assert abs(r["losses"][rk][0] - float(fx["losses32"][rk])) <= 1e-5, (rk, r["losses"][rk][0])
+    torch.manual_seed(0)
+    m = UNet3D(n_modalities=5, n_classes=1)
+    names = [k for k, _ in m.named_parameters()]
+    params, grads, p0, off = {}, {}, {}, 0
+    for k, p in m.named_parameters():
+        n = p.numel()
+        params[k] = r["params"][off:off + n]
+        grads[k] = r["grad"][off:off + n]
+        p0[k] = p.detach().reshape(-1)
+        off += n
+    bn_names = [k for k in m.state_dict() if k.endswith(("running_mean", "running_var"))]
+    bufs, off = {}, 0
+    for k in bn_names:
+        n = m.state_dict()[k].numel()
+        bufs[k] = r["bn"][off:off + n]
+        off += n
+    rep = {}
+    gu.check_step_against_fixture(params, grads, p0, bufs, fx, report=rep, min_confident=0.2)
+    print(f"\n[config-3 shape, 2 ranks] worst grad rel-L2 {rep['worst_grad_rl2'][0]:.2e} ({rep['worst_grad_rl2'][1]}), "
+          f"confident params {rep['confident']:.3f}, {len(names)} tensors")
 
 
 def test_dp_trainer_train_loop_two_ranks(tmp_path):

@@ -5,26 +5,26 @@
   sample, script/data_loader.py:320-322).
 * config 5: 1 x 5x256x256x96 with decoder activation checkpointing.
 
-Bars, against the CPU oracle (tests/test_oracle_golden.py pins it to the
-reference) run on the GPU box's host cores:
-* fp32 build, configs 2 and 4, a whole training step: train-mode logits within 1e-3,
-  identical ``logit > 0`` masks where |ref| >= 1e-3, loss within 1e-5; every gradient's
-  relative L2 distance to the oracle's fp64 gradient within max(5e-3, 10x the fp32
-  oracle's own distance to it) (the golden tests' bar: at this size two fp32 summation
-  orders alone differ by ~5e-3 on some BatchNorm parameters; the 18 pre-BN conv biases,
-  whose exact gradient is 0, within 1e-4 absolute); the
-  post-Adam parameters within 2.01 lr everywhere and within 1e-5 relative on "confident"
-  elements (|g + wd p| of the oracle above 8x the tensor's largest gradient discrepancy,
-  so the Adam update's sign and size are fixed); BatchNorm running statistics within
-  1e-4 relative.
-* bf16 build (bf16 storage cannot meet 1e-3): measured against the same fp32
-  oracle with a bar set by the oracle's OWN bf16 run (torch CPU autocast bf16 of the same
-  restatement, same weights and input): max |dlogit| <= 2x the autocast run's, mask
-  agreement >= the autocast run's - 0.5 %, loss within 2x the autocast run's loss error
-  (floor 1e-3).  Configs 2, 4 and 5 (config 5: the decoder-checkpointed step).
+Pinned to the REFERENCE itself: tests/golden/full_<cfg>.npz were written by
+tests/golden/make_golden_full.py, which runs the reference's own models/unet3d.py UNet3D and
+utils/losses.py BCEDiceLoss (one step of utils/trainer.py:183-192, fp32; the same forward +
+backward in fp64 for configs 2 / 4 and under CPU bf16 autocast) on the same seed-0 init and
+seed-1234 batch (pins: tests/test_oracle_golden.py::test_full_fixtures_pinned).  No oracle runs
+on the GPU box's host.  Bars:
+* fp32 build, configs 2 and 4, a whole training step: train-mode logits within 1e-3 (at the
+  fixture's 2^18 sampled positions), identical ``logit > 0`` masks where |ref| >= 1e-3 (every
+  voxel), loss within 1e-5; every gradient's relative L2 distance to the reference's fp64
+  gradient within max(5e-3, 10x the reference's fp32 distance to it) (the 18 pre-BN conv
+  biases, exact gradient 0, within 1e-4 absolute); the post-Adam parameters within
+  2.01 lr everywhere and within 1e-5 relative on "confident" elements; BatchNorm running
+  statistics within 1e-4 relative (gradients / parameters at 8192 strided positions per tensor).
+* bf16 build (bf16 storage cannot meet 1e-3): against the reference's fp32 run with
+  a bar set by the reference's OWN bf16-autocast run: max |dlogit| <= 2x the autocast run's (same
+  sampled positions), mask agreement >= the autocast run's - 0.5 % (every voxel), loss within
+  2x the autocast run's loss error (floor 1e-3).  Configs 2, 4 and 5 (config 5: the
+  decoder-checkpointed step, and every gradient within max(3x the autocast run's relative L2
+  distance to the fp32 gradient, 2e-2)).
 """
-import os
-
 import pytest
 import torch
 
@@ -36,63 +36,26 @@ CFG2 = (2, (128, 128, 64))
 CFG5 = (1, (256, 256, 96))
 
 
-def _threads():
-    try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
-
-
-def _oracle_forward_pair(sd, x, y):
-    """The oracle's fp32 train-mode forward and its bf16-autocast run (the bf16 bar)."""
-    from oracle import unet3d_cpu as ref
-    with torch.no_grad():
-        l32 = ref.forward({k: v.clone() for k, v in sd.items()}, x, training=True)
-        loss32 = float(ref.bce_dice_loss(l32, y))
-        with torch.autocast("cpu", dtype=torch.bfloat16):
-            lbf = ref.forward({k: v.clone() for k, v in sd.items()}, x, training=True)
-        lbf = lbf.float()
-        lossbf = float(ref.bce_dice_loss(lbf, y))
-    return {"l32": l32, "loss32": loss32, "lbf": lbf, "lossbf": lossbf}
-
-
-@pytest.fixture(scope="module", params=[False, True], ids=["cfg2", "cfg4_zero_fill"])
-def oracle_run(request):
-    """The oracle's whole training step (utils/trainer.py:183-192) at config 2 / 4: logits,
-    loss, every gradient, the post-Adam parameters and BatchNorm buffers; plus the
-    autocast-bf16 forward for the bf16 bar."""
-    from oracle import unet3d_cpu as ref
-    from pcms_amd.synthetic import make_batch
-    zero_fill = request.param
-    torch.set_num_threads(_threads())
-    n, spatial = CFG2
-    b = make_batch(n, spatial, seed=1234, zero_fill=zero_fill)
-    x, y = b["image"], b["label"]
-    if zero_fill:
+@pytest.fixture(scope="module", params=["cfg2", "cfg4"], ids=["cfg2", "cfg4_zero_fill"])
+def fixture_run(request):
+    """The reference's step at config 2 / 4 (the committed fixture) and the batch it ran on."""
+    cfg = request.param
+    fx = gu.full_fixture(cfg)
+    x, y = gu.full_batch(cfg)
+    assert abs(float(x.double().sum()) - float(fx["input_sum"])) <= 1e-6 * abs(float(fx["input_sum"]))
+    if cfg == "cfg4":
         per_sample_zero = (x.abs().amax(dim=(2, 3, 4)) == 0).sum(1)
         assert all(1 <= int(k) <= 2 for k in per_sample_zero)
-    torch.manual_seed(0)
-    sd = ref.init_params(5, 1)
-    out = _oracle_forward_pair(sd, x, y)
-    out["grads64"] = gu.oracle_grads64(sd, x, y)
-    step = ref.RefStep(sd, lr=1e-4, loss="bce_dice")
-    p0 = {k: sd[k].detach().clone() for k in step.keys}
-    loss, logits = step.forward_backward(x, y)
-    grads = {k: sd[k].grad.detach().clone() for k in step.keys}
-    step.opt.step()
-    post = {k: v.detach().clone() for k, v in sd.items()}
-    out.update({"x": x, "y": y, "zero_fill": zero_fill, "step_loss": float(loss), "step_logits": logits,
-                "p0": p0, "grads": grads, "post": post, "keys": step.keys})
-    return out
+    return {"cfg": cfg, "fx": fx, "x": x, "y": y}
 
 
-def _gpu_step(precision, x, y, ckpt=False, keep_grad=False):
+def _gpu_step(precision, x, y, ckpt=False, keep_grad=False, keep_p0=False):
     from pcms_amd.models.unet3d import UNet3D
     from pcms_amd.optim import FlatAdam
     from pcms_amd.utils.losses import BCEDiceLoss
     torch.manual_seed(0)
     m = UNet3D(n_modalities=5, n_classes=1, precision=precision, checkpoint_decoder=ckpt).cuda()
+    p0 = {k: p.detach().cpu().clone() for k, p in m.named_parameters()} if keep_p0 else None
     opt = FlatAdam(m, lr=1e-4, weight_decay=1e-5)
     crit = BCEDiceLoss()
     m.train()
@@ -103,31 +66,42 @@ def _gpu_step(precision, x, y, ckpt=False, keep_grad=False):
     grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()} if keep_grad else None
     opt.step()
     torch.cuda.synchronize()
+    if keep_p0:
+        return m, logits.detach().cpu(), float(loss.detach()), grads, p0
     if keep_grad:
         return m, logits.detach().cpu(), float(loss.detach()), grads
     return m, logits.detach().cpu(), float(loss.detach())
 
 
-def test_fp32_build_matches_oracle(oracle_run):
-    r = oracle_run
-    m, lg, loss, grads = _gpu_step("fp32", r["x"], r["y"], keep_grad=True)
-    ref = r["l32"]
-    err = (lg - ref).abs().max().item()
+def _logits_vs_fixture(lg, fx):
+    st = int(fx["logit_stride"])
+    return lg.reshape(-1)[::st].double(), torch.from_numpy(fx["l32_s"]).double(), torch.from_numpy(fx["lbf_s"]).double()
+
+
+def test_fp32_build_matches_reference(fixture_run):
+    r = fixture_run
+    fx = r["fx"]
+    m, lg, loss, grads, p0 = _gpu_step("fp32", r["x"], r["y"], keep_grad=True, keep_p0=True)
+    got, ref, _ = _logits_vs_fixture(lg, fx)
+    err = (got - ref).abs().max().item()
     assert err <= 1e-3, err
-    sure = ref.abs() >= 1e-3
-    assert torch.equal((lg > 0)[sure], (ref > 0)[sure])
-    assert abs(loss - r["loss32"]) <= 1e-5, (loss, r["loss32"])
-    assert abs(loss - r["step_loss"]) <= 1e-5
+    n = lg.numel()
+    sure = gu.unpack_bits(fx["sure_bits"], n)
+    m32 = gu.unpack_bits(fx["m32_bits"], n)
+    mine = (lg > 0).reshape(-1)
+    assert torch.equal(mine[sure], m32[sure])
+    assert abs(loss - float(fx["loss32"])) <= 1e-5, (loss, float(fx["loss32"]))
     rep = {}
-    gu.check_step_against_oracle(m, grads, r, report=rep)
-    print(f"\n[{'cfg4' if r['zero_fill'] else 'cfg2'} fp32] max|dlogit| {err:.2e}, worst grad rel-L2 "
+    params = {k: p.detach().cpu() for k, p in m.named_parameters()}
+    gu.check_step_against_fixture(params, grads, p0, m.state_dict(), fx, report=rep)
+    print(f"\n[{r['cfg']} fp32 vs reference] max|dlogit| {err:.2e}, worst grad rel-L2 "
           f"{rep['worst_grad_rl2'][0]:.2e} ({rep['worst_grad_rl2'][1]}), confident params {rep['confident']:.3f}")
 
 
-def test_bf16_build_within_bf16_bar(oracle_run):
-    r = oracle_run
+def test_bf16_build_within_bf16_bar(fixture_run):
+    r = fixture_run
     _, lg, loss = _gpu_step("bf16", r["x"], r["y"])
-    _bf16_bar(lg, loss, r, "cfg4" if r["zero_fill"] else "cfg2")
+    _bf16_bar(lg, loss, r["fx"], r["cfg"])
 
 
 def test_config2_full_step_deterministic():
@@ -166,119 +140,53 @@ def test_config5_checkpointed_vs_plain():
     assert n0 == n1 == [1] * 18
 
 
-def _bf16_bar(lg, loss, r, tag):
-    ref, auto = r["l32"], r["lbf"]
+def _bf16_bar(lg, loss, fx, tag):
+    got, ref, auto = _logits_vs_fixture(lg, fx)
     e_auto = (auto - ref).abs().max().item()
-    agree_auto = ((auto > 0) == (ref > 0)).float().mean().item()
-    e = (lg - ref).abs().max().item()
-    agree = ((lg > 0) == (ref > 0)).float().mean().item()
-    print(f"\n[{tag} bf16] max|dlogit| {e:.4f} (autocast {e_auto:.4f}), masks {agree:.5f} (autocast {agree_auto:.5f}), "
-          f"loss {loss:.6f} vs {r['loss32']:.6f} (autocast {r['lossbf']:.6f})")
+    e = (got - ref).abs().max().item()
+    n = lg.numel()
+    m32 = gu.unpack_bits(fx["m32_bits"], n)
+    agree_auto = float(fx["agree_auto"])
+    agree = ((lg > 0).reshape(-1) == m32).float().mean().item()
+    loss32, lossbf = float(fx["loss32"]), float(fx["lossbf"])
+    print(f"\n[{tag} bf16 vs reference] max|dlogit| {e:.4f} (autocast {e_auto:.4f}; full tensor "
+          f"{float(fx['e_auto']):.4f}), masks {agree:.5f} (autocast {agree_auto:.5f}), "
+          f"loss {loss:.6f} vs {loss32:.6f} (autocast {lossbf:.6f})")
     assert e <= 2 * e_auto, (e, e_auto)
     assert agree >= agree_auto - 0.005, (agree, agree_auto)
-    assert abs(loss - r["loss32"]) <= max(2 * abs(r["lossbf"] - r["loss32"]), 1e-3), (loss, r["loss32"], r["lossbf"])
+    assert abs(loss - loss32) <= max(2 * abs(lossbf - loss32), 1e-3), (loss, loss32, lossbf)
 
 
-def _heartbeat(tag):
-    """A progress line under gpurun_out/ (on the GPU box) while the host oracle computes for
-    minutes with pytest's output captured."""
-    root = os.environ.get("GRAFT_REPO_ROOT")
-    if root and os.path.isdir(os.path.join(root, "gpurun_out")):
-        import time
-        with open(os.path.join(root, "gpurun_out", "heartbeat_cfg5.txt"), "a") as f:
-            f.write(f"{time.strftime('%H:%M:%S')} {tag}\n")
-
-
-class _Beat:
-    """_heartbeat every 30 s from a background thread (the oracle's torch ops hold the main one)."""
-
-    def __init__(self, tag):
-        import threading
-        self.tag, self.stop = tag, threading.Event()
-        self.t = threading.Thread(target=self._run, daemon=True)
-
-    def _run(self):
-        i = 0
-        while not self.stop.wait(30):
-            i += 1
-            _heartbeat(f"{self.tag} +{30 * i}s")
-
-    def __enter__(self):
-        _heartbeat(self.tag)
-        self.t.start()
-        return self
-
-    def __exit__(self, *a):
-        self.stop.set()
-        self.t.join()
-
-
-def _oracle_train_grads(sd, x, y, bf16):
-    """One oracle forward / BCEDice / backward at fp32 or under CPU bf16 autocast (the
-    reference's reduced-precision form): logits, loss, every gradient."""
-    from oracle import unet3d_cpu as ref
-    s = {k: v.detach().clone() for k, v in sd.items()}
-    keys = ref.param_keys(s)
-    for k in keys:
-        s[k].requires_grad_(True)
-    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=bf16):
-        out = ref.forward(s, x, training=True)
-    out = out.float()
-    loss = ref.bce_dice_loss(out, y)
-    loss.backward()
-    return out.detach(), float(loss), {k: s[k].grad.detach() for k in keys}
-
-
-def test_config5_checkpointed_bf16_vs_oracle():
-    """Config 5 (1 x 5x256x256x96, decoder checkpointing, bf16) against the oracle at that
-    shape with the autocast-relative bf16 bar (train logits / masks / loss as at configs 2
-    and 4), and every gradient: its relative L2 distance to the oracle's fp32 gradient within
-    max(3x the oracle's own bf16-autocast run's distance, 2e-2) (pre-BN conv biases, exact
-    gradient 0, SURVEY H5: within 1e-4 absolute).  The gradient form runs the oracle's fp32 AND
-    autocast backward at this size (~4 minutes of host time on the GPU box, with a heartbeat
-    file under gpurun_out/); PCMS_CFG5_GRADS=0 keeps the forward checks only.  Record:
-    profiles/r4_cfg5_grad_parity.txt."""
-    from oracle import unet3d_cpu as ref
-    from pcms_amd.synthetic import make_batch
-    torch.set_num_threads(_threads())
-    b = make_batch(*CFG5, seed=1234)
-    torch.manual_seed(0)
-    sd = ref.init_params(5, 1)
-    grads_too = os.environ.get("PCMS_CFG5_GRADS", "1") != "0"
-    if not grads_too:
-        with _Beat("oracle fp32 + autocast forward"):
-            r = _oracle_forward_pair(sd, b["image"], b["label"])
-        m, lg, loss = _gpu_step("bf16", b["image"], b["label"], ckpt=True)
-        del m
-        torch.cuda.empty_cache()
-        _bf16_bar(lg, loss, r, "cfg5 ckpt")
-        return
-    with _Beat("oracle fp32 step"):
-        l32, loss32, g32 = _oracle_train_grads(sd, b["image"], b["label"], bf16=False)
-    with _Beat("oracle bf16-autocast step"):
-        lbf, lossbf, gbf = _oracle_train_grads(sd, b["image"], b["label"], bf16=True)
-    _heartbeat("GPU step")
-    r = {"l32": l32, "loss32": loss32, "lbf": lbf, "lossbf": lossbf}
-    m, lg, loss, grads = _gpu_step("bf16", b["image"], b["label"], ckpt=True, keep_grad=True)
+def test_config5_checkpointed_bf16_vs_reference():
+    """Config 5 (1 x 5x256x256x96, decoder checkpointing, bf16) against the reference's step at
+    that shape (tests/golden/full_cfg5.npz) with the autocast-relative bf16 bar (train logits /
+    masks / loss as at configs 2 and 4), and every gradient: its relative L2 distance to the
+    reference's fp32 gradient within max(3x the reference's own bf16-autocast run's distance,
+    2e-2), on the fixture's sample positions (pre-BN conv biases, exact gradient 0, SURVEY H5:
+    within 1e-4 absolute)."""
+    fx = gu.full_fixture("cfg5")
+    x, y = gu.full_batch("cfg5")
+    assert abs(float(x.double().sum()) - float(fx["input_sum"])) <= 1e-6 * abs(float(fx["input_sum"]))
+    m, lg, loss, grads = _gpu_step("bf16", x, y, ckpt=True, keep_grad=True)
     del m
     torch.cuda.empty_cache()
-    _bf16_bar(lg, loss, r, "cfg5 ckpt")
+    _bf16_bar(lg, loss, fx, "cfg5 ckpt")
     worst = (0.0, "")
     rows = []
-    for k, t in g32.items():
-        got = grads[k].double()
+    for k, g in grads.items():
+        got = gu.fixture_sampled(g, fx, k)
         if k.endswith(gu.PRE_BN_BIAS):
             assert got.abs().max() < 1e-4, k
             continue
-        t = t.double()
+        t = torch.from_numpy(fx["g32__" + k]).double()
         nrm = max(float(t.norm()), 1e-30)
         rl = float((got - t).norm()) / nrm
-        rl_auto = float((gbf[k].double() - t).norm()) / nrm
+        rl_auto = float((torch.from_numpy(fx["gbf__" + k]).double() - t).norm()) / nrm
         bar = max(3 * rl_auto, 2e-2)
         rows.append((k, rl, rl_auto))
         worst = max(worst, (rl / bar, k))
     for k, rl, rl_auto in rows:
-        print(f"  {k:48s} rel-L2 {rl:.3e} (oracle autocast {rl_auto:.3e})")
-    print(f"[cfg5 ckpt bf16] worst gradient rel-L2 / bar {worst[0]:.3f} ({worst[1]})")
+        print(f"  {k:48s} rel-L2 {rl:.3e} (reference autocast {rl_auto:.3e})")
+    print(f"[cfg5 ckpt bf16 vs reference] worst gradient rel-L2 / bar {worst[0]:.3f} ({worst[1]})")
     for k, rl, rl_auto in rows:
         assert rl <= max(3 * rl_auto, 2e-2), (k, rl, rl_auto)

@@ -1043,3 +1043,147 @@ def test_bnin_conv_and_wgrad_bit_identical(N, S, C, wgs):
     finally:
         L.query("pcms_conv3_big_min_boxes", old)
         L.query("pcms_conv3_big_max_wgs", old_w)
+
+
+def _pack16(L, w, cout, cin, fwd=True, dgrad=True):
+    """pcms_conv3_pack16 of one conv (a one-row table): (fwd16, dgrad16) device tensors."""
+    T = torch.bfloat16
+    f = torch.empty(L.query("pcms_conv3_pack16_elems", cout, cin), dtype=T, device=DEV) if fwd else None
+    d = torch.empty(L.query("pcms_conv3_pack16_elems", cin, cout), dtype=T, device=DEV) if dgrad else None
+    wd = w.reshape(-1).to(DEV).contiguous()
+    tab = torch.tensor([[wd.data_ptr(), cout, cin, f.data_ptr() if f is not None else 0,
+                         d.data_ptr() if d is not None else 0, 0, 0, 0]], dtype=torch.int64, device=DEV)
+    L.call("pcms_conv3_pack16", tab, 1, (cout // 32) * (cin // 32))
+    torch.cuda.synchronize()
+    return f, d
+
+
+@pytest.mark.parametrize("N,c0,c1,cout,cy0,S,wgs", [
+    (1, 64, 0, 64, 64, (8, 8, 16), 0),         # one box
+    (2, 32, 32, 128, 64, (16, 8, 32), 0),      # dual source, two-pointer output, 2 channel blocks
+    (1, 16, 48, 64, 64, (8, 16, 16), 0),       # chunks split unevenly between the sources
+    (1, 128, 0, 192, 128, (16, 16, 16), 0),    # odd number of 64-channel blocks, split output
+    (2, 64, 0, 64, 64, (16, 16, 32), 3),       # persistent: 3 slots walk 16 boxes (6, 5, 5)
+    (2, 32, 32, 128, 64, (16, 16, 32), 4),     # 2 slots x 2 channel blocks, 8 boxes each
+    (1, 64, 64, 64, 64, (16, 24, 16), 5),      # dual source, 5 slots over 6 boxes (2 + 1 x 4)
+])
+def test_conv3_fwd16_big_box(N, c0, c1, cout, cy0, S, wgs):
+    """The 16x16x32 big-box kernel (pcms_conv3_fwd16, tap pairs x 16 channels per MFMA, the
+    pack16 weights) on the big-box cases: vs torch conv3d in fp64 on the same bf16 inputs, the
+    BN partial moments, and within bf16 rounding of the 32x32x16 big-box kernel's output."""
+    L = _lib()
+    old = L.query("pcms_conv3_big_min_boxes", 1)
+    old_w = L.query("pcms_conv3_big_max_wgs", wgs)
+    try:
+        dt = torch.bfloat16
+        g = torch.Generator().manual_seed(c0 + 5 * c1 + cout)
+        x0 = torch.randn(N, c0, *S, generator=g).to(dt)
+        x1 = torch.randn(N, c1, *S, generator=g).to(dt)
+        cin = c0 + c1
+        w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+        b = torch.randn(cout, generator=g)
+        ref = F.conv3d(torch.cat([x0, x1], 1).double(), w.to(dt).double(), b.double(), padding=1)
+        assert L.query("pcms_conv3_big16_ok", N, *S, c0, c1, cout) == 1
+        w16, _ = _pack16(L, w, cout, cin, dgrad=False)
+        wp = torch.empty(L.query("pcms_conv3_pack_elems", 1, cout, cin), dtype=dt, device=DEV)
+        L.call("pcms_conv3_pack", 1, w.to(DEV), wp, cout, cin, 0)
+        nvox = N * S[0] * S[1] * S[2]
+        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, c0, c1, cout)
+        outs = []
+        for k16 in (True, False):
+            y0 = torch.full((N, *S, cy0), float("nan"), dtype=dt, device=DEV)
+            y1 = torch.full((N, *S, max(cout - cy0, 8)), float("nan"), dtype=dt, device=DEV)
+            stats = torch.full((rows * (cout * 2 + 1),), float("nan"), device=DEV)
+            xa, xb = ndhwc(x0).to(DEV), ndhwc(x1).to(DEV) if c1 else None
+            if k16:
+                L.call("pcms_conv3_fwd16", xa, c0, xb, c1, None, None, w16, b.to(DEV), y0,
+                       y1 if cout > cy0 else None, cy0, stats, 0, N, *S, cout)
+            else:
+                L.call("pcms_conv3_fwd", 1, xa, c0, xb, c1, wp, b.to(DEV), y0, y1 if cout > cy0 else None, cy0, None,
+                       stats, 0, N, *S, cout, 1)
+            torch.cuda.synchronize()
+            got = ncdhw(y0.cpu())
+            if cout > cy0:
+                got = torch.cat([got, ncdhw(y1.cpu())], 1)
+            outs.append(got)
+            close(got, ref, 1e-2, f"big-box fwd ({'16x16x32' if k16 else '32x32x16'})")
+            mean, var = bn_moments(stats, rows, cout, nvox)
+            yref = ref.transpose(0, 1).reshape(cout, -1)
+            close(mean, yref.mean(1), 1e-3, "stats mean")
+            close(var, yref.var(1, unbiased=False), 1e-3, "stats var")
+        close(outs[0], outs[1].double(), 1e-2, "16x16x32 vs 32x32x16")
+    finally:
+        L.query("pcms_conv3_big_min_boxes", old)
+        L.query("pcms_conv3_big_max_wgs", old_w)
+
+
+@pytest.mark.parametrize("N,cout,cin,S,wgs", [(2, 64, 64, (16, 16, 32), 0), (1, 64, 128, (16, 16, 16), 3),
+                                              (2, 128, 64, (8, 16, 32), 0)])
+def test_conv3_dgrad16(N, cout, cin, S, wgs):
+    """The dgrad direction on the 16x16x32 kernel (pack16 dgrad form: rows Cin, k Cout, taps
+    mirrored): dx = conv(dy, w transposed and flipped) vs fp64, and the split output of a
+    dgrad into the two Up3D sources (cy0)."""
+    L = _lib()
+    old = L.query("pcms_conv3_big_min_boxes", 1)
+    old_w = L.query("pcms_conv3_big_max_wgs", wgs)
+    try:
+        dt = torch.bfloat16
+        g = torch.Generator().manual_seed(cout * 7 + cin)
+        dy = torch.randn(N, cout, *S, generator=g).to(dt)
+        w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cout)
+        ref = F.conv_transpose3d(dy.double(), w.to(dt).double(), padding=1)
+        _, d16 = _pack16(L, w, cout, cin, fwd=False)
+        cy0 = cin // 2 if cin >= 128 else cin
+        y0 = torch.empty(N, *S, cy0, dtype=dt, device=DEV)
+        y1 = torch.empty(N, *S, max(cin - cy0, 8), dtype=dt, device=DEV)
+        L.call("pcms_conv3_fwd16", ndhwc(dy).to(DEV), cout, None, 0, None, None, d16, None, y0,
+               y1 if cin > cy0 else None, cy0, None, 0, N, *S, cin)
+        torch.cuda.synchronize()
+        got = ncdhw(y0.cpu())
+        if cin > cy0:
+            got = torch.cat([got, ncdhw(y1.cpu())], 1)
+        close(got, ref, 1e-2, "dgrad16")
+    finally:
+        L.query("pcms_conv3_big_min_boxes", old)
+        L.query("pcms_conv3_big_max_wgs", old_w)
+
+
+@pytest.mark.parametrize("N,S,C,wgs", [(2, (32, 32, 32), 64, 0), (1, (32, 32, 32), 128, 24)])
+def test_bnin_conv16_bit_identical(N, S, C, wgs):
+    """pcms_conv3_fwd16 with the input BatchNorm + ReLU in its staging (isc / ish) against the
+    same kernel on the stored a1 = pcms_bn_relu(y1): bit-identical outputs and BN partials;
+    padding stays zero."""
+    L = _lib()
+    old = L.query("pcms_conv3_big_min_boxes", 1)
+    old_w = L.query("pcms_conv3_big_max_wgs", wgs)
+    try:
+        g = torch.Generator().manual_seed(22)
+        nvox = N * S[0] * S[1] * S[2]
+        T = torch.bfloat16
+        y1 = (torch.randn(nvox * C, generator=g) * 2).to(T).to(DEV)
+        sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        sh = (torch.randn(C, generator=g) * 0.5).to(DEV)
+        w = (torch.randn(C, C, 27, generator=g) * 0.05)
+        w16, _ = _pack16(L, w, C, C, dgrad=False)
+        bias = torch.randn(C, generator=g).to(DEV)
+        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, C, 0, C)
+        a1 = torch.empty_like(y1)
+        L.call("pcms_bn_relu", 1, y1, a1, sc, sh, C, nvox)
+        out = []
+        for fused in (False, True):
+            y = torch.full_like(y1, float("nan"))
+            st = torch.full((rows * (2 * C + 1),), float("nan"), device=DEV)
+            if fused:
+                L.call("pcms_conv3_fwd16", y1, C, None, 0, sc, sh, w16, bias, y, None, C, st, 0, N, *S, C)
+            else:
+                L.call("pcms_conv3_fwd16", a1, C, None, 0, None, None, w16, bias, y, None, C, st, 0, N, *S, C)
+            torch.cuda.synchronize()
+            out.append((y.view(torch.int16).clone(), st.clone()))
+        assert torch.equal(out[0][0], out[1][0])
+        assert torch.equal(out[0][1], out[1][1])
+        a64 = ncdhw(a1.view(N, *S, C).cpu()).double()
+        ref = F.conv3d(a64, w.view(C, C, 3, 3, 3).to(T).double(), bias.cpu().double(), padding=1)
+        close(ncdhw(out[1][0].view(T).view(N, *S, C).cpu()), ref, 1e-2, "fused conv16 vs fp64")
+    finally:
+        L.query("pcms_conv3_big_min_boxes", old)
+        L.query("pcms_conv3_big_max_wgs", old_w)

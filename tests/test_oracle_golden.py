@@ -64,3 +64,22 @@ def test_oracle_matches_golden(name):
 def test_dice_shape_mismatch_raises():
     with pytest.raises(ValueError):
         ref.dice_loss(torch.zeros(1, 1, 2, 2, 2), torch.zeros(1, 2, 2, 2, 2))
+
+
+@pytest.mark.parametrize("cfg", list(gu.FULL_CFGS))
+def test_full_fixtures_pinned(cfg):
+    """The full-size fixtures (tests/golden/make_golden_full.py, the reference at configs 2, 4
+    and 5) were made from the seed-0 init the engine builds (pcms_amd UNet3D, state-dict
+    SHA-256) and from the batch the GPU tests regenerate (checksums)."""
+    import pcms_amd  # noqa: F401
+    from pcms_amd.models.unet3d import UNet3D
+    fx = gu.full_fixture(cfg)
+    torch.manual_seed(0)
+    m = UNet3D(n_modalities=5, n_classes=1)
+    assert gu.sd_hash(m.state_dict()) == str(fx["sd_sha256"]) == SHA0
+    x, y = gu.full_batch(cfg)
+    assert abs(float(x.double().sum()) - float(fx["input_sum"])) <= 1e-9 * abs(float(fx["input_sum"]))
+    assert abs(float(y.double().sum()) - float(fx["label_sum"])) < 1e-6
+    n = x.shape[0] * x.shape[2] * x.shape[3] * x.shape[4]
+    assert fx["m32_bits"].size == (n + 7) // 8
+    assert float(fx["e_auto"]) > 0 and 0.9 < float(fx["agree_auto"]) <= 1.0

@@ -26,6 +26,7 @@ def worker(lib_suffix):
     import pcms_amd  # noqa: F401
     import bench
     from pcms_amd import _lib as L
+    k16 = lib_suffix == "k16"  # the 16x16x32 big-box kernel of the product library (pcms_conv3_fwd16)
     probe = bench.ClockProbe()
     res = []
     for (N, D, H, W, c0, c1, cout) in SHAPES:
@@ -42,10 +43,21 @@ def worker(lib_suffix):
         stats = torch.zeros(L.query("pcms_conv3_fwd_rows", 1, N, D, H, W, c0, c1, cout) * (2 * cout + 1) + 1024,
                             device="cuda")
 
+        if k16:
+            w16 = torch.empty(L.query("pcms_conv3_pack16_elems", cout, cin), dtype=T, device="cuda")
+            wd = w.reshape(-1).contiguous()
+            tab = torch.tensor([[wd.data_ptr(), cout, cin, w16.data_ptr(), 0, 0, 0, 0]], dtype=torch.int64,
+                               device="cuda")
+            L.call("pcms_conv3_pack16", tab, 1, (cout // 32) * (cin // 32))
+
         def run(i):
             a, b = xs[i % 2]
-            L.call("pcms_conv3_fwd", 1, a, c0, b if c1 else None, c1, wp, bias, y, None, cout, None, stats, 0,
-                   N, D, H, W, cout, 1)
+            if k16:
+                L.call("pcms_conv3_fwd16", a, c0, b if c1 else None, c1, None, None, w16, bias, y, None, cout, stats,
+                       0, N, D, H, W, cout)
+            else:
+                L.call("pcms_conv3_fwd", 1, a, c0, b if c1 else None, c1, wp, bias, y, None, cout, None, stats, 0,
+                       N, D, H, W, cout, 1)
         for i in range(5):
             run(i)
         torch.cuda.synchronize()
@@ -74,7 +86,7 @@ def main():
     for rnd in range(2):
         for suf in sufs:
             env = dict(os.environ)
-            if suf:
+            if suf and suf != "k16":
                 env["PCMS_LIB"] = os.path.join(PKG, f"libpcms_hip_{suf}.so")
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", suf or "-"], env=env,
                                capture_output=True, text=True, timeout=300)

@@ -9,7 +9,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 
-SPATIAL = (32, 32, 16)
+SPATIAL = tuple(int(v) for v in os.environ.get("PCMS_DP_SPATIAL", "32,32,16").split(","))
 
 
 def main():
