@@ -107,14 +107,17 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, int flags, hipStream_t s);
 /* The big-box convs on v_mfma_f32_16x16x32_bf16 (round 5): K = a pair of taps x 16 channels,
- * 8 M-tiles x 4 N-tiles per wave; the same boxes, halo pipeline and outputs (y, BN partial
- * rows: pcms_conv3_fwd_rows) as the 32x32x16 big-box path of pcms_conv3_fwd.  Weights in the
+ * 8 M-tiles x 4 N-tiles per wave, one wave per box d-plane; boxes of 8 d-planes (levels 0-1,
+ * the shapes of the 32x32x16 big-box path of pcms_conv3_fwd) or, where those leave CUs idle
+ * and 4-deep boxes x 64-channel blocks fill them (level 2), of 4.  BN partial rows:
+ * pcms_conv3_fwd16_rows (0: not a fwd16 shape).  Weights in the
  * pack16 layout: pcms_conv3_pack16 writes both directions of the convs of a table (int64 rows
  * {fp32 weight ptr, Cout, Cin, fwd16 ptr or 0, dgrad16 ptr or 0, first tile, 0, 0}, one tile
  * per 32 x 32 channels; fwd16 = rows Cout, k Cin; dgrad16 = rows Cin, k Cout, taps mirrored).
  * pcms_conv3_fwd16 takes isc / ish (the input's BatchNorm + ReLU, as pcms_conv3_fwd_bnin) or
  * NULL; flags 0 or PCMS_CONV_RELU; -5 where pcms_conv3_big16_ok is 0.                      */
 int pcms_conv3_big16_ok(int N, int D, int H, int W, int c0, int c1, int Cout);
+int pcms_conv3_fwd16_rows(int N, int D, int H, int W, int c0, int c1, int Cout);
 int pcms_conv3_pack16_elems(int J, int Kdim);
 int pcms_conv3_pack16(const long long* table, int ntab, int ntiles, hipStream_t s);
 int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float* isc, const float* ish,

@@ -36,6 +36,7 @@ SIGNATURES = {
     "pcms_conv3_wgrad": "ipipipppiiiiiiiis",
     "pcms_conv3_wgrad_tg_maxbox": "i",
     "pcms_conv3_big16_ok": "iiiiiii",
+    "pcms_conv3_fwd16_rows": "iiiiiii",
     "pcms_conv3_pack16_elems": "ii",
     "pcms_conv3_pack16": "piis",
     "pcms_conv3_fwd16": "pipippppppipiiiiiis",

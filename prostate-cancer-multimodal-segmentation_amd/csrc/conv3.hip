@@ -40,7 +40,16 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r_lane = lane & 31, hsel = lane >> 5;
-  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  // 1-D grid of (box, co block, split), co block fastest in the logical id; the logical id is
+  // XCD-aware (dispatch is round-robin over the 8 XCDs): an XCD runs consecutive logical ids,
+  // i.e. every co block of a few adjacent boxes, which share their halos in its L2.  (The
+  // other order -- an XCD holding every box of a few weight slices -- measured slower at
+  // levels 2-3 in round 4: DESIGN.md §0c item 3(b).)
+  const int nbox = p.N * p.nbd * p.nbh * p.nbw, nco = p.Cout >> 6;
+  const int G = gridDim.x;
+  const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int bx = (lg / nco) % nbox, by = lg % nco;
+  const int bz = lg / (nbox * nco);
   int mb = bx;
   const int bwi = mb % p.nbw; mb /= p.nbw;
   const int bhi = mb % p.nbh; mb /= p.nbh;
@@ -407,7 +416,7 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
       float* st = p.stats + ((long)bx * p.Cout + co_base + tid) * 2;
       st[0] = S;
       st[1] = M2;
-      if (tid == 0 && by == 0) p.stats[(long)gridDim.x * p.Cout * 2 + bx] = Nn;
+      if (tid == 0 && by == 0) p.stats[(long)nbox * p.Cout * 2 + bx] = Nn;
     }
   }
 }
@@ -1817,18 +1826,35 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_big_kernel(Conv3Param
 // in its own LDS slice -- no cross-wave barrier -- and writes whole 128-B channel rows.
 // ------------------------------------------------------------------------------------
 constexpr int kB6Steps = 14;                       // tap pairs per chunk
-constexpr int kB6Dist = 1;                         // B prefetch distance (k-steps)
-static_assert(kB6Steps % (kB6Dist + 1) == 0, "B ring index must continue across chunks");
+// B prefetch distance (k-steps; (Dist + 1) | 14 so the ring index continues across chunks): 1
+// with two waves per SIMD (8-deep boxes), 6 with one (4-deep: the other wave no longer covers
+// a weight fetch that misses L2)
+#ifndef B6_DIST4
+#define B6_DIST4 6  // (A/B builds: -DB6_DIST4=1)
+#endif
+template <int BD> constexpr int b6_dist() { return BD == 8 ? 1 : B6_DIST4; }
 constexpr int kB6Row = 144;                        // epilogue slice row (64 ch bf16 + pad: conflict-free writes)
 constexpr int kB6Slice = 16 * kB6Row;
-constexpr int kB6Red = 8 * 64 * 3 * 4;
-constexpr int kB6SliceOff = 2 * kBgBuf + kBgDummy;
-constexpr int kB6RedOff = kB6SliceOff + 8 * kB6Slice;
-constexpr int kB6Lds = kB6RedOff + kB6Red + 64 * 4;  // + bias
-constexpr int kB6BnOff = kB6Lds;
-constexpr int kB6LdsBn = kB6Lds + 2 * kBgBnMax * 4;
-static_assert(kB6LdsBn <= 160 * 1024, "LDS");
 constexpr int kB6EpiStores = 16;                   // 16-B stores per wave and box
+// geometry of a box of BD d-planes (one wave each): 8 (levels 0-1) or 4 (level 2, whose 8-deep
+// boxes would leave half the CUs idle).  pieces pc = tid + T j; the wave-instructions wholly
+// past the halo's 2 Halo pieces aim at a 1 KiB dummy slot (out-of-range source: no memory
+// traffic) so every wave issues the same count; a buffer holds rows up to the last real piece.
+template <int BD> struct B6G {
+  static constexpr int T = BD * 64;
+  static constexpr int Halo = (BD + 2) * kBgHH * kBgHW;                 // rows x 32 B
+  static constexpr int Pieces = (2 * Halo + T - 1) / T;                 // DMA pieces / thread
+  static constexpr int Buf = (2 * Halo + 63) / 64 * 1024;
+  static constexpr int SliceOff = 2 * Buf + kBgDummy;
+  static constexpr int RedOff = SliceOff + BD * kB6Slice;
+  static constexpr int Lds = RedOff + BD * 64 * 3 * 4 + 64 * 4;         // + bias
+  static constexpr int BnOff = Lds;
+  static constexpr int LdsBn = Lds + 2 * kBgBnMax * 4;
+  static_assert(Pieces <= kB6Steps, "one piece per k-step");
+  static_assert((Pieces - 2) * T + (BD - 1) * 64 < 2 * Halo, "dummy pieces in the last round only");
+  static_assert(LdsBn <= 160 * 1024, "LDS");
+};
+static_assert(B6G<8>::Buf == kBgBuf && B6G<8>::Pieces == kBgPieces, "8-deep geometry");
 
 __device__ __forceinline__ f32x4_t mfma16(s16x8_t a, s16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -1852,9 +1878,10 @@ template <int P, int Dist> constexpr int b6_wait(int t) {
   return n;
 }
 
-template <bool BNIN = false>
-__global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Params p, uint32_t x0bytes,
-                                                                     uint32_t x1bytes) {
+template <bool BNIN = false, int BD = 8>
+__global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p, uint32_t x0bytes,
+                                                                  uint32_t x1bytes) {
+  typedef B6G<BD> G6;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1870,7 +1897,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
     const int bhi = q % p.nbh; q /= p.nbh;
     const int bdi = q % p.nbd;
     n = q / p.nbd;
-    d0 = bdi * kBgBD; h0 = bhi * 8; w0 = bwi * 16;
+    d0 = bdi * BD; h0 = bhi * 8; w0 = bwi * 16;
   };
   const i32x4_t xr0 = buffer_desc(p.x0, x0bytes);
   const i32x4_t xr1 = buffer_desc(p.x1 ? p.x1 : p.x0, x1bytes);
@@ -1882,28 +1909,28 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
     const bool first = c < p.c0;
     const uint32_t stride = first ? p.c0 : p.c1;
     const uint32_t cofs = first ? c : c - p.c0;
-    const int pc = opaque(tid) + j * kBgThreads;
+    const int pc = opaque(tid) + j * G6::T;
     const int hv = pc >> 1;
     const int hw_ = hv % kBgHW, t_ = hv / kBgHW, hh_ = t_ % kBgHH, hd_ = t_ / kBgHH;
     const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
     uint32_t voff = kOOB;
-    if (live && hv < kBgHalo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
+    if (live && hv < G6::Halo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
         (unsigned)gw < (unsigned)p.W)
       voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs + (uint32_t)(pc & 1) * 8u) * 2u;
-    const bool dummy = j == kBgPieces - 1 && wave > 0;
+    const bool dummy = j == G6::Pieces - 1 && j * G6::T + wave * 64 >= 2 * G6::Halo;
     const uint32_t lb = __builtin_amdgcn_readfirstlane(
-        dummy ? lds0 + 2 * kBgBuf : lds0 + buf * kBgBuf + (wave * 64 + j * kBgThreads) * 16);
+        dummy ? lds0 + 2 * G6::Buf : lds0 + buf * G6::Buf + (wave * 64 + j * G6::T) * 16);
     dma16(first ? xr0 : xr1, lb, dummy ? kOOB : voff, 0);
-    return (!dummy && voff != kOOB ? 1u << j : 0u) | ((uint32_t)(pc & 1) << (8 + j));
+    return !dummy && voff != kOOB ? 1u << j : 0u;
   };
-  float* bnt = reinterpret_cast<float*>(lds + kB6BnOff);
+  float* bnt = reinterpret_cast<float*>(lds + G6::BnOff);
   auto bn_apply = [&](int buf, int chunk, uint32_t pm) {
 #pragma unroll
-    for (int j = 0; j < kBgPieces; ++j) {
+    for (int j = 0; j < G6::Pieces; ++j) {
       if (!((pm >> j) & 1)) continue;
-      const int pc = tid + j * kBgThreads;
-      u32x4_t* q = reinterpret_cast<u32x4_t*>(lds + buf * kBgBuf + pc * 16);
-      const int c = chunk * 16 + ((pm >> (8 + j)) & 1) * 8;
+      const int pc = tid + j * G6::T;
+      u32x4_t* q = reinterpret_cast<u32x4_t*>(lds + buf * G6::Buf + pc * 16);
+      const int c = chunk * 16 + (tid & 1) * 8;  // piece pc = tid + T j: its half is tid & 1
       const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(bnt + c), s1 = *reinterpret_cast<const f32x4_t*>(bnt + c + 4);
       const f32x4_t h0 = *reinterpret_cast<const f32x4_t*>(bnt + kBgBnMax + c);
       const f32x4_t h1 = *reinterpret_cast<const f32x4_t*>(bnt + kBgBnMax + c + 4);
@@ -1935,18 +1962,20 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
     bload16<3072>(dst[3], wr, off);
   };
 
-  float* red = reinterpret_cast<float*>(lds + kB6RedOff);  // [wave][64][mean, M2, n]
-  float* bls = red + 8 * 64 * 3;
+  float* red = reinterpret_cast<float*>(lds + G6::RedOff);  // [wave][64][mean, M2, n]
+  float* bls = red + BD * 64 * 3;
   if (tid < 64) bls[tid] = p.bias ? p.bias[co_base + tid] : 0.f;
   const bool to0 = co_base < p.cy0;
   const long ys = to0 ? p.cy0 : Cout - p.cy0;
   const int yc0 = to0 ? co_base : co_base - p.cy0;
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
       to0 ? p.y0 : p.y1, (short)0, (int)(p.nvox * ys * 2), 0x00020000);
-  char* slice = lds + kB6SliceOff + wave * kB6Slice;
+  char* slice = lds + G6::SliceOff + wave * kB6Slice;
   int nbdone = 0;
 
   f32x4_t acc[8][4];
+  constexpr int kB6Dist = b6_dist<BD>();
+  static_assert(kB6Steps % (kB6Dist + 1) == 0, "B ring index must continue across chunks");
   s16x8_t bset[kB6Dist + 1][4];
   int box = slot;
   int n, d0, h0, w0;
@@ -1955,7 +1984,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
     for (int i = 0; i < 2 * (slot & 3); ++i) __builtin_amdgcn_s_sleep(127);
   uint32_t pmask = 0;
 #pragma unroll
-  for (int j = 0; j < kBgPieces; ++j) pmask |= stage_piece(n, d0, h0, w0, 0, 0, j, true);
+  for (int j = 0; j < G6::Pieces; ++j) pmask |= stage_piece(n, d0, h0, w0, 0, 0, j, true);
   {
     const uint32_t boff0 = (uint32_t)(cob * 4096 + lane * 16);
 #pragma unroll
@@ -1985,7 +2014,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
       // A: this lane's halo row base -- box voxel (d = wave, h = 0, w = r16), its channel half
       // (g4 & 1) -- plus the row offset of its tap of the pair (g4 >> 1); M-tile mt = h-row mt
       // is an immediate (mt x 18 rows)
-      const uint32_t abase = lds0 + buf * kBgBuf +
+      const uint32_t abase = lds0 + buf * G6::Buf +
                              (uint32_t)(((wave * kBgHH) * kBgHW + (lo & 15)) * 32 + ((lo >> 4) & 1) * 16);
       const bool hi_tap = (lo >> 5) & 1;
       // A fragment of (step st, M-tile mt); fragments are read two M-tiles ahead of their four
@@ -2003,13 +2032,13 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
         constexpr int sn_ = st + kB6Dist;
         if constexpr (sn_ < kB6Steps) load_b(bset[sn_ % (kB6Dist + 1)], chunk, sn_, boff);
         else load_b(bset[sn_ % (kB6Dist + 1)], schunk, sn_ - kB6Steps, boff);
-        if constexpr (st < kBgPieces) {
+        if constexpr (st < G6::Pieces) {
           const uint32_t bits = stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, st, live);
           if constexpr (BNIN) pmask = (st == 0 ? 0u : pmask) | bits;
         }
         s16x8_t (&b)[4] = bset[st % (kB6Dist + 1)];
         constexpr int extra = (Slack && st < kB6Dist) ? kB6EpiStores : 0;
-        vm_wait4<b6_wait<kBgPieces, kB6Dist>(st) + extra>(b);
+        vm_wait4<b6_wait<G6::Pieces, kB6Dist>(st) + extra>(b);
         static_for<8>([&](auto mc) {
           constexpr int mt = decltype(mc)::value;
           constexpr int q = st * 8 + mt + 2;  // the fragment read now: position q (two ahead)
@@ -2025,7 +2054,7 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
         }
         __builtin_amdgcn_sched_barrier(0);
       });
-      if (!last) vm_wait<4 * (kB6Steps - kBgPieces)>();
+      if (!last) vm_wait<4 * (kB6Steps - G6::Pieces)>();
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (BNIN) bn_apply(buf ^ 1, schunk, pmask);
       __syncthreads();
@@ -2113,14 +2142,14 @@ __global__ void __launch_bounds__(kBgThreads, 1) conv3_fwd_b16_kernel(Conv3Param
   if (tid < 64) {
     float S = 0.f, Nn = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
+    for (int w = 0; w < BD; ++w) {
       S += red[(w * 64 + tid) * 3] * red[(w * 64 + tid) * 3 + 2];
       Nn += red[(w * 64 + tid) * 3 + 2];
     }
     const float m = S / Nn;
     float M2 = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
+    for (int w = 0; w < BD; ++w) {
       const float c = red[(w * 64 + tid) * 3 + 2];
       const float d = red[(w * 64 + tid) * 3] - m;
       M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
@@ -2361,10 +2390,38 @@ int pcms_conv3_fwd_bnin(int dtype, const void* x, int cin, const float* isc, con
 }
 
 // ---- 16x16x32 big-box path (conv3_fwd_b16_kernel) ----
-// 1 when pcms_conv3_fwd16 runs this conv (bf16, the big-box shapes, one split); the engine
-// keeps a pack16 for such convs
+// box depth pcms_conv3_fwd16 runs a conv with: 8 where its 8-deep boxes (x 64-channel blocks)
+// fill every CU (levels 0-1; level 2's 512-channel outputs), else 4 where 4-deep boxes do
+// (level 2's 256-channel outputs: one wave per SIMD, profiles/r5_deep_ab.txt), else 0
+static bool b16_shape_ok(int bd, int N, int D, int H, int W, int c0, int c1) {
+  const long nvox = (long)N * D * H * W;
+  return D % bd == 0 && H % 8 == 0 && W % 16 == 0 && c0 % 16 == 0 && c1 % 16 == 0 && c0 >= 16 &&
+         nvox < (1L << 30) && nvox * std::max(c0, c1) * 2 < (long)kOOB;
+}
+static int b16_depth(int N, int D, int H, int W, int c0, int c1, int Cout) {
+  if (Cout % 64 || (long)N * D * H * W * Cout * 2 >= (long)kOOB) return 0;
+  const long nb8 = (long)N * (D / 8) * (H / 8) * (W / 16), ncob = Cout / 64;
+  if (big_fwd_ok(PCMS_BF16, N, D, H, W, c0, c1)) return 8;
+  if (b16_shape_ok(8, N, D, H, W, c0, c1) && nb8 * ncob >= g_big_min_boxes) return 8;
+  const long nb4 = (long)N * (D / 4) * (H / 8) * (W / 16);
+  if (b16_shape_ok(4, N, D, H, W, c0, c1) && nb4 * ncob >= g_big_min_boxes) return 4;
+  return 0;
+}
+static int b16_slots(int bd, int N, int D, int H, int W, int Cout) {
+  const int nbox = N * (D / bd) * (H / 8) * (W / 16);
+  const int G = g_big_max_wgs > 0 ? g_big_max_wgs : device_cus();
+  return std::max(1, std::min(nbox, G / (Cout / 64)));
+}
+
+// 1 when pcms_conv3_fwd16 runs this conv (bf16, one split); the engine keeps a pack16 for
+// such convs
 int pcms_conv3_big16_ok(int N, int D, int H, int W, int c0, int c1, int Cout) {
-  return Cout % 64 == 0 && big_fwd_ok(PCMS_BF16, N, D, H, W, c0, c1) && (long)N * D * H * W * Cout * 2 < (long)kOOB;
+  return b16_depth(N, D, H, W, c0, c1, Cout) ? 1 : 0;
+}
+// BatchNorm partial rows pcms_conv3_fwd16 writes for this conv (0: not a fwd16 shape)
+int pcms_conv3_fwd16_rows(int N, int D, int H, int W, int c0, int c1, int Cout) {
+  const int bd = b16_depth(N, D, H, W, c0, c1, Cout);
+  return bd ? b16_slots(bd, N, D, H, W, Cout) : 0;
 }
 int pcms_conv3_pack16_elems(int J, int Kdim) { return (J % 16 || Kdim % 16) ? -1 : (Kdim / 16) * kB6Steps * J * 32; }
 // pack16 forms (fwd16: rows = Cout, k = Cin; dgrad16: rows = Cin, k = Cout, taps mirrored) of the
@@ -2382,7 +2439,8 @@ int pcms_conv3_pack16(const long long* table, int ntab, int ntiles, hipStream_t 
 int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float* isc, const float* ish,
                      const void* wpack16, const float* bias, void* y0, void* y1, int cy0, float* stats, int flags,
                      int N, int D, int H, int W, int Cout, hipStream_t s) {
-  if (!pcms_conv3_big16_ok(N, D, H, W, c0, c1, Cout) || (c1 > 0 && x1 == nullptr)) return -5;
+  const int bd = b16_depth(N, D, H, W, c0, c1, Cout);
+  if (!bd || (c1 > 0 && x1 == nullptr)) return -5;
   if (isc && (c1 != 0 || c0 > kBgBnMax || !ish)) return -1;
   if (stats && flags) return -6;
   if (flags & ~PCMS_CONV_RELU) return -8;
@@ -2396,12 +2454,13 @@ int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float
   p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = c0 + c1; p.Cout = Cout;
   p.nvox = (long)N * D * H * W;
   p.nchunk = p.Cin / 16; p.chunks_per_split = p.nchunk;
-  p.nbd = D / kBgBD; p.nbh = H / 8; p.nbw = W / 16;
-  const int nslot = big_slots(N, D, H, W, Cout);
-  auto kern = isc ? conv3_fwd_b16_kernel<true> : conv3_fwd_b16_kernel<false>;
-  const int ldsb = isc ? kB6LdsBn : kB6Lds;
+  p.nbd = D / bd; p.nbh = H / 8; p.nbw = W / 16;
+  const int nslot = b16_slots(bd, N, D, H, W, Cout);
+  auto kern = bd == 8 ? (isc ? conv3_fwd_b16_kernel<true, 8> : conv3_fwd_b16_kernel<false, 8>)
+                      : (isc ? conv3_fwd_b16_kernel<true, 4> : conv3_fwd_b16_kernel<false, 4>);
+  const int ldsb = bd == 8 ? (isc ? B6G<8>::LdsBn : B6G<8>::Lds) : (isc ? B6G<4>::LdsBn : B6G<4>::Lds);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldsb);
-  hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64)), dim3(kBgThreads), ldsb, s, p,
+  hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64)), dim3(bd * 64), ldsb, s, p,
                      (uint32_t)(p.nvox * c0 * 2), (uint32_t)(p.nvox * c1 * 2));
   PCMS_CHECK_LAUNCH();
 }
@@ -2452,7 +2511,7 @@ static int conv3_fwd_any(int dtype, const void* x0, int c0, const void* x1, int 
     PCMS_CHECK_LAUNCH();
   }
   if (p.isc) return -5;  // the input BatchNorm + ReLU runs on the big-box path only
-  dim3 grid(N * p.nbd * p.nbh * p.nbw, Cout / 64, splits);
+  dim3 grid(N * p.nbd * p.nbh * p.nbw * (Cout / 64) * splits);
   const bool hot = b.lbd == 2 && b.lbh == 3 && b.lbw == 4;
   const bool small = b.lbd + b.lbh + b.lbw <= 8 && g_conv_mtw2;  // <= 256 voxels: 2 M-tiles per wave
   if (dtype == PCMS_BF16) {

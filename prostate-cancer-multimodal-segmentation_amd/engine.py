@@ -586,6 +586,9 @@ class UNetEngine:
         # workspaces
         rows_f = max(max(query("pcms_conv3_mblocks", N, *S[l]) for l in range(5)),
                      query("pcms_stem_fwd_rows", N, *S[0]))
+        for blk, l in [(bk, i) for i, bk in enumerate(self.enc)] + [(bk, 3 - i) for i, bk in enumerate(self.dec)]:
+            for cs, c1 in ((blk.c0, C[l] if blk in self.dec else 0), (blk.c1, 0)):
+                rows_f = max(rows_f, query("pcms_conv3_fwd16_rows", N, *S[l], cs.cin_store - c1, c1, cs.cout))
         rows_s = max(query("pcms_split_epilogue_rows", nv[l]) for l in range(5))
         rows_b = max(query("pcms_bn_bwd_rows", self.code, C[l], nv[l]) for l in range(5))
         # BN partials [rows][C][2] + [rows] voxel counts
@@ -686,7 +689,7 @@ class UNetEngine:
         if bnin is not None and cs.fwd16 is not None:
             call("pcms_conv3_fwd16", x0, c0, None, 0, bnin.scale, bnin.shift, cs.fwd16, cs.mod.bias, y, None, cs.cout,
                  st, 0, N, *S, cs.cout)
-            rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, 0, cs.cout)
+            rows = query("pcms_conv3_fwd16_rows", N, *S, c0, 0, cs.cout)
         elif bnin is not None:
             call("pcms_conv3_fwd_bnin", cs.code, x0, c0, bnin.scale, bnin.shift, cs.fwd, cs.mod.bias, y, st, N,
                  *S, cs.cout)
@@ -698,7 +701,7 @@ class UNetEngine:
         elif splits == 1 and cs.fwd16 is not None:
             call("pcms_conv3_fwd16", x0, c0, x1, c1, None, None, cs.fwd16, cs.mod.bias, y, None, cs.cout, st, 0,
                  N, S[0], S[1], S[2], cs.cout)
-            rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, c1, cs.cout)
+            rows = query("pcms_conv3_fwd16_rows", N, *S, c0, c1, cs.cout)
         elif splits == 1:
             call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)

@@ -1117,6 +1117,78 @@ def test_conv3_fwd16_big_box(N, c0, c1, cout, cy0, S, wgs):
         L.query("pcms_conv3_big_max_wgs", old_w)
 
 
+@pytest.mark.parametrize("N,c0,c1,cout,cy0,S,wgs", [
+    (1, 64, 0, 64, 64, (12, 8, 16), 0),        # 3 four-deep boxes
+    (2, 32, 32, 128, 64, (4, 16, 32), 0),      # dual source, two-pointer output, 2 channel blocks
+    (1, 128, 0, 192, 128, (12, 16, 16), 4),    # 3 channel blocks x 1 slot walking 6 boxes
+    (2, 16, 16, 64, 64, (20, 8, 16), 3),       # 3 slots over 10 boxes
+])
+def test_conv3_fwd16_four_deep(N, c0, c1, cout, cy0, S, wgs):
+    """pcms_conv3_fwd16 on boxes of 4 d-planes (4 waves, one workgroup per CU: the level-2
+    shapes, where 8-deep boxes leave CUs idle; D % 8 != 0 here so the 4-deep form is the one
+    that runs): vs torch conv3d in fp64 on the same bf16 inputs, and its BN partial moments
+    (pcms_conv3_fwd16_rows rows)."""
+    L = _lib()
+    old = L.query("pcms_conv3_big_min_boxes", 1)
+    old_w = L.query("pcms_conv3_big_max_wgs", wgs)
+    try:
+        dt = torch.bfloat16
+        g = torch.Generator().manual_seed(3 * c0 + 7 * c1 + cout)
+        x0 = torch.randn(N, c0, *S, generator=g).to(dt)
+        x1 = torch.randn(N, c1, *S, generator=g).to(dt)
+        cin = c0 + c1
+        w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+        b = torch.randn(cout, generator=g)
+        ref = F.conv3d(torch.cat([x0, x1], 1).double(), w.to(dt).double(), b.double(), padding=1)
+        assert L.query("pcms_conv3_big16_ok", N, *S, c0, c1, cout) == 1
+        w16, _ = _pack16(L, w, cout, cin, dgrad=False)
+        nvox = N * S[0] * S[1] * S[2]
+        rows = L.query("pcms_conv3_fwd16_rows", N, *S, c0, c1, cout)
+        nbox = N * (S[0] // 4) * (S[1] // 8) * (S[2] // 16)
+        assert 1 <= rows <= nbox
+        y0 = torch.full((N, *S, cy0), float("nan"), dtype=dt, device=DEV)
+        y1 = torch.full((N, *S, max(cout - cy0, 8)), float("nan"), dtype=dt, device=DEV)
+        stats = torch.full((rows * (cout * 2 + 1),), float("nan"), device=DEV)
+        xa, xb = ndhwc(x0).to(DEV), ndhwc(x1).to(DEV) if c1 else None
+        L.call("pcms_conv3_fwd16", xa, c0, xb, c1, None, None, w16, b.to(DEV), y0, y1 if cout > cy0 else None, cy0,
+               stats, 0, N, *S, cout)
+        torch.cuda.synchronize()
+        got = ncdhw(y0.cpu())
+        if cout > cy0:
+            got = torch.cat([got, ncdhw(y1.cpu())], 1)
+        close(got, ref, 1e-2, "four-deep fwd16")
+        mean, var = bn_moments(stats, rows, cout, nvox)
+        yref = ref.transpose(0, 1).reshape(cout, -1)
+        close(mean, yref.mean(1), 1e-3, "stats mean")
+        close(var, yref.var(1, unbiased=False), 1e-3, "stats var")
+        # the dgrad direction on the same boxes (pack16 dgrad form) and the fused input BN + ReLU
+        if c1 == 0:
+            _, d16 = _pack16(L, w, cout, cin, fwd=False)
+            dy = torch.randn(N, cout, *S, generator=g).to(dt)
+            dx = torch.empty(N, *S, cin, dtype=dt, device=DEV)
+            L.call("pcms_conv3_fwd16", ndhwc(dy).to(DEV), cout, None, 0, None, None, d16, None, dx, None, cin, None,
+                   0, N, *S, cin)
+            torch.cuda.synchronize()
+            close(ncdhw(dx.cpu()), F.conv_transpose3d(dy.double(), w.to(dt).double(), padding=1), 1e-2,
+                  "four-deep dgrad16")
+            sc = (torch.rand(cin, generator=g) + 0.5).to(DEV)
+            sh = (torch.randn(cin, generator=g) * 0.5).to(DEV)
+            a = torch.empty_like(xa)
+            L.call("pcms_bn_relu", 1, xa, a, sc, sh, cin, nvox)
+            outs = []
+            for fused in (False, True):
+                y = torch.full((N, *S, cout), float("nan"), dtype=dt, device=DEV)
+                st = torch.full((rows * (cout * 2 + 1),), float("nan"), device=DEV)
+                L.call("pcms_conv3_fwd16", xa if fused else a, c0, None, 0, sc if fused else None,
+                       sh if fused else None, w16, b.to(DEV), y, None, cout, st, 0, N, *S, cout)
+                torch.cuda.synchronize()
+                outs.append((y.view(torch.int16).clone(), st.clone()))
+            assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    finally:
+        L.query("pcms_conv3_big_min_boxes", old)
+        L.query("pcms_conv3_big_max_wgs", old_w)
+
+
 @pytest.mark.parametrize("N,cout,cin,S,wgs", [(2, 64, 64, (16, 16, 32), 0), (1, 64, 128, (16, 16, 16), 3),
                                               (2, 128, 64, (8, 16, 32), 0)])
 def test_conv3_dgrad16(N, cout, cin, S, wgs):

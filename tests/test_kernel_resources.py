@@ -1,6 +1,6 @@
 """Register / scratch resources of the hand-pipelined kernels (CPU: device assembly only).
 
-The big-box conv, the stem kernels and the bf16 general conv count their vector-memory
+The big-box convs (32x32x16 and 16x16x32), the stem kernels and the bf16 general conv count their vector-memory
 operations by hand (LDS-DMA from inline asm + counted ``s_waitcnt vmcnt``); a register spill
 inside such a loop adds scratch loads whose compiler-inserted waits drain the pipeline.  The
 kernels must therefore fit their VGPR budget with no scratch (private segment 0).  The
@@ -17,13 +17,15 @@ CSRC = os.path.join(REPO, "prostate-cancer-multimodal-segmentation_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 KERNELS = {
-    "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E"],
+    "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_b16_kernelILb0ELi8E", "conv3_fwd_b16_kernelILb1ELi8E",
+                  "conv3_fwd_b16_kernelILb0ELi4E", "conv3_fwd_b16_kernelILb1ELi4E", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E"],
     "stem.hip": ["stem_fwd_direct_kernelILi2ELi3E", "stem_fwd_direct_kernelILi3ELi2E", "stem_wgrad_stream_kernel"],
     "convt.hip": ["convt_lds_kernel", "convt_fwd_stream_kernel"],
     # streaming fusions: a spill there would add scratch traffic to an HBM-bound pass
     "ops.hip": ["maxpool_bwd_bn_kernel", "head_bwd_kernel", "head_bn_apply_kernel", "bn_relu_pool_kernel"],
 }
-VGPR_BUDGET = {"convt_lds_kernel": 128}
+# (the 4-deep 16x16x32 conv runs one 256-thread workgroup per CU: one wave per SIMD)
+VGPR_BUDGET = {"convt_lds_kernel": 128, "conv3_fwd_b16_kernelILb0ELi4E": 512, "conv3_fwd_b16_kernelILb1ELi4E": 512}
 
 
 def _meta(src, tmp):

@@ -19,6 +19,8 @@ def flops(name, a):
         return 2 * 27 * (a[2] + a[4]) * a[17] * a[13] * a[14] * a[15] * a[16]
     if name == "pcms_conv3_wgrad":
         return 2 * 27 * (a[2] + a[4]) * a[12] * a[8] * a[9] * a[10] * a[11]
+    if name == "pcms_conv3_fwd16":
+        return 2 * 27 * (a[1] + a[3]) * a[17] * a[13] * a[14] * a[15] * a[16]
     if name == "pcms_conv3_fwd_bnin":
         return 2 * 27 * a[2] * a[13] * a[9] * a[10] * a[11] * a[12]
     if name == "pcms_conv3_wgrad_bnin":
@@ -43,6 +45,9 @@ def desc(name, a):
         return f"{a[2]}+{a[4]}->{a[17]} {a[14]}x{a[15]}x{a[16]} sp{a[18]}" + (" dgrad" if a[6] is None else "")
     if name == "pcms_conv3_wgrad":
         return f"{a[2]}+{a[4]}->{a[12]} {a[9]}x{a[10]}x{a[11]}"
+    if name == "pcms_conv3_fwd16":
+        return (f"{'bn(' if a[4] is not None else ''}{a[1]}{')' if a[4] is not None else ''}+{a[3]}->{a[17]} "
+                f"{a[14]}x{a[15]}x{a[16]} 16x16x32" + (" dgrad" if a[7] is None else ""))
     if name == "pcms_convt_dgrad":
         return f"{a[8]}->{a[9]} {a[5]}x{a[6]}x{a[7]}"
     if name == "pcms_conv3_fwd_bnin":
