@@ -103,6 +103,10 @@ int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, in
 /* bf16 grids of at most v boxes split the taps over two workgroups (no partial rows) before
  * splitting the voxels; 0 never, v < 0 queries; returns the previous value              */
 int pcms_conv3_wgrad_tg_maxbox(int v);
+/* compile-time-box bf16 weight gradients (the LDS-DMA kernels of levels 0-4) on
+ * v_mfma_f32_16x16x32_bf16 (1) or v_mfma_f32_32x32x16_bf16 (0, default); v < 0 queries;
+ * returns the previous setting (A/B switch) */
+int pcms_conv3_wgrad_k16(int v);
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, int flags, hipStream_t s);

@@ -35,6 +35,7 @@ SIGNATURES = {
     "pcms_conv3_wgrad_ws_floats": "iiiiiiiii",
     "pcms_conv3_wgrad": "ipipipppiiiiiiiis",
     "pcms_conv3_wgrad_tg_maxbox": "i",
+    "pcms_conv3_wgrad_k16": "i",
     "pcms_conv3_big16_ok": "iiiiiii",
     "pcms_conv3_fwd16_rows": "iiiiiii",
     "pcms_conv3_pack16_elems": "ii",

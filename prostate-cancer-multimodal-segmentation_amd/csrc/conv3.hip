@@ -424,7 +424,17 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
 // ------------------------------------------------------------------------------------
 // weight-gradient kernel
 // ------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x4_t mfma16(s16x8_t a, s16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
 constexpr int kWThreads = 512;          // 8 waves: wave = (co-tile, tap-group)
+// ablation builds only (tests/tools/wgrad_abl.py; 0 in the product): bit 1 the direct flush's
+// global stores dropped, 2 no staging after a workgroup's first box, 4 no MFMA phase
+#ifndef WGRAD_ABL
+#define WGRAD_ABL 0
+#endif
 constexpr int kWHaloMax = 720;          // halo rows (box <= 256 voxels)
 
 template <typename T> struct WTraits;
@@ -487,8 +497,14 @@ struct WgradParams {
 // in LDS by the thread that staged each piece, after its DMA landed and before the barrier that
 // publishes the buffer (the BatchNorm + ReLU of the layer below, fused as in
 // conv3_fwd_big_kernel<true>); out-of-range pieces (zero padding) stay zero
-template <typename T, int LBD, int LBH, int LBW, bool TG = false, bool P4 = false, bool BNIN = false>
+// K16 (bf16, compile-time box, no TG): v_mfma_f32_16x16x32_bf16 instead of 32x32x16 -- the same
+// LDS reads per FLOP (K = 32 voxels per step: 8 A + 4 B transposed reads per tap pair of
+// ci tiles), the MFMA shape that runs the power-capped big-box convs at a higher clock
+// (profiles/r5_mfma_shape_probe.txt).  acc16[j][ct][t]: tap j, 16-co tile ct, 16-ci tile t.
+template <typename T, int LBD, int LBH, int LBW, bool TG = false, bool P4 = false, bool BNIN = false,
+          bool K16 = false>
 __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p) {
+  static_assert(!K16 || (std::is_same<T, bf16_t>::value && LBW >= 2 && !TG), "K16: bf16 fixed boxes");
   const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
   typedef WTraits<T> Tr;
   typedef typename Tr::Frag Frag;
@@ -543,6 +559,15 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   for (int t = 0; t < 8; ++t)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  f32x4_t acc16[4][4][2];
+  if constexpr (K16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc16[j][c][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  }
 
   // register staging: pieces of 16 B
   constexpr int DYP = Tr::BV * Tr::DYROW / 16;
@@ -840,9 +865,77 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       }
     });
   };
+  // K16: 32-voxel steps; lane (G = lane / 16, q, pp) reads voxels 8 G + q and 8 G + q + 4 of a
+  // step (one w-row, or two adjacent h-rows at w = 4), A = dy^T rows co 16 c + 4 pp.., B = x
+  // columns ci 16 t + 4 pp.. of the tap's halo rows; MFMAs walk co tile c outermost.
+  auto compute_fixed16 = [&](const char* buf, auto&& mid) __attribute__((always_inline)) {
+    constexpr int LD = LBW >= 2 ? LBD : 0, LH = LBW >= 2 ? LBH : 0, LW = LBW >= 2 ? LBW : 4;
+    constexpr int HHc = (1 << LH) + 2, HWc = (1 << LW) + 2;
+    constexpr int NK = (1 << (LD + LH + LW)) / 32;
+    static_assert(LW >= 3 || (LW == 2 && LH >= 3), "K16 box: a 32-voxel step stays in one d-plane");
+    constexpr int D4 = LW >= 3 ? 4 : HWc;
+    const int G4 = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int vl = 8 * G4 + q;
+    const int vrow = (vl >> LW) * HWc + (vl & ((1 << LW) - 1));
+    const char* ab[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ab[c] = buf + dy_off_bf16(vl, c * 16 + pp * 4);
+    const char* bb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tap = tapof(j);
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      bb[j] = buf + DYBYTES + (vrow + (kd * HHc + kh) * HWc + kw) * Tr::XROW + pp * 8;
+    }
+    auto cat = [](s16x4_t lo, s16x4_t hi) __attribute__((always_inline)) {
+      return (s16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    auto hro = [](int s) __attribute__((always_inline)) {
+      const int v0 = 32 * s, rd = v0 >> (LH + LW), rh = (v0 >> LW) & ((1 << LH) - 1);
+      return (rd * HHc + rh) * HWc * Tr::XROW;
+    };
+    // one register set per operand: co tile c's A fragment of step s + 1 is read right after
+    // c's MFMAs of step s (a whole step of slack); tap j's B fragments after their last use
+    // (c = 3), a few MFMAs before the next step needs them (the other wave of the SIMD covers)
+    s16x8_t fa[4], fb[4][2];
+    auto loadA = [&](int s, int c) __attribute__((always_inline)) {
+      fa[c] = cat(tr_read(ab[c], s * 4096), tr_read(ab[c], s * 4096 + 512));
+    };
+    auto loadB = [&](int s, int j) __attribute__((always_inline)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        fb[j][t] = cat(tr_read(bb[j], hro(s) + t * 32), tr_read(bb[j], hro(s) + D4 * Tr::XROW + t * 32));
+    };
+#pragma unroll
+    for (int c = 0; c < 4; ++c) loadA(0, c);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) loadB(0, j);
+    if (four) loadB(0, 3);
+    static_for<NK>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (s == NK / 2) mid();  // BNIN: the next box's BN apply under this box's MFMAs
+      static_for<4>([&](auto ccc) __attribute__((always_inline)) {
+        constexpr int c = decltype(ccc)::value;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) acc16[j][c][t] = mfma16(fa[c], fb[j][t], acc16[j][c][t]);
+          if constexpr (c == 3 && s + 1 < NK) loadB(s + 1, j);
+        }
+        if (four) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) acc16[3][c][t] = mfma16(fa[c], fb[3][t], acc16[3][c][t]);
+          if constexpr (c == 3 && s + 1 < NK) loadB(s + 1, 3);
+        }
+        if constexpr (s + 1 < NK) loadA(s + 1, c);
+      });
+    });
+  };
   // mid(): work placed halfway through the box's MFMA steps (compute_fixed), or after them
   auto compute_box = [&](const char* buf, auto&& mid) __attribute__((always_inline)) {
-    if constexpr (!kX3 && !kX6 && LBW >= 2) {
+    if constexpr (K16) {
+      compute_fixed16(buf, mid);
+    } else if constexpr (!kX3 && !kX6 && LBW >= 2) {
       compute_fixed(buf, mid);
     } else {
       compute(buf);
@@ -933,7 +1026,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       __syncthreads();
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
-        if (b + 1 < b_end) xm = stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
+        if (b + 1 < b_end && !(WGRAD_ABL & 2)) xm = stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
         if constexpr (BNIN) {
           // this thread's pieces of box b + 1 have landed once its vmcnt drains (LDS-DMA
           // completion is per wave); nobody reads buffer cur ^ 1 before the barrier below
@@ -941,7 +1034,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (b + 1 < b_end) bn_x(wlds + (cur ^ 1) * BUFBYTES, xm);
           });
-        } else {
+        } else if constexpr (!(WGRAD_ABL & 4)) {
           compute_box(wlds + cur * BUFBYTES, nomid);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -995,6 +1088,22 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
               const int col = (e & 3) + 8 * (e >> 2) + 4 * hsel;
               tile[(col * 32 + (lane & 7)) * 27 + tap] = acc[ct * 4][e];
             }
+        } else if constexpr (K16) {
+          // acc16[j][c][t] element e: co 16 c + 4 (lane / 16) + e, ci 16 t + lane % 16
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (!owned(j)) continue;
+            const int tap = tapof(j);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+              for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const int col = cc * 16 + 4 * (lane >> 4) + e;
+                  tile[(col * 32 + t * 16 + (lane & 15)) * 27 + tap] = acc16[j][2 * ct + cc][t][e];
+                }
+          }
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -1034,7 +1143,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
 #pragma unroll
           for (int k = 0; k < kPer; ++k) {
             const int q4 = tid + k * kWThreads, row = q4 / 216, q = q4 % 216;
-#if defined(WGRAD_ABL) && (WGRAD_ABL & 1)  // ablation build: the flush's global stores dropped
+#if WGRAD_ABL & 1  // ablation build: the flush's global stores dropped
             const f32x4_t o = g[k] + *reinterpret_cast<const f32x4_t*>(tile + row * 864 + 4 * q);
             if (q4 < kQ && o[0] == 1.2345e30f)
               *reinterpret_cast<f32x4_t*>(p.dw + ((long)(co_base + ct * 32 + row) * p.cw + ci_base) * 27 + 4 * q) = o;
@@ -1067,6 +1176,24 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
             const int co = co_base + ct * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel;
             if (co < p.Cout) prow[((long)tap * p.Cout + co) * p.Cin + ci] = acc[ct * 4][e];
           }
+      return;
+    }
+    if constexpr (K16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!owned(j)) continue;
+        const int tap = tapof(j);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int co = co_base + c * 16 + 4 * (lane >> 4) + e;
+              const int ci = ci_base + t * 16 + (lane & 15);
+              if (co < p.Cout && ci < p.Cin) prow[((long)tap * p.Cout + co) * p.Cin + ci] = acc16[j][c][t][e];
+            }
+      }
       return;
     }
 #pragma unroll
@@ -1856,10 +1983,6 @@ template <int BD> struct B6G {
 };
 static_assert(B6G<8>::Buf == kBgBuf && B6G<8>::Pieces == kBgPieces, "8-deep geometry");
 
-__device__ __forceinline__ f32x4_t mfma16(s16x8_t a, s16x8_t b, f32x4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
-                                                 0, 0, 0);
-}
 // halo row offset of tap t (10 x 18 rows per plane); the zero-weight 28th tap reads tap 26's rows
 __host__ __device__ constexpr int b6_tapoff(int t) {
   return t > 26 ? b6_tapoff(26) : ((t / 9) * kBgHH + (t / 3) % 3) * kBgHW + t % 3;
@@ -2538,6 +2661,9 @@ extern "C" {
 // bf16 grids of at most this many boxes split their taps over two workgroups (TG) before
 // splitting their voxels (partial rows + a reduction pass); 0 disables
 static int g_wgrad_tg_maxbox = 64;
+// compile-time-box bf16 weight gradients on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0, the
+// product: the 16x16x32 form ran at a higher clock but slower, profiles/r5_wgrad_k16_abl.txt)
+static int g_wgrad_k16 = 0;
 struct WgradPlan { Box b; int nbd, nbh, nbw, nbox, bps, splits, ntg; };
 static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int Cout, int target_wgs) {
   WgradPlan q;
@@ -2555,7 +2681,14 @@ static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int 
   return q;
 }
 
-// fp32 workspace floats pcms_conv3_wgrad needs: one [27][Cout][c0+c1] partial row per split
+// the compile-time-box bf16 weight gradients on 16x16x32 (1) or 32x32x16 (0) MFMAs; v < 0
+// queries.  Returns the previous value.
+int pcms_conv3_wgrad_k16(int v) {
+  const int old = g_wgrad_k16;
+  if (v >= 0) g_wgrad_k16 = v;
+  return old;
+}
+
 // grids of at most v boxes split the taps of the bf16 weight gradient over two workgroups
 // before splitting the voxels (0: never); v < 0 queries.  Returns the previous value.
 int pcms_conv3_wgrad_tg_maxbox(int v) {
@@ -2564,6 +2697,7 @@ int pcms_conv3_wgrad_tg_maxbox(int v) {
   return old;
 }
 
+// fp32 workspace floats pcms_conv3_wgrad needs: one [27][Cout][c0+c1] partial row per split
 int pcms_conv3_wgrad_ws_floats(int dtype, int N, int D, int H, int W, int c0, int c1, int Cout, int target_wgs) {
   const int Cin = c0 + c1;
   return wgrad_plan(dtype, N, D, H, W, Cin, Cout, target_wgs).splits * 27 * Cout * Cin;
@@ -2641,9 +2775,13 @@ static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, in
     lds = (size_t)WTraits<bf16_t>::NBUF * (WTraits<bf16_t>::BV * WTraits<bf16_t>::DYROW + kWHaloMax * WTraits<bf16_t>::XROW) +
           64 * sizeof(float);
     auto kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1, false, false, true>;
-    if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4, false, false, true>;
-    else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4, false, false, true>;
-    else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3, false, false, true>;
+    const bool k16 = g_wgrad_k16;
+    if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4)
+      kern = k16 ? conv3_wgrad_kernel<bf16_t, 2, 2, 4, false, false, true, true> : conv3_wgrad_kernel<bf16_t, 2, 2, 4, false, false, true>;
+    else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4)
+      kern = k16 ? conv3_wgrad_kernel<bf16_t, 1, 3, 4, false, false, true, true> : conv3_wgrad_kernel<bf16_t, 1, 3, 4, false, false, true>;
+    else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3)
+      kern = k16 ? conv3_wgrad_kernel<bf16_t, 2, 3, 3, false, false, true, true> : conv3_wgrad_kernel<bf16_t, 2, 3, 3, false, false, true>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
   } else if (dtype == PCMS_BF16) {
@@ -2652,10 +2790,15 @@ static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, in
     if (q.ntg == 2) {
       kern = conv3_wgrad_kernel<bf16_t, -1, -1, -1, true>;
       if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3, true>;
-    } else if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
-    else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) kern = conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
-    else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) kern = conv3_wgrad_kernel<bf16_t, 2, 3, 3>;
-    else if (q.b.lbd == 3 && q.b.lbh == 3 && q.b.lbw == 2) kern = conv3_wgrad_kernel<bf16_t, 3, 3, 2>;  // level 4
+    } else if (q.b.lbd == 2 && q.b.lbh == 2 && q.b.lbw == 4) {
+      kern = g_wgrad_k16 ? conv3_wgrad_kernel<bf16_t, 2, 2, 4, false, false, false, true> : conv3_wgrad_kernel<bf16_t, 2, 2, 4>;
+    } else if (q.b.lbd == 1 && q.b.lbh == 3 && q.b.lbw == 4) {
+      kern = g_wgrad_k16 ? conv3_wgrad_kernel<bf16_t, 1, 3, 4, false, false, false, true> : conv3_wgrad_kernel<bf16_t, 1, 3, 4>;
+    } else if (q.b.lbd == 2 && q.b.lbh == 3 && q.b.lbw == 3) {
+      kern = g_wgrad_k16 ? conv3_wgrad_kernel<bf16_t, 2, 3, 3, false, false, false, true> : conv3_wgrad_kernel<bf16_t, 2, 3, 3>;
+    } else if (q.b.lbd == 3 && q.b.lbh == 3 && q.b.lbw == 2) {  // level 4
+      kern = g_wgrad_k16 ? conv3_wgrad_kernel<bf16_t, 3, 3, 2, false, false, false, true> : conv3_wgrad_kernel<bf16_t, 3, 3, 2>;
+    }
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);
   } else if (dtype == PCMS_F32X3) {

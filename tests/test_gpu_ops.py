@@ -341,6 +341,26 @@ def _wgrad_case(L, dt, code, N, c0, c1, cout, S, store):
     close(got, wr.grad, 1e-4 if code else 2e-5, "wgrad")
 
 
+@pytest.mark.parametrize("k16", [1, 0])
+@pytest.mark.parametrize("N,c0,c1,cout,S", [
+    (2, 64, 0, 64, (16, 32, 64)),      # level-0/1 geometry (box 4x4x16 or 2x8x16), voxel splits
+    (1, 64, 64, 128, (8, 16, 16)),     # two sources, 2 co blocks
+    (2, 128, 0, 128, (16, 16, 8)),     # compile-time 4x8x8 box
+    (2, 64, 0, 64, (8, 8, 4)),         # 8x8x4 box: 4-wide rows, a step spans 8 h-rows
+])
+def test_conv3_wgrad_k16(k16, N, c0, c1, cout, S):
+    """The compile-time-box bf16 weight gradient on v_mfma_f32_16x16x32_bf16 (the product) and
+    on 32x32x16 (pcms_conv3_wgrad_k16(0)), both vs fp64, with the fresh-store and the
+    accumulate flush."""
+    L = _lib()
+    old = L.query("pcms_conv3_wgrad_k16", k16)
+    try:
+        for store in (1, 0):
+            _wgrad_case(L, torch.bfloat16, 1, N, c0, c1, cout, S, store)
+    finally:
+        L.query("pcms_conv3_wgrad_k16", old)
+
+
 @pytest.mark.parametrize("c0,c1,S", [(64, 0, (32, 32, 32)), (32, 32, (24, 20, 40))])
 def test_conv3_wgrad_many_boxes(c0, c1, S):
     """bf16 weight gradient over a grid of many boxes (the level-0..2 voxel-split plan, partial
