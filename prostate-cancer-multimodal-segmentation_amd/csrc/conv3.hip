@@ -810,7 +810,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // LDS latency is behind the MFMAs instead of in front of each pair.  Taps wave + 8 j, j < 3
   // for every wave; the fourth (waves 0-2: taps 24-26) in a uniform branch at the step's end,
   // its fragment also one step ahead (one code path: no per-variant register allocation).
-  auto compute_fixed = [&](const char* buf, auto&& mid) __attribute__((always_inline)) {
+  auto compute_fixed = [&](const char* buf, auto&& mid, auto&& stage) __attribute__((always_inline)) {
     constexpr int LD = LBW >= 2 ? LBD : 0, LH = LBW >= 2 ? LBH : 0, LW = LBW >= 2 ? LBW : 4;
     constexpr int HHc = (1 << LH) + 2, HWc = (1 << LW) + 2;
     constexpr int NK = (1 << (LD + LH + LW)) / 16;
@@ -851,6 +851,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     if (four) load3(0, 0);
     static_for<NK>([&](auto sc) __attribute__((always_inline)) {
       constexpr int s = decltype(sc)::value, cs = s & 1, ns = cs ^ 1;
+      stage(sc);  // the next box's halo pieces of this step (their address VALU under the MFMAs)
       if constexpr (s == NK / 2) mid();  // BNIN: the next box's BN apply under this box's MFMAs
       if constexpr (s + 1 < NK) load(s + 1, ns);
 #pragma unroll
@@ -868,7 +869,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
   // K16: 32-voxel steps; lane (G = lane / 16, q, pp) reads voxels 8 G + q and 8 G + q + 4 of a
   // step (one w-row, or two adjacent h-rows at w = 4), A = dy^T rows co 16 c + 4 pp.., B = x
   // columns ci 16 t + 4 pp.. of the tap's halo rows; MFMAs walk co tile c outermost.
-  auto compute_fixed16 = [&](const char* buf, auto&& mid) __attribute__((always_inline)) {
+  auto compute_fixed16 = [&](const char* buf, auto&& mid, auto&& stage) __attribute__((always_inline)) {
     constexpr int LD = LBW >= 2 ? LBD : 0, LH = LBW >= 2 ? LBH : 0, LW = LBW >= 2 ? LBW : 4;
     constexpr int HHc = (1 << LH) + 2, HWc = (1 << LW) + 2;
     constexpr int NK = (1 << (LD + LH + LW)) / 32;
@@ -913,6 +914,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     if (four) loadB(0, 3);
     static_for<NK>([&](auto sc) __attribute__((always_inline)) {
       constexpr int s = decltype(sc)::value;
+      stage(sc);
       if constexpr (s == NK / 2) mid();  // BNIN: the next box's BN apply under this box's MFMAs
       static_for<4>([&](auto ccc) __attribute__((always_inline)) {
         constexpr int c = decltype(ccc)::value;
@@ -932,23 +934,59 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     });
   };
   // mid(): work placed halfway through the box's MFMA steps (compute_fixed), or after them
-  auto compute_box = [&](const char* buf, auto&& mid) __attribute__((always_inline)) {
+  // stage(s): called at the start of every k-step of the compile-time-box loops
+  constexpr bool kSpread = !kX3 && !kX6 && LBW >= 2;
+  auto compute_box = [&](const char* buf, auto&& mid, auto&& stage) __attribute__((always_inline)) {
     if constexpr (K16) {
-      compute_fixed16(buf, mid);
-    } else if constexpr (!kX3 && !kX6 && LBW >= 2) {
-      compute_fixed(buf, mid);
+      compute_fixed16(buf, mid, stage);
+    } else if constexpr (kSpread) {
+      compute_fixed(buf, mid, stage);
     } else {
       compute(buf);
       mid();
     }
   };
   auto nomid = []() __attribute__((always_inline)) {};
+  auto nostage = [](auto) __attribute__((always_inline)) {};
 
   // bf16 hot path: both tiles arrive by buffer LDS-DMA (no register staging); the next box
   // streams in while this one computes.  The dy tile keeps dy_off_bf16's half swap (applied
   // to the source address); each wave instruction is all-dy or all-halo (2048 dy pieces);
   // out-of-range pieces read zeros.
   // BNIN: bit i = piece i of this thread is a real (in-range) x-halo piece
+  // piece i (16 B; i < MAXP) of this thread for the box at (n, d0, h0, w0) into buf; returns
+  // bit i when it is a real (in-range) x-halo piece (BNIN)
+  auto stage_piece = [&](char* buf, int i, int n, int d0, int h0, int w0) -> uint32_t {
+    const int pc0 = (tid & ~63) + i * kWThreads;  // wave-uniform first piece
+    if (pc0 >= DYP + XP) return 0u;
+    const uint32_t lb0 = lds_addr(buf);
+    const int pc = pc0 + lane;
+    uint32_t voff = kOOB;
+    if (pc0 < DYP) {
+      const int r = pc >> 3, q = pc & 7;
+      const int ql = q ^ (((r >> 1) & 1) << 2);
+      if (r < boxvol) {
+        const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+        const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+        if (gd < p.D && gh < p.H && gw < p.W)
+          voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * p.Cout + co_base + ql * 8) * 2);
+      }
+      dma16(buffer_desc(p.dy, p.dybytes), __builtin_amdgcn_readfirstlane(lb0 + pc0 * 16), voff, 0);
+      return 0u;
+    }
+    const bool first = ci_base < p.c0;  // a 32-channel block lies in one source
+    const int xs = first ? p.c0 : p.c1, xc = first ? ci_base : ci_base - p.c0;
+    const int hp = pc - DYP;
+    const int hv = hp >> 2, q = hp & 3;
+    const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+    const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+    if (hp < XP && gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && xc + q * 8 < xs)
+      voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * xs + xc + q * 8) * 2);
+    dma16(buffer_desc(first ? p.x0 : p.x1, first ? p.x0bytes : p.x1bytes),
+          __builtin_amdgcn_readfirstlane(lb0 + DYBYTES + (pc0 - DYP) * 16), voff, 0);
+    return voff != kOOB ? 1u << i : 0u;
+  };
+  // a whole box at once (runtime-geometry kernels and the first box)
   auto stage_dma = [&](char* buf, int b) -> uint32_t {
     uint32_t xm = 0;
     int n, d0, h0, w0;
@@ -1026,16 +1064,43 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       __syncthreads();
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
-        if (b + 1 < b_end && !(WGRAD_ABL & 2)) xm = stage_dma(wlds + (cur ^ 1) * BUFBYTES, b + 1);
+        const bool nxt = b + 1 < b_end && !(WGRAD_ABL & 2);
+        char* nbuf = wlds + (cur ^ 1) * BUFBYTES;
+        // compile-time boxes: the next box's pieces are issued PPS per k-step over the first
+        // SPW steps, so their address arithmetic runs on the VALU beside this box's MFMAs
+        // instead of in a block before them (where both waves of a SIMD stalled the MFMA pipe
+        // together); they land long before the box-end wait (BNIN: before its apply at NK / 2)
+        int n1 = 0, d1 = 0, h1 = 0, w1 = 0;
+        if constexpr (kSpread && !(WGRAD_ABL & 4)) {
+          if (nxt) box_origin(b + 1, n1, d1, h1, w1);
+          xm = 0;
+        } else if (nxt) {
+          xm = stage_dma(nbuf, b + 1);
+        }
+        auto stage = [&](auto sc) __attribute__((always_inline)) {
+          if constexpr (kSpread) {
+            constexpr int st = decltype(sc)::value;
+            constexpr int NKc = (1 << (LBD + LBH + LBW)) / (K16 ? 32 : 16);
+            constexpr int SPW = BNIN ? NKc / 4 : NKc / 2;
+            constexpr int PPS = (MAXP + SPW - 1) / SPW;
+            if constexpr (st * PPS < MAXP) {
+              if (nxt) {
+#pragma unroll
+                for (int k = 0; k < PPS; ++k)
+                  if (st * PPS + k < MAXP) xm |= stage_piece(nbuf, st * PPS + k, n1, d1, h1, w1);
+              }
+            }
+          }
+        };
         if constexpr (BNIN) {
           // this thread's pieces of box b + 1 have landed once its vmcnt drains (LDS-DMA
           // completion is per wave); nobody reads buffer cur ^ 1 before the barrier below
           compute_box(wlds + cur * BUFBYTES, [&]() __attribute__((always_inline)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (b + 1 < b_end) bn_x(wlds + (cur ^ 1) * BUFBYTES, xm);
-          });
+            if (b + 1 < b_end) bn_x(nbuf, xm);
+          }, stage);
         } else if constexpr (!(WGRAD_ABL & 4)) {
-          compute_box(wlds + cur * BUFBYTES, nomid);
+          compute_box(wlds + cur * BUFBYTES, nomid, stage);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1049,7 +1114,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
       for (int b = b_beg; b < b_end; ++b) {
         const int cur = (b - b_beg) & 1;
         if (b + 1 < b_end) stage_load(b + 1);
-        compute_box(wlds + cur * BUFBYTES, nomid);
+        compute_box(wlds + cur * BUFBYTES, nomid, nostage);
         if (b + 1 < b_end) stage_store(wlds + (cur ^ 1) * BUFBYTES);
         __syncthreads();
       }

@@ -67,7 +67,7 @@ def worker(suf):
 def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--worker":
         return worker(sys.argv[2] if sys.argv[2] != "-" else "")
-    sufs = sys.argv[1:] or [""]
+    sufs = [("" if a in ("product", "-") else a) for a in sys.argv[1:]] or [""]
     for rnd in range(2):
         for suf in sufs:
             env = dict(os.environ)
