@@ -122,6 +122,10 @@ int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, 
  * NULL; flags 0 or PCMS_CONV_RELU; -5 where pcms_conv3_big16_ok is 0.                      */
 int pcms_conv3_big16_ok(int N, int D, int H, int W, int c0, int c1, int Cout);
 int pcms_conv3_fwd16_rows(int N, int D, int H, int W, int c0, int c1, int Cout);
+/* 128-channel blocks (4-deep boxes, 8 N-tiles per wave: one staged halo feeds 128 output
+ * channels) where Cout % 128 == 0 and they fill the CUs: 1 or 0 (default); v < 0 queries;
+ * returns the previous setting (set before any workspace query)                          */
+int pcms_conv3_b16_nt8(int v);
 int pcms_conv3_pack16_elems(int J, int Kdim);
 int pcms_conv3_pack16(const long long* table, int ntab, int ntiles, hipStream_t s);
 int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float* isc, const float* ish,

@@ -2024,22 +2024,28 @@ constexpr int kB6Steps = 14;                       // tap pairs per chunk
 #ifndef B6_DIST4
 #define B6_DIST4 6  // (A/B builds: -DB6_DIST4=1)
 #endif
-template <int BD> constexpr int b6_dist() { return BD == 8 ? 1 : B6_DIST4; }
-constexpr int kB6Row = 144;                        // epilogue slice row (64 ch bf16 + pad: conflict-free writes)
-constexpr int kB6Slice = 16 * kB6Row;
-constexpr int kB6EpiStores = 16;                   // 16-B stores per wave and box
+// NT = 8 (128 output channels per wave, 256 accumulators: one wave per SIMD only) keeps two
+// register sets, Dist 1
+template <int BD, int NT = 4> constexpr int b6_dist() { return BD == 8 || NT == 8 ? 1 : B6_DIST4; }
 // geometry of a box of BD d-planes (one wave each): 8 (levels 0-1) or 4 (level 2, whose 8-deep
-// boxes would leave half the CUs idle).  pieces pc = tid + T j; the wave-instructions wholly
-// past the halo's 2 Halo pieces aim at a 1 KiB dummy slot (out-of-range source: no memory
-// traffic) so every wave issues the same count; a buffer holds rows up to the last real piece.
-template <int BD> struct B6G {
+// boxes would leave half the CUs idle; and, with NT = 8 N-tiles per wave, the 128-channel
+// blocks of levels 0-1: one staged halo feeds twice the MFMAs).  pieces pc = tid + T j; the
+// wave-instructions wholly past the halo's 2 Halo pieces aim at a 1 KiB dummy slot
+// (out-of-range source: no memory traffic) so every wave issues the same count; a buffer
+// holds rows up to the last real piece.  Epilogue slice rows: NT x 16 channels bf16 + 16 B
+// (conflict-free 2-B writes), 16 rows (one M-tile) per wave.
+template <int BD, int NT = 4> struct B6G {
   static constexpr int T = BD * 64;
+  static constexpr int CO = NT * 16;                                    // channels per workgroup
   static constexpr int Halo = (BD + 2) * kBgHH * kBgHW;                 // rows x 32 B
   static constexpr int Pieces = (2 * Halo + T - 1) / T;                 // DMA pieces / thread
   static constexpr int Buf = (2 * Halo + 63) / 64 * 1024;
+  static constexpr int Row = CO * 2 + 16;
+  static constexpr int Slice = 16 * Row;
+  static constexpr int EpiStores = 8 * NT / 2;                          // 16-B stores per wave and box
   static constexpr int SliceOff = 2 * Buf + kBgDummy;
-  static constexpr int RedOff = SliceOff + BD * kB6Slice;
-  static constexpr int Lds = RedOff + BD * 64 * 3 * 4 + 64 * 4;         // + bias
+  static constexpr int RedOff = SliceOff + BD * Slice;
+  static constexpr int Lds = RedOff + BD * CO * 3 * 4 + CO * 4;         // + bias
   static constexpr int BnOff = Lds;
   static constexpr int LdsBn = Lds + 2 * kBgBnMax * 4;
   static_assert(Pieces <= kB6Steps, "one piece per k-step");
@@ -2047,38 +2053,47 @@ template <int BD> struct B6G {
   static_assert(LdsBn <= 160 * 1024, "LDS");
 };
 static_assert(B6G<8>::Buf == kBgBuf && B6G<8>::Pieces == kBgPieces, "8-deep geometry");
+static_assert(B6G<8>::Row == 144 && B6G<8>::EpiStores == 16, "64-channel slice rows");
 
 // halo row offset of tap t (10 x 18 rows per plane); the zero-weight 28th tap reads tap 26's rows
 __host__ __device__ constexpr int b6_tapoff(int t) {
   return t > 26 ? b6_tapoff(26) : ((t / 9) * kBgHH + (t / 3) % 3) * kBgHW + t % 3;
 }
-// retire the hidden loads of the four B fragments of a step (and everything issued before)
+// retire the hidden loads of the B fragments of a step (and everything issued before)
 template <int N> __device__ __forceinline__ void vm_wait4(s16x8_t (&b)[4]) {
   static_assert(N >= 0 && N <= 63, "vmcnt");
   asm volatile("s_waitcnt vmcnt(%4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : "n"(N) : "memory");
 }
+template <int N> __device__ __forceinline__ void vm_wait4(s16x8_t (&b)[8]) {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7])
+               : "n"(N) : "memory");
+}
 template <int P> constexpr int b6_piece(int s) { return ((s % kB6Steps) + kB6Steps) % kB6Steps < P ? 1 : 0; }
-// vector-memory ops issued after the last of B(t)'s 4 loads by the time step t waits for it:
-// every step u issues B(u + D) (4 loads) then piece(u) (u < P)
-template <int P, int Dist> constexpr int b6_wait(int t) {
+// vector-memory ops issued after the last of B(t)'s NT loads by the time step t waits for it:
+// every step u issues B(u + D) (NT loads) then piece(u) (u < P)
+template <int P, int Dist, int NT = 4> constexpr int b6_wait(int t) {
   int n = b6_piece<P>(t - Dist);
-  for (int u = t - Dist + 1; u <= t; ++u) n += 4 + b6_piece<P>(u);
+  for (int u = t - Dist + 1; u <= t; ++u) n += NT + b6_piece<P>(u);
   return n;
 }
 
-template <bool BNIN = false, int BD = 8>
+template <bool BNIN = false, int BD = 8, int NT = 4>
 __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p, uint32_t x0bytes,
                                                                   uint32_t x1bytes) {
-  typedef B6G<BD> G6;
+  typedef B6G<BD, NT> G6;
+  static_assert(NT == 4 || (NT == 8 && BD == 4), "128-channel blocks: one wave per SIMD");
+  constexpr int CO = G6::CO;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int Cout = p.Cout, ncob = Cout >> 6;
+  const int Cout = p.Cout, ncob = Cout / CO;
   const int G = gridDim.x;
   const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const int cob = lg % ncob, slot = lg / ncob, nslot = G / ncob;
   const int nbox = p.N * p.nbd * p.nbh * p.nbw;
-  const int co_base = cob * 64;
+  const int co_base = cob * CO;
   auto origin = [&](int box, int& n, int& d0, int& h0, int& w0) {
     int q = box;
     const int bwi = q % p.nbw; q /= p.nbw;
@@ -2137,34 +2152,41 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     __syncthreads();
   }
 
-  // B: pack16, (16-chunk c, step s) rows of Cout / 16 fragments of 1 KiB; this wave's four
-  // N-tiles are the workgroup's 64 channels: one base + immediates 0 / 1 / 2 / 3 KiB
+  // B: pack16, (16-chunk c, step s) rows of Cout / 16 fragments of 1 KiB; this wave's NT
+  // N-tiles are the workgroup's CO channels: bases off (+ 4 KiB) + immediates 0-3 KiB
   const int nchunk = p.Cin >> 4;
   const uint32_t step_bytes = (uint32_t)Cout * 64u;
   const i32x4_t wr = buffer_desc(p.w, (uint32_t)nchunk * kB6Steps * step_bytes);
-  auto load_b = [&](s16x8_t (&dst)[4], int chunk, int st, uint32_t boff) {
+  auto load_b = [&](s16x8_t (&dst)[NT], int chunk, int st, uint32_t boff) {
     const uint32_t off = boff + (uint32_t)(chunk * kB6Steps + st) * step_bytes;
-    bload16<0>(dst[0], wr, off);
-    bload16<1024>(dst[1], wr, off);
-    bload16<2048>(dst[2], wr, off);
-    bload16<3072>(dst[3], wr, off);
+#pragma unroll
+    for (int h = 0; h < NT / 4; ++h) {
+      bload16<0>(dst[4 * h + 0], wr, off + h * 4096u);
+      bload16<1024>(dst[4 * h + 1], wr, off + h * 4096u);
+      bload16<2048>(dst[4 * h + 2], wr, off + h * 4096u);
+      bload16<3072>(dst[4 * h + 3], wr, off + h * 4096u);
+    }
   };
 
-  float* red = reinterpret_cast<float*>(lds + G6::RedOff);  // [wave][64][mean, M2, n]
-  float* bls = red + BD * 64 * 3;
-  if (tid < 64) bls[tid] = p.bias ? p.bias[co_base + tid] : 0.f;
-  const bool to0 = co_base < p.cy0;
-  const long ys = to0 ? p.cy0 : Cout - p.cy0;
-  const int yc0 = to0 ? co_base : co_base - p.cy0;
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
-      to0 ? p.y0 : p.y1, (short)0, (int)(p.nvox * ys * 2), 0x00020000);
-  char* slice = lds + G6::SliceOff + wave * kB6Slice;
+  float* red = reinterpret_cast<float*>(lds + G6::RedOff);  // [wave][CO][mean, M2, n]
+  float* bls = red + BD * CO * 3;
+  if (tid < CO) bls[tid] = p.bias ? p.bias[co_base + tid] : 0.f;
+  // outputs per 64-channel half h of the block: y0 below cy0, y1 from it (the dgrad's two Up3D
+  // sources; cy0 % 64 == 0)
+  auto ydst = [&](int h, long& ys, int& yc0) {
+    const int cb = co_base + 64 * h;
+    const bool to0 = cb < p.cy0;
+    ys = to0 ? p.cy0 : Cout - p.cy0;
+    yc0 = to0 ? cb : cb - p.cy0;
+    return __builtin_amdgcn_make_buffer_rsrc(to0 ? p.y0 : p.y1, (short)0, (int)(p.nvox * ys * 2), 0x00020000);
+  };
+  char* slice = lds + G6::SliceOff + wave * G6::Slice;
   int nbdone = 0;
 
-  f32x4_t acc[8][4];
-  constexpr int kB6Dist = b6_dist<BD>();
+  f32x4_t acc[8][NT];
+  constexpr int kB6Dist = b6_dist<BD, NT>();
   static_assert(kB6Steps % (kB6Dist + 1) == 0, "B ring index must continue across chunks");
-  s16x8_t bset[kB6Dist + 1][4];
+  s16x8_t bset[kB6Dist + 1][NT];
   int box = slot;
   int n, d0, h0, w0;
   origin(box, n, d0, h0, w0);
@@ -2174,7 +2196,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
 #pragma unroll
   for (int j = 0; j < G6::Pieces; ++j) pmask |= stage_piece(n, d0, h0, w0, 0, 0, j, true);
   {
-    const uint32_t boff0 = (uint32_t)(cob * 4096 + lane * 16);
+    const uint32_t boff0 = (uint32_t)(cob * NT * 1024 + lane * 16);
 #pragma unroll
     for (int t = 0; t < kB6Dist; ++t) load_b(bset[t], 0, t, boff0);
   }
@@ -2186,7 +2208,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     const int nbx = box + nslot;
     const bool has_next = nbx < nbox;
     int nn = n, nd0 = d0, nh0 = h0, nw0 = w0;
@@ -2198,7 +2220,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
       const int sn = last ? nn : n, sd = last ? nd0 : d0, sh = last ? nh0 : h0, sw = last ? nw0 : w0;
       const int schunk = last ? 0 : chunk + 1;
       const int lo = opaque(lane);
-      const uint32_t boff = (uint32_t)(cob * 4096 + lo * 16);
+      const uint32_t boff = (uint32_t)(cob * NT * 1024 + lo * 16);
       // A: this lane's halo row base -- box voxel (d = wave, h = 0, w = r16), its channel half
       // (g4 & 1) -- plus the row offset of its tap of the pair (g4 >> 1); M-tile mt = h-row mt
       // is an immediate (mt x 18 rows)
@@ -2224,25 +2246,25 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
           const uint32_t bits = stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, st, live);
           if constexpr (BNIN) pmask = (st == 0 ? 0u : pmask) | bits;
         }
-        s16x8_t (&b)[4] = bset[st % (kB6Dist + 1)];
-        constexpr int extra = (Slack && st < kB6Dist) ? kB6EpiStores : 0;
-        vm_wait4<b6_wait<G6::Pieces, kB6Dist>(st) + extra>(b);
+        s16x8_t (&b)[NT] = bset[st % (kB6Dist + 1)];
+        constexpr int extra = (Slack && st < kB6Dist) ? G6::EpiStores : 0;
+        vm_wait4<b6_wait<G6::Pieces, kB6Dist, NT>(st) + extra>(b);
         static_for<8>([&](auto mc) {
           constexpr int mt = decltype(mc)::value;
           constexpr int q = st * 8 + mt + 2;  // the fragment read now: position q (two ahead)
           if constexpr (q < kB6Steps * 8) ar[q % 3] = rd(q / 8, q % 8);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[mt][j] = mfma16(ar[(st * 8 + mt) % 3], b[j], acc[mt][j]);
+          for (int j = 0; j < NT; ++j) acc[mt][j] = mfma16(ar[(st * 8 + mt) % 3], b[j], acc[mt][j]);
         });
-        // keep the order (1 read, 4 MFMAs per M-tile) and every step's work in its step
+        // keep the order (1 read, NT MFMAs per M-tile) and every step's work in its step
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
           if (st * 8 + mt + 2 < kB6Steps * 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);  // NT MFMA
         }
         __builtin_amdgcn_sched_barrier(0);
       });
-      if (!last) vm_wait<4 * (kB6Steps - G6::Pieces)>();
+      if (!last) vm_wait<NT * (kB6Steps - G6::Pieces)>();
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (BNIN) bn_apply(buf ^ 1, schunk, pmask);
       __syncthreads();
@@ -2253,45 +2275,48 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
 
     // ---- epilogue of this box: lane (g4, r16) holds, per (M-tile mt, N-tile j), voxels w =
     // 4 g4 + i (i < 4) of h-row mt, channel 16 j + r16.  One M-tile at a time through the wave's
-    // own slice (16 rows of 144 B): + bias, bf16; read back as whole 128-B rows (2 x 16 B per
-    // lane), 16-B stores.  BatchNorm moments shifted by K (the running mean; the bias before
-    // the first box), per channel over the wave's 128 voxels, Chan-merged per (wave, channel).
+    // own slice (16 rows of Row B): + bias, bf16; read back as whole 128-B half rows (NT / 2 x
+    // 16 B per lane, each store instruction inside one 64-channel half), 16-B stores.
+    // BatchNorm moments shifted by K (the running mean; the bias before the first box), per
+    // channel over the wave's 128 voxels, Chan-merged per (wave, channel).
     const int lane_o = opaque(lane);
     const int rr = lane_o & 15, gg = lane_o >> 4;
     const long plane = (long)p.H * p.W;
     const long vbase = (((long)n * p.D + d0 + wave) * p.H + h0) * p.W + w0;
     const bool relu = p.accumulate & PCMS_CONV_RELU;
-    float bias_j[4], K0[4], c0s[4], S1[4], S2[4];
+    float bias_j[NT], K0[NT], S1[NT], S2[NT];
     const float rn = (float)nbdone * 128.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NT; ++j) {
       bias_j[j] = bls[16 * j + rr];
-      K0[j] = nbdone ? red[(wave * 64 + 16 * j + rr) * 3] : bias_j[j];
-      c0s[j] = bias_j[j] - K0[j];
+      K0[j] = nbdone ? red[(wave * CO + 16 * j + rr) * 3] : bias_j[j];
       S1[j] = 0.f;
       S2[j] = 0.f;
     }
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v0 = acc[mt][j][i];
-          *reinterpret_cast<bf16_t*>(slice + (4 * gg + i) * kB6Row + (16 * j + rr) * 2) =
+          *reinterpret_cast<bf16_t*>(slice + (4 * gg + i) * G6::Row + (16 * j + rr) * 2) =
               f2bf(relu ? fmaxf(v0 + bias_j[j], 0.f) : v0 + bias_j[j]);
-          const float e0 = v0 + c0s[j];
+          const float e0 = v0 + (bias_j[j] - K0[j]);
           S1[j] += e0;
           S2[j] = fmaf(e0, e0, S2[j]);
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int q = lane_o + 64 * k, vw = q >> 3, c16 = q & 7;
-        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(slice + vw * kB6Row + c16 * 16);
+      for (int k = 0; k < NT / 2; ++k) {
+        const int h = k >> 1, vw = ((k & 1) * 64 + lane_o) >> 3, c8 = lane_o & 7;
+        long ys;
+        int yc0;
+        const auto yr = ydst(h, ys, yc0);
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(slice + vw * G6::Row + (h * 8 + c8) * 16);
         const long vox = vbase + (long)mt * p.W + vw;
         if constexpr ((BG_ABL & 2) == 0)
-          __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c16 * 8) * 2), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c8 * 8) * 2), 0, 0);
         else
           asm volatile("" ::"v"(v), "v"((int)vox));
       }
@@ -2301,7 +2326,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
       constexpr float nb = 128.f;  // voxels per wave and box
       const float nnew = rn + nb;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NT; ++j) {
         float s1 = S1[j], s2 = S2[j];
         s1 += __shfl_xor(s1, 16, 64);
         s2 += __shfl_xor(s2, 16, 64);
@@ -2309,7 +2334,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
         s2 += __shfl_xor(s2, 32, 64);
         const float mbox = K0[j] + s1 / nb;
         const float m2b = fmaxf(s2 - s1 * s1 / nb, 0.f);
-        float* rme = red + (wave * 64 + 16 * j + rr) * 3;
+        float* rme = red + (wave * CO + 16 * j + rr) * 3;
         const float rmean = nbdone ? rme[0] : 0.f, rm2 = nbdone ? rme[1] : 0.f;
         const float delta = mbox - rmean;
         if (gg == 0) {
@@ -2327,20 +2352,20 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
 
   if (!p.stats) return;
   __syncthreads();
-  if (tid < 64) {
+  if (tid < CO) {
     float S = 0.f, Nn = 0.f;
 #pragma unroll
     for (int w = 0; w < BD; ++w) {
-      S += red[(w * 64 + tid) * 3] * red[(w * 64 + tid) * 3 + 2];
-      Nn += red[(w * 64 + tid) * 3 + 2];
+      S += red[(w * CO + tid) * 3] * red[(w * CO + tid) * 3 + 2];
+      Nn += red[(w * CO + tid) * 3 + 2];
     }
     const float m = S / Nn;
     float M2 = 0.f;
 #pragma unroll
     for (int w = 0; w < BD; ++w) {
-      const float c = red[(w * 64 + tid) * 3 + 2];
-      const float d = red[(w * 64 + tid) * 3] - m;
-      M2 += red[(w * 64 + tid) * 3 + 1] + c * d * d;
+      const float c = red[(w * CO + tid) * 3 + 2];
+      const float d = red[(w * CO + tid) * 3] - m;
+      M2 += red[(w * CO + tid) * 3 + 1] + c * d * d;
     }
     float* st = p.stats + ((long)slot * Cout + co_base + tid) * 2;
     st[0] = S;
@@ -2586,30 +2611,45 @@ static bool b16_shape_ok(int bd, int N, int D, int H, int W, int c0, int c1) {
   return D % bd == 0 && H % 8 == 0 && W % 16 == 0 && c0 % 16 == 0 && c1 % 16 == 0 && c0 >= 16 &&
          nvox < (1L << 30) && nvox * std::max(c0, c1) * 2 < (long)kOOB;
 }
-static int b16_depth(int N, int D, int H, int W, int c0, int c1, int Cout) {
-  if (Cout % 64 || (long)N * D * H * W * Cout * 2 >= (long)kOOB) return 0;
-  const long nb8 = (long)N * (D / 8) * (H / 8) * (W / 16), ncob = Cout / 64;
-  if (big_fwd_ok(PCMS_BF16, N, D, H, W, c0, c1)) return 8;
-  if (b16_shape_ok(8, N, D, H, W, c0, c1) && nb8 * ncob >= g_big_min_boxes) return 8;
-  const long nb4 = (long)N * (D / 4) * (H / 8) * (W / 16);
-  if (b16_shape_ok(4, N, D, H, W, c0, c1) && nb4 * ncob >= g_big_min_boxes) return 4;
-  return 0;
+struct B16Cfg { int bd, nt; };
+// 128-channel blocks on 4-deep boxes (B6G<4, 8>) where Cout allows and they fill the CUs (A/B
+// switch pcms_conv3_b16_nt8; off: 12-20 % slower than 64-channel blocks on 8-deep boxes at
+// every level-0/1 shape despite a 5-12 % higher clock -- one wave per SIMD with 64 MFMAs per
+// k-step cannot hide its B fetches, profiles/r5_nt8_ab.txt)
+static int g_b16_nt8 = 0;
+static B16Cfg b16_config(int N, int D, int H, int W, int c0, int c1, int Cout) {
+  if (Cout % 64 || (long)N * D * H * W * Cout * 2 >= (long)kOOB) return {0, 0};
+  const long nb8 = (long)N * (D / 8) * (H / 8) * (W / 16), nb4 = (long)N * (D / 4) * (H / 8) * (W / 16);
+  const long ncob = Cout / 64;
+  if (g_b16_nt8 && Cout % 128 == 0 && b16_shape_ok(4, N, D, H, W, c0, c1) && nb4 * (Cout / 128) >= g_big_min_boxes)
+    return {4, 8};
+  if (big_fwd_ok(PCMS_BF16, N, D, H, W, c0, c1)) return {8, 4};
+  if (b16_shape_ok(8, N, D, H, W, c0, c1) && nb8 * ncob >= g_big_min_boxes) return {8, 4};
+  if (b16_shape_ok(4, N, D, H, W, c0, c1) && nb4 * ncob >= g_big_min_boxes) return {4, 4};
+  return {0, 0};
 }
-static int b16_slots(int bd, int N, int D, int H, int W, int Cout) {
-  const int nbox = N * (D / bd) * (H / 8) * (W / 16);
+static int b16_slots(B16Cfg c, int N, int D, int H, int W, int Cout) {
+  const int nbox = N * (D / c.bd) * (H / 8) * (W / 16);
   const int G = g_big_max_wgs > 0 ? g_big_max_wgs : device_cus();
-  return std::max(1, std::min(nbox, G / (Cout / 64)));
+  return std::max(1, std::min(nbox, G / (Cout / (16 * c.nt))));
 }
 
 // 1 when pcms_conv3_fwd16 runs this conv (bf16, one split); the engine keeps a pack16 for
 // such convs
 int pcms_conv3_big16_ok(int N, int D, int H, int W, int c0, int c1, int Cout) {
-  return b16_depth(N, D, H, W, c0, c1, Cout) ? 1 : 0;
+  return b16_config(N, D, H, W, c0, c1, Cout).bd ? 1 : 0;
+}
+// 128-channel blocks of the 16x16x32 kernel on (1) or off (0); v < 0 queries; returns the
+// previous setting (set before any workspace query: it changes pcms_conv3_fwd16_rows)
+int pcms_conv3_b16_nt8(int v) {
+  const int old = g_b16_nt8;
+  if (v >= 0) g_b16_nt8 = v;
+  return old;
 }
 // BatchNorm partial rows pcms_conv3_fwd16 writes for this conv (0: not a fwd16 shape)
 int pcms_conv3_fwd16_rows(int N, int D, int H, int W, int c0, int c1, int Cout) {
-  const int bd = b16_depth(N, D, H, W, c0, c1, Cout);
-  return bd ? b16_slots(bd, N, D, H, W, Cout) : 0;
+  const B16Cfg c = b16_config(N, D, H, W, c0, c1, Cout);
+  return c.bd ? b16_slots(c, N, D, H, W, Cout) : 0;
 }
 int pcms_conv3_pack16_elems(int J, int Kdim) { return (J % 16 || Kdim % 16) ? -1 : (Kdim / 16) * kB6Steps * J * 32; }
 // pack16 forms (fwd16: rows = Cout, k = Cin; dgrad16: rows = Cin, k = Cout, taps mirrored) of the
@@ -2627,7 +2667,8 @@ int pcms_conv3_pack16(const long long* table, int ntab, int ntiles, hipStream_t 
 int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float* isc, const float* ish,
                      const void* wpack16, const float* bias, void* y0, void* y1, int cy0, float* stats, int flags,
                      int N, int D, int H, int W, int Cout, hipStream_t s) {
-  const int bd = b16_depth(N, D, H, W, c0, c1, Cout);
+  const B16Cfg cf = b16_config(N, D, H, W, c0, c1, Cout);
+  const int bd = cf.bd;
   if (!bd || (c1 > 0 && x1 == nullptr)) return -5;
   if (isc && (c1 != 0 || c0 > kBgBnMax || !ish)) return -1;
   if (stats && flags) return -6;
@@ -2643,12 +2684,15 @@ int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float
   p.nvox = (long)N * D * H * W;
   p.nchunk = p.Cin / 16; p.chunks_per_split = p.nchunk;
   p.nbd = D / bd; p.nbh = H / 8; p.nbw = W / 16;
-  const int nslot = b16_slots(bd, N, D, H, W, Cout);
-  auto kern = bd == 8 ? (isc ? conv3_fwd_b16_kernel<true, 8> : conv3_fwd_b16_kernel<false, 8>)
-                      : (isc ? conv3_fwd_b16_kernel<true, 4> : conv3_fwd_b16_kernel<false, 4>);
-  const int ldsb = bd == 8 ? (isc ? B6G<8>::LdsBn : B6G<8>::Lds) : (isc ? B6G<4>::LdsBn : B6G<4>::Lds);
+  const int nslot = b16_slots(cf, N, D, H, W, Cout);
+  auto kern = cf.nt == 8 ? (isc ? conv3_fwd_b16_kernel<true, 4, 8> : conv3_fwd_b16_kernel<false, 4, 8>)
+              : bd == 8  ? (isc ? conv3_fwd_b16_kernel<true, 8> : conv3_fwd_b16_kernel<false, 8>)
+                         : (isc ? conv3_fwd_b16_kernel<true, 4> : conv3_fwd_b16_kernel<false, 4>);
+  const int ldsb = cf.nt == 8 ? (isc ? B6G<4, 8>::LdsBn : B6G<4, 8>::Lds)
+                   : bd == 8  ? (isc ? B6G<8>::LdsBn : B6G<8>::Lds)
+                              : (isc ? B6G<4>::LdsBn : B6G<4>::Lds);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldsb);
-  hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64)), dim3(bd * 64), ldsb, s, p,
+  hipLaunchKernelGGL(kern, dim3(nslot * (Cout / (16 * cf.nt))), dim3(bd * 64), ldsb, s, p,
                      (uint32_t)(p.nvox * c0 * 2), (uint32_t)(p.nvox * c1 * 2));
   PCMS_CHECK_LAUNCH();
 }

@@ -1078,6 +1078,7 @@ def _pack16(L, w, cout, cin, fwd=True, dgrad=True):
     return f, d
 
 
+@pytest.mark.parametrize("nt8", [1, 0])
 @pytest.mark.parametrize("N,c0,c1,cout,cy0,S,wgs", [
     (1, 64, 0, 64, 64, (8, 8, 16), 0),         # one box
     (2, 32, 32, 128, 64, (16, 8, 32), 0),      # dual source, two-pointer output, 2 channel blocks
@@ -1086,14 +1087,17 @@ def _pack16(L, w, cout, cin, fwd=True, dgrad=True):
     (2, 64, 0, 64, 64, (16, 16, 32), 3),       # persistent: 3 slots walk 16 boxes (6, 5, 5)
     (2, 32, 32, 128, 64, (16, 16, 32), 4),     # 2 slots x 2 channel blocks, 8 boxes each
     (1, 64, 64, 64, 64, (16, 24, 16), 5),      # dual source, 5 slots over 6 boxes (2 + 1 x 4)
+    (1, 64, 0, 256, 128, (8, 16, 16), 3),      # 128-channel blocks (nt8): 2 blocks, split output
 ])
-def test_conv3_fwd16_big_box(N, c0, c1, cout, cy0, S, wgs):
+def test_conv3_fwd16_big_box(nt8, N, c0, c1, cout, cy0, S, wgs):
     """The 16x16x32 big-box kernel (pcms_conv3_fwd16, tap pairs x 16 channels per MFMA, the
     pack16 weights) on the big-box cases: vs torch conv3d in fp64 on the same bf16 inputs, the
-    BN partial moments, and within bf16 rounding of the 32x32x16 big-box kernel's output."""
+    BN partial moments, and within bf16 rounding of the 32x32x16 big-box kernel's output.
+    nt8 1: 128-channel outputs run as 128-channel blocks on 4-deep boxes (B6G<4, 8>)."""
     L = _lib()
     old = L.query("pcms_conv3_big_min_boxes", 1)
     old_w = L.query("pcms_conv3_big_max_wgs", wgs)
+    old_nt = L.query("pcms_conv3_b16_nt8", nt8)
     try:
         dt = torch.bfloat16
         g = torch.Generator().manual_seed(c0 + 5 * c1 + cout)
@@ -1108,9 +1112,10 @@ def test_conv3_fwd16_big_box(N, c0, c1, cout, cy0, S, wgs):
         wp = torch.empty(L.query("pcms_conv3_pack_elems", 1, cout, cin), dtype=dt, device=DEV)
         L.call("pcms_conv3_pack", 1, w.to(DEV), wp, cout, cin, 0)
         nvox = N * S[0] * S[1] * S[2]
-        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, c0, c1, cout)
         outs = []
         for k16 in (True, False):
+            rows = L.query("pcms_conv3_fwd16_rows" if k16 else "pcms_conv3_fwd_rows", *([] if k16 else [1]), N, *S,
+                           c0, c1, cout)
             y0 = torch.full((N, *S, cy0), float("nan"), dtype=dt, device=DEV)
             y1 = torch.full((N, *S, max(cout - cy0, 8)), float("nan"), dtype=dt, device=DEV)
             stats = torch.full((rows * (cout * 2 + 1),), float("nan"), device=DEV)
@@ -1135,6 +1140,7 @@ def test_conv3_fwd16_big_box(N, c0, c1, cout, cy0, S, wgs):
     finally:
         L.query("pcms_conv3_big_min_boxes", old)
         L.query("pcms_conv3_big_max_wgs", old_w)
+        L.query("pcms_conv3_b16_nt8", old_nt)
 
 
 @pytest.mark.parametrize("N,c0,c1,cout,cy0,S,wgs", [
@@ -1209,15 +1215,17 @@ def test_conv3_fwd16_four_deep(N, c0, c1, cout, cy0, S, wgs):
         L.query("pcms_conv3_big_max_wgs", old_w)
 
 
+@pytest.mark.parametrize("nt8", [1, 0])
 @pytest.mark.parametrize("N,cout,cin,S,wgs", [(2, 64, 64, (16, 16, 32), 0), (1, 64, 128, (16, 16, 16), 3),
-                                              (2, 128, 64, (8, 16, 32), 0)])
-def test_conv3_dgrad16(N, cout, cin, S, wgs):
+                                              (2, 128, 64, (8, 16, 32), 0), (1, 64, 256, (8, 8, 16), 0)])
+def test_conv3_dgrad16(nt8, N, cout, cin, S, wgs):
     """The dgrad direction on the 16x16x32 kernel (pack16 dgrad form: rows Cin, k Cout, taps
     mirrored): dx = conv(dy, w transposed and flipped) vs fp64, and the split output of a
     dgrad into the two Up3D sources (cy0)."""
     L = _lib()
     old = L.query("pcms_conv3_big_min_boxes", 1)
     old_w = L.query("pcms_conv3_big_max_wgs", wgs)
+    old_nt = L.query("pcms_conv3_b16_nt8", nt8)
     try:
         dt = torch.bfloat16
         g = torch.Generator().manual_seed(cout * 7 + cin)
@@ -1238,9 +1246,10 @@ def test_conv3_dgrad16(N, cout, cin, S, wgs):
     finally:
         L.query("pcms_conv3_big_min_boxes", old)
         L.query("pcms_conv3_big_max_wgs", old_w)
+        L.query("pcms_conv3_b16_nt8", old_nt)
 
 
-@pytest.mark.parametrize("N,S,C,wgs", [(2, (32, 32, 32), 64, 0), (1, (32, 32, 32), 128, 24)])
+@pytest.mark.parametrize("N,S,C,wgs", [(2, (32, 32, 32), 64, 0), (1, (32, 32, 32), 128, 24), (1, (16, 16, 32), 128, 0)])
 def test_bnin_conv16_bit_identical(N, S, C, wgs):
     """pcms_conv3_fwd16 with the input BatchNorm + ReLU in its staging (isc / ish) against the
     same kernel on the stored a1 = pcms_bn_relu(y1): bit-identical outputs and BN partials;
@@ -1258,7 +1267,7 @@ def test_bnin_conv16_bit_identical(N, S, C, wgs):
         w = (torch.randn(C, C, 27, generator=g) * 0.05)
         w16, _ = _pack16(L, w, C, C, dgrad=False)
         bias = torch.randn(C, generator=g).to(DEV)
-        rows = L.query("pcms_conv3_fwd_rows", 1, N, *S, C, 0, C)
+        rows = L.query("pcms_conv3_fwd16_rows", N, *S, C, 0, C)
         a1 = torch.empty_like(y1)
         L.call("pcms_bn_relu", 1, y1, a1, sc, sh, C, nvox)
         out = []

@@ -17,15 +17,21 @@ CSRC = os.path.join(REPO, "prostate-cancer-multimodal-segmentation_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 KERNELS = {
-    "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_b16_kernelILb0ELi8E", "conv3_fwd_b16_kernelILb1ELi8E",
-                  "conv3_fwd_b16_kernelILb0ELi4E", "conv3_fwd_b16_kernelILb1ELi4E", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E"],
+    "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_b16_kernelILb0ELi8ELi4E", "conv3_fwd_b16_kernelILb1ELi8ELi4E",
+                  "conv3_fwd_b16_kernelILb0ELi4ELi4E", "conv3_fwd_b16_kernelILb1ELi4ELi4E",
+                  "conv3_fwd_b16_kernelILb0ELi4ELi8E", "conv3_fwd_b16_kernelILb1ELi4ELi8E", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E"],
     "stem.hip": ["stem_fwd_direct_kernelILi2ELi3E", "stem_fwd_direct_kernelILi3ELi2E", "stem_wgrad_stream_kernel"],
     "convt.hip": ["convt_lds_kernel", "convt_fwd_stream_kernel"],
     # streaming fusions: a spill there would add scratch traffic to an HBM-bound pass
     "ops.hip": ["maxpool_bwd_bn_kernel", "head_bwd_kernel", "head_bn_apply_kernel", "bn_relu_pool_kernel"],
 }
 # (the 4-deep 16x16x32 conv runs one 256-thread workgroup per CU: one wave per SIMD)
-VGPR_BUDGET = {"convt_lds_kernel": 128, "conv3_fwd_b16_kernelILb0ELi4E": 512, "conv3_fwd_b16_kernelILb1ELi4E": 512}
+VGPR_BUDGET = {"convt_lds_kernel": 128, "conv3_fwd_b16_kernelILb0ELi4ELi4E": 512, "conv3_fwd_b16_kernelILb1ELi4ELi4E": 512,
+               "conv3_fwd_b16_kernelILb0ELi4ELi8E": 512, "conv3_fwd_b16_kernelILb1ELi4ELi8E": 512}
+# scratch allowed where a kernel's only spills sit outside its vmcnt-counted pipeline (checked
+# in the device assembly when the budget was set): the 128-channel 16x16x32 conv keeps 256
+# accumulators live and reloads one value in its prologue / final BN reduction
+SCRATCH_BUDGET = {"conv3_fwd_b16_kernelILb0ELi4ELi8E": 8, "conv3_fwd_b16_kernelILb1ELi4ELi8E": 24}
 
 
 def _meta(src, tmp):
@@ -51,6 +57,6 @@ def test_pipelined_kernels_do_not_spill(src, tmp_path):
         hits = [(n, v) for n, v in meta.items() if key in n]
         assert hits, f"{key} not found in {src}"
         for name, (priv, vgpr) in hits:
-            assert priv == 0, f"{name}: {priv} B of scratch (spills) at {vgpr} VGPRs"
+            assert priv <= SCRATCH_BUDGET.get(key, 0), f"{name}: {priv} B of scratch (spills) at {vgpr} VGPRs"
             budget = VGPR_BUDGET.get(key, 256)
             assert vgpr <= budget, f"{name}: {vgpr} VGPRs (budget {budget}: its waves per SIMD)"
