@@ -126,6 +126,12 @@ int pcms_conv3_fwd16_rows(int N, int D, int H, int W, int c0, int c1, int Cout);
  * channels) where Cout % 128 == 0 and they fill the CUs: 1 or 0 (default); v < 0 queries;
  * returns the previous setting (set before any workspace query)                          */
 int pcms_conv3_b16_nt8(int v);
+/* Level 3 (rows of 8 w): the same kernel on 4 d x 16 h x 8 w boxes, split over K into fp32
+ * partial rows yacc[split][vox][Cout] (no bias / statistics; pcms_split_epilogue sums them in
+ * split order).  _split_ok: the split count it uses for this conv, 0 where it does not apply. */
+int pcms_conv3_fwd16_split_ok(int N, int D, int H, int W, int c0, int c1, int Cout);
+int pcms_conv3_fwd16_split(const void* x0, int c0, const void* x1, int c1, const void* wpack16, float* yacc,
+                           int N, int D, int H, int W, int Cout, int splits, hipStream_t s);
 int pcms_conv3_pack16_elems(int J, int Kdim);
 int pcms_conv3_pack16(const long long* table, int ntab, int ntiles, hipStream_t s);
 int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float* isc, const float* ish,

@@ -39,6 +39,8 @@ SIGNATURES = {
     "pcms_conv3_big16_ok": "iiiiiii",
     "pcms_conv3_fwd16_rows": "iiiiiii",
     "pcms_conv3_b16_nt8": "i",
+    "pcms_conv3_fwd16_split_ok": "iiiiiii",
+    "pcms_conv3_fwd16_split": "pipippiiiiiis",
     "pcms_conv3_pack16_elems": "ii",
     "pcms_conv3_pack16": "piis",
     "pcms_conv3_fwd16": "pipippppppipiiiiiis",

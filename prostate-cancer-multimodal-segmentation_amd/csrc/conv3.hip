@@ -2048,6 +2048,11 @@ template <int BD, int NT = 4> struct B6G {
   static constexpr int Lds = RedOff + BD * CO * 3 * 4 + CO * 4;         // + bias
   static constexpr int BnOff = Lds;
   static constexpr int LdsBn = Lds + 2 * kBgBnMax * 4;
+  // split-K form (fp32 partial rows): its own slice of 16 rows x CO fp32 (+ 16 B) per wave
+  static constexpr int Row32 = CO * 4 + 16;
+  static constexpr int LdsSplit = SliceOff + BD * 16 * Row32;
+  static constexpr int EpiStores32 = 8 * CO / 16;                       // 16-B stores per wave and box
+  static_assert(LdsSplit <= 160 * 1024, "LDS");
   static_assert(Pieces <= kB6Steps, "one piece per k-step");
   static_assert((Pieces - 2) * T + (BD - 1) * 64 < 2 * Halo, "dummy pieces in the last round only");
   static_assert(LdsBn <= 160 * 1024, "LDS");
@@ -2055,9 +2060,17 @@ template <int BD, int NT = 4> struct B6G {
 static_assert(B6G<8>::Buf == kBgBuf && B6G<8>::Pieces == kBgPieces, "8-deep geometry");
 static_assert(B6G<8>::Row == 144 && B6G<8>::EpiStores == 16, "64-channel slice rows");
 
-// halo row offset of tap t (10 x 18 rows per plane); the zero-weight 28th tap reads tap 26's rows
-__host__ __device__ constexpr int b6_tapoff(int t) {
-  return t > 26 ? b6_tapoff(26) : ((t / 9) * kBgHH + (t / 3) % 3) * kBgHW + t % 3;
+// box w width WB: 16 (levels 0-2: an M-tile is one h-row of 16 w) or 8 (level 3: an M-tile is
+// two h-rows of 8 w); the box is BD d-planes x (128 / WB) h x WB w, its halo plane HH x HW
+// rows (10 x 18 or 18 x 10: 180 rows either way)
+template <int WB> struct B6W {
+  static constexpr int BH = 128 / WB, HH = BH + 2, HW = WB + 2;
+  static constexpr int MTR = (16 / WB) * HW;  // halo rows between M-tiles
+};
+static_assert(B6W<16>::HH == kBgHH && B6W<16>::HW == kBgHW && B6W<8>::HH * B6W<8>::HW == kBgHH * kBgHW, "halo");
+// halo row offset of tap t; the zero-weight 28th tap reads tap 26's rows
+template <int WB = 16> __host__ __device__ constexpr int b6_tapoff(int t) {
+  return t > 26 ? b6_tapoff<WB>(26) : ((t / 9) * B6W<WB>::HH + (t / 3) % 3) * B6W<WB>::HW + t % 3;
 }
 // retire the hidden loads of the B fragments of a step (and everything issued before)
 template <int N> __device__ __forceinline__ void vm_wait4(s16x8_t (&b)[4]) {
@@ -2079,11 +2092,16 @@ template <int P, int Dist, int NT = 4> constexpr int b6_wait(int t) {
   return n;
 }
 
-template <bool BNIN = false, int BD = 8, int NT = 4>
+// WB: box w width (B6W).  SPLIT (level 3): the workgroups of a (slot, co block) cover 1 / nsplit of
+// the input chunks each (p.chunks_per_split) and write fp32 partial rows p.yacc[split][vox][co]
+// (no bias / statistics: pcms_split_epilogue sums the splits in a fixed order)
+template <bool BNIN = false, int BD = 8, int NT = 4, int WB = 16, bool SPLIT = false>
 __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p, uint32_t x0bytes,
                                                                   uint32_t x1bytes) {
   typedef B6G<BD, NT> G6;
+  typedef B6W<WB> GW;
   static_assert(NT == 4 || (NT == 8 && BD == 4), "128-channel blocks: one wave per SIMD");
+  static_assert(!SPLIT || (!BNIN && NT == 4), "split-K form: plain 64-channel blocks");
   constexpr int CO = G6::CO;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2091,7 +2109,9 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
   const int Cout = p.Cout, ncob = Cout / CO;
   const int G = gridDim.x;
   const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-  const int cob = lg % ncob, slot = lg / ncob, nslot = G / ncob;
+  const int nsplit = SPLIT ? p.nchunk / p.chunks_per_split : 1;
+  const int cob = lg % ncob, split = SPLIT ? (lg / ncob) % nsplit : 0;
+  const int slot = lg / ncob / nsplit, nslot = G / ncob / nsplit;
   const int nbox = p.N * p.nbd * p.nbh * p.nbw;
   const int co_base = cob * CO;
   auto origin = [&](int box, int& n, int& d0, int& h0, int& w0) {
@@ -2100,7 +2120,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     const int bhi = q % p.nbh; q /= p.nbh;
     const int bdi = q % p.nbd;
     n = q / p.nbd;
-    d0 = bdi * BD; h0 = bhi * 8; w0 = bwi * 16;
+    d0 = bdi * BD; h0 = bhi * GW::BH; w0 = bwi * WB;
   };
   const i32x4_t xr0 = buffer_desc(p.x0, x0bytes);
   const i32x4_t xr1 = buffer_desc(p.x1 ? p.x1 : p.x0, x1bytes);
@@ -2114,7 +2134,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     const uint32_t cofs = first ? c : c - p.c0;
     const int pc = opaque(tid) + j * G6::T;
     const int hv = pc >> 1;
-    const int hw_ = hv % kBgHW, t_ = hv / kBgHW, hh_ = t_ % kBgHH, hd_ = t_ / kBgHH;
+    const int hw_ = hv % GW::HW, t_ = hv / GW::HW, hh_ = t_ % GW::HH, hd_ = t_ / GW::HH;
     const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
     uint32_t voff = kOOB;
     if (live && hv < G6::Halo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
@@ -2154,7 +2174,8 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
 
   // B: pack16, (16-chunk c, step s) rows of Cout / 16 fragments of 1 KiB; this wave's NT
   // N-tiles are the workgroup's CO channels: bases off (+ 4 KiB) + immediates 0-3 KiB
-  const int nchunk = p.Cin >> 4;
+  const int nchunk = p.Cin >> 4;  // (the pack's chunk count; SPLIT: this split's [cbeg, cend))
+  const int cbeg = split * (SPLIT ? p.chunks_per_split : 0), cend = SPLIT ? cbeg + p.chunks_per_split : nchunk;
   const uint32_t step_bytes = (uint32_t)Cout * 64u;
   const i32x4_t wr = buffer_desc(p.w, (uint32_t)nchunk * kB6Steps * step_bytes);
   auto load_b = [&](s16x8_t (&dst)[NT], int chunk, int st, uint32_t boff) {
@@ -2180,7 +2201,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     yc0 = to0 ? cb : cb - p.cy0;
     return __builtin_amdgcn_make_buffer_rsrc(to0 ? p.y0 : p.y1, (short)0, (int)(p.nvox * ys * 2), 0x00020000);
   };
-  char* slice = lds + G6::SliceOff + wave * G6::Slice;
+  char* slice = lds + G6::SliceOff + wave * (SPLIT ? 16 * G6::Row32 : G6::Slice);
   int nbdone = 0;
 
   f32x4_t acc[8][NT];
@@ -2190,15 +2211,15 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
   int box = slot;
   int n, d0, h0, w0;
   origin(box, n, d0, h0, w0);
-  if (nchunk <= 4)
+  if (cend - cbeg <= 4)
     for (int i = 0; i < 2 * (slot & 3); ++i) __builtin_amdgcn_s_sleep(127);
   uint32_t pmask = 0;
 #pragma unroll
-  for (int j = 0; j < G6::Pieces; ++j) pmask |= stage_piece(n, d0, h0, w0, 0, 0, j, true);
+  for (int j = 0; j < G6::Pieces; ++j) pmask |= stage_piece(n, d0, h0, w0, cbeg, 0, j, true);
   {
     const uint32_t boff0 = (uint32_t)(cob * NT * 1024 + lane * 16);
 #pragma unroll
-    for (int t = 0; t < kB6Dist; ++t) load_b(bset[t], 0, t, boff0);
+    for (int t = 0; t < kB6Dist; ++t) load_b(bset[t], cbeg, t, boff0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (BNIN) bn_apply(0, 0, pmask);
@@ -2215,24 +2236,25 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     if (has_next) origin(nbx, nn, nd0, nh0, nw0);
     auto run_chunk = [&](int chunk, auto slack_tag) {
       constexpr bool Slack = decltype(slack_tag)::value;
-      const bool last = chunk + 1 == nchunk;
+      const bool last = chunk + 1 == cend;
       const bool live = !last || has_next;
       const int sn = last ? nn : n, sd = last ? nd0 : d0, sh = last ? nh0 : h0, sw = last ? nw0 : w0;
-      const int schunk = last ? 0 : chunk + 1;
+      const int schunk = last ? cbeg : chunk + 1;
       const int lo = opaque(lane);
       const uint32_t boff = (uint32_t)(cob * NT * 1024 + lo * 16);
       // A: this lane's halo row base -- box voxel (d = wave, h = 0, w = r16), its channel half
       // (g4 & 1) -- plus the row offset of its tap of the pair (g4 >> 1); M-tile mt = h-row mt
       // is an immediate (mt x 18 rows)
+      const int r16 = lo & 15;  // the lane's voxel of an M-tile: h-row r16 / WB, w r16 % WB
       const uint32_t abase = lds0 + buf * G6::Buf +
-                             (uint32_t)(((wave * kBgHH) * kBgHW + (lo & 15)) * 32 + ((lo >> 4) & 1) * 16);
+                             (uint32_t)(((wave * GW::HH + r16 / WB) * GW::HW + r16 % WB) * 32 + ((lo >> 4) & 1) * 16);
       const bool hi_tap = (lo >> 5) & 1;
       // A fragment of (step st, M-tile mt); fragments are read two M-tiles ahead of their four
       // MFMAs through a 3-register rotation, across step boundaries (a deeper, per-step rolling
       // set made the compiler double-buffer it into spills)
       auto rd = [&](int st, int mt) {
-        const uint32_t ad = abase + (uint32_t)(hi_tap ? b6_tapoff(2 * st + 1) : b6_tapoff(2 * st)) * 32u;
-        return *reinterpret_cast<const LDS_AS s16x8_t*>((const LDS_AS char*)(uintptr_t)ad + mt * kBgHW * 32);
+        const uint32_t ad = abase + (uint32_t)(hi_tap ? b6_tapoff<WB>(2 * st + 1) : b6_tapoff<WB>(2 * st)) * 32u;
+        return *reinterpret_cast<const LDS_AS s16x8_t*>((const LDS_AS char*)(uintptr_t)ad + mt * GW::MTR * 32);
       };
       s16x8_t ar[3];
       ar[0] = rd(0, 0);
@@ -2247,7 +2269,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
           if constexpr (BNIN) pmask = (st == 0 ? 0u : pmask) | bits;
         }
         s16x8_t (&b)[NT] = bset[st % (kB6Dist + 1)];
-        constexpr int extra = (Slack && st < kB6Dist) ? G6::EpiStores : 0;
+        constexpr int extra = (Slack && st < kB6Dist) ? (SPLIT ? G6::EpiStores32 : G6::EpiStores) : 0;
         vm_wait4<b6_wait<G6::Pieces, kB6Dist, NT>(st) + extra>(b);
         static_for<8>([&](auto mc) {
           constexpr int mt = decltype(mc)::value;
@@ -2270,8 +2292,39 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
       __syncthreads();
       buf ^= 1;
     };
-    run_chunk(0, std::true_type{});
-    for (int chunk = 1; chunk < nchunk; ++chunk) run_chunk(chunk, std::false_type{});
+    run_chunk(cbeg, std::true_type{});
+    for (int chunk = cbeg + 1; chunk < cend; ++chunk) run_chunk(chunk, std::false_type{});
+
+    if constexpr (SPLIT) {
+      // fp32 partial rows of this split: one M-tile at a time through the wave's slice (16 rows
+      // of CO fp32), read back as whole 256-B voxel rows, 16-B stores
+      const int lane_o = opaque(lane);
+      const int rr = lane_o & 15, gg = lane_o >> 4;
+      const long vbase = (((long)n * p.D + d0 + wave) * p.H + h0) * p.W + w0;
+      const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+          p.yacc, (short)0, (int)((long)nsplit * p.nvox * Cout * 4), 0x00020000);
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<float*>(slice + (4 * gg + i) * G6::Row32 + (16 * j + rr) * 4) = acc[mt][j][i];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < CO / 16; ++k) {
+          const int q = lane_o + 64 * k, vw = q >> 4, c4 = q & 15;
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(slice + vw * G6::Row32 + c4 * 16);
+          const long vox = vbase + (long)(mt * (16 / WB) + vw / WB) * p.W + vw % WB;
+          __builtin_amdgcn_raw_buffer_store_b128(v, ar, (int)((((long)split * p.nvox + vox) * Cout + co_base + c4 * 4) * 4),
+                                                 0, 0);
+        }
+      }
+      if (!has_next) break;
+      box = nbx;
+      n = nn; d0 = nd0; h0 = nh0; w0 = nw0;
+      continue;
+    }
 
     // ---- epilogue of this box: lane (g4, r16) holds, per (M-tile mt, N-tile j), voxels w =
     // 4 g4 + i (i < 4) of h-row mt, channel 16 j + r16.  One M-tile at a time through the wave's
@@ -2314,7 +2367,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
         int yc0;
         const auto yr = ydst(h, ys, yc0);
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(slice + vw * G6::Row + (h * 8 + c8) * 16);
-        const long vox = vbase + (long)mt * p.W + vw;
+        const long vox = vbase + (long)(mt * (16 / WB) + vw / WB) * p.W + vw % WB;
         if constexpr ((BG_ABL & 2) == 0)
           __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c8 * 8) * 2), 0, 0);
         else
@@ -2350,7 +2403,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     n = nn; d0 = nd0; h0 = nh0; w0 = nw0;
   }
 
-  if (!p.stats) return;
+  if (SPLIT || !p.stats) return;
   __syncthreads();
   if (tid < CO) {
     float S = 0.f, Nn = 0.f;
@@ -2693,6 +2746,50 @@ int pcms_conv3_fwd16(const void* x0, int c0, const void* x1, int c1, const float
                               : (isc ? B6G<4>::LdsBn : B6G<4>::Lds);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldsb);
   hipLaunchKernelGGL(kern, dim3(nslot * (Cout / (16 * cf.nt))), dim3(bd * 64), ldsb, s, p,
+                     (uint32_t)(p.nvox * c0 * 2), (uint32_t)(p.nvox * c1 * 2));
+  PCMS_CHECK_LAUNCH();
+}
+
+// ---- split-K 16x16x32 form for level 3 (W = 8 rows): boxes of 4 d x 16 h x 8 w ----
+// the split count pcms_conv3_fwd16_split uses for this conv (0: not such a shape -- whole
+// 4-deep W8 boxes, fewer than 256 (box, 64-channel block) items, and a power-of-two split
+// of the 16-channel chunks that brings them to >= 256 workgroups)
+int pcms_conv3_fwd16_split_ok(int N, int D, int H, int W, int c0, int c1, int Cout) {
+  const long nvox = (long)N * D * H * W;
+  if (Cout % 64 || D % 4 || H % 16 || W % 8 || c0 % 16 || c1 % 16 || c0 < 16) return 0;
+  if (nvox >= (1L << 30) || nvox * std::max(std::max(c0, c1), Cout) * 2 >= (long)kOOB) return 0;
+  const long items = (long)N * (D / 4) * (H / 16) * (W / 8) * (Cout / 64);
+  const int nchunk = (c0 + c1) / 16;
+  if (items >= g_big_min_boxes) return 0;
+  int sp = 1;
+  while (items * sp < g_big_min_boxes && nchunk % (2 * sp) == 0) sp *= 2;
+  if (sp == 1 || (long)sp * nvox * Cout * 4 >= (long)kOOB) return 0;
+  return sp;
+}
+
+// yacc[split][vox][Cout] fp32 = this split's partial sums (no bias, no statistics; sum them
+// with pcms_split_epilogue(yacc, splits, ...)); splits = pcms_conv3_fwd16_split_ok(...), -5 if
+// that is 0
+int pcms_conv3_fwd16_split(const void* x0, int c0, const void* x1, int c1, const void* wpack16, float* yacc,
+                           int N, int D, int H, int W, int Cout, int splits, hipStream_t s) {
+  if (splits < 2 || splits != pcms_conv3_fwd16_split_ok(N, D, H, W, c0, c1, Cout) || (c1 > 0 && x1 == nullptr))
+    return -5;
+  Conv3Params p;
+  p.x0 = x0; p.x1 = x1; p.c0 = c0; p.c1 = c1;
+  p.isc = nullptr; p.ish = nullptr;
+  p.w = wpack16; p.bias = nullptr; p.y0 = nullptr; p.y1 = nullptr; p.cy0 = Cout;
+  p.yacc = yacc; p.stats = nullptr; p.accumulate = 0;
+  p.N = N; p.D = D; p.H = H; p.W = W; p.Cin = c0 + c1; p.Cout = Cout;
+  p.nvox = (long)N * D * H * W;
+  p.nchunk = p.Cin / 16; p.chunks_per_split = p.nchunk / splits;
+  p.nbd = D / 4; p.nbh = H / 16; p.nbw = W / 8;
+  const int nbox = N * p.nbd * p.nbh * p.nbw;
+  const int G = g_big_max_wgs > 0 ? g_big_max_wgs : device_cus();
+  const int nslot = std::max(1, std::min(nbox, G / ((Cout / 64) * splits)));
+  auto kern = conv3_fwd_b16_kernel<false, 4, 4, 8, true>;
+  const int ldsb = B6G<4>::LdsSplit;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldsb);
+  hipLaunchKernelGGL(kern, dim3(nslot * (Cout / 64) * splits), dim3(256), ldsb, s, p,
                      (uint32_t)(p.nvox * c0 * 2), (uint32_t)(p.nvox * c1 * 2));
   PCMS_CHECK_LAUNCH();
 }

@@ -616,6 +616,8 @@ class UNetEngine:
                     sp = self._splits(N, S[l], cin, cout, cs.code)
                     if sp > 1:
                         yacc = max(yacc, query("pcms_conv3_splits", cs.code, cin, sp) * nv[l] * cout)
+                    if self.use_b16 and self.code == BF16:  # the level-3 16x16x32 split-K form
+                        yacc = max(yacc, query("pcms_conv3_fwd16_split_ok", N, *S[l], cin, 0, cout) * nv[l] * cout)
         b["yacc"] = torch.empty(yacc, dtype=torch.float32, device=dev)
         # partial rows of the head / ConvT-bias gradient reductions (summed in a fixed order)
         red = [query("pcms_head_bwd_ws_floats", D * H * W, N, self.ncls)]
@@ -644,9 +646,11 @@ class UNetEngine:
                     if cs is self.convs[0]:
                         continue  # the stem runs on its own kernels
                     c0 = cs.cin_store - c1
-                    if query("pcms_conv3_big16_ok", N, *S[l], c0, c1, cs.cout):
+                    if query("pcms_conv3_big16_ok", N, *S[l], c0, c1, cs.cout) or \
+                            query("pcms_conv3_fwd16_split_ok", N, *S[l], c0, c1, cs.cout):
                         cs.fwd16 = torch.empty(query("pcms_conv3_pack16_elems", cs.cout, cs.cin), dtype=T, device=dev)
-                    if query("pcms_conv3_big16_ok", N, *S[l], cs.cout, 0, cs.cin):
+                    if query("pcms_conv3_big16_ok", N, *S[l], cs.cout, 0, cs.cin) or \
+                            query("pcms_conv3_fwd16_split_ok", N, *S[l], cs.cout, 0, cs.cin):
                         cs.dgrad16 = torch.empty(query("pcms_conv3_pack16_elems", cs.cin, cs.cout), dtype=T, device=dev)
         self._p16 = None
         self._dirty = True  # build the new pack16 forms before the next conv
@@ -698,10 +702,15 @@ class UNetEngine:
             with self._timed("stem_fwd"):
                 call("pcms_stem_fwd", x0, self.stem_pack, cs.mod.bias, y, st, N, S[0], S[1], S[2], self.stem_dense)
             rows = query("pcms_stem_fwd_rows", N, *S)
-        elif splits == 1 and cs.fwd16 is not None:
+        elif splits == 1 and cs.fwd16 is not None and query("pcms_conv3_big16_ok", N, *S, c0, c1, cs.cout):
             call("pcms_conv3_fwd16", x0, c0, x1, c1, None, None, cs.fwd16, cs.mod.bias, y, None, cs.cout, st, 0,
                  N, S[0], S[1], S[2], cs.cout)
             rows = query("pcms_conv3_fwd16_rows", N, *S, c0, c1, cs.cout)
+        elif cs.fwd16 is not None and (sp16 := query("pcms_conv3_fwd16_split_ok", N, *S, c0, c1, cs.cout)):
+            acc = b["yacc"]
+            call("pcms_conv3_fwd16_split", x0, c0, x1, c1, cs.fwd16, acc, N, *S, cs.cout, sp16)
+            call("pcms_split_epilogue", self.code, acc, sp16, cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox, 0)
+            rows = query("pcms_split_epilogue_rows", nvox)
         elif splits == 1:
             call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
@@ -901,12 +910,16 @@ class UNetEngine:
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
         splits = self._splits(N, S, cs.cout, cs.cin, cs.code)
-        if splits == 1 and cs.dgrad16 is not None:
+        if splits == 1 and cs.dgrad16 is not None and query("pcms_conv3_big16_ok", N, *S, cs.cout, 0, cs.cin):
             call("pcms_conv3_fwd16", gy, cs.cout, None, 0, None, None, cs.dgrad16, None, out0, out1, cy0, None, 0,
                  N, *S, cs.cin)
         elif splits == 1:
             call("pcms_conv3_fwd", cs.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  None, None, 0, N, *S, cs.cin, 1)
+        elif cs.dgrad16 is not None and (sp16 := query("pcms_conv3_fwd16_split_ok", N, *S, cs.cout, 0, cs.cin)):
+            acc = b["yacc"]
+            call("pcms_conv3_fwd16_split", gy, cs.cout, None, 0, cs.dgrad16, acc, N, *S, cs.cin, sp16)
+            call("pcms_split_epilogue", self.code, acc, sp16, None, out0, out1, cy0, None, cs.cin, nvox, 0)
         else:
             acc = b["yacc"]
             call("pcms_conv3_fwd", cs.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,

@@ -1215,6 +1215,58 @@ def test_conv3_fwd16_four_deep(N, c0, c1, cout, cy0, S, wgs):
         L.query("pcms_conv3_big_max_wgs", old_w)
 
 
+@pytest.mark.parametrize("N,c0,c1,cout,S", [
+    (2, 64, 0, 128, (8, 16, 8)),       # 4 boxes x 2 channel blocks, 4 splits of 1 chunk
+    (2, 128, 128, 128, (4, 16, 8)),    # dual source (the chunks of a split may span both)
+    (1, 256, 0, 64, (16, 32, 16)),     # 16 boxes x 1 channel block, 16 chunks in 16 splits
+])
+def test_conv3_fwd16_split(N, c0, c1, cout, S):
+    """The level-3 split-K form of the 16x16x32 kernel (4 d x 16 h x 8 w boxes, fp32 partial
+    rows per split) summed by pcms_split_epilogue: bf16 output and BN moments vs torch conv3d
+    in fp64 on the same bf16 inputs; and the dgrad direction (dgrad pack16, split output)."""
+    L = _lib()
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(5 * c0 + c1 + cout)
+    cin = c0 + c1
+    x0 = torch.randn(N, c0, *S, generator=g).to(dt)
+    x1 = torch.randn(N, c1, *S, generator=g).to(dt)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+    b = torch.randn(cout, generator=g)
+    sp = L.query("pcms_conv3_fwd16_split_ok", N, *S, c0, c1, cout)
+    assert sp >= 2
+    w16, d16 = _pack16(L, w, cout, cin)
+    nvox = N * S[0] * S[1] * S[2]
+    acc = torch.full((sp * nvox * cout,), float("nan"), device=DEV)
+    L.call("pcms_conv3_fwd16_split", ndhwc(x0).to(DEV), c0, ndhwc(x1).to(DEV) if c1 else None, c1, w16, acc,
+           N, *S, cout, sp)
+    y = torch.empty(N, *S, cout, dtype=dt, device=DEV)
+    rows = L.query("pcms_split_epilogue_rows", nvox)
+    stats = torch.full((rows * (cout * 2 + 1),), float("nan"), device=DEV)
+    L.call("pcms_split_epilogue", 1, acc, sp, b.to(DEV), y, None, cout, stats, cout, nvox, 0)
+    torch.cuda.synchronize()
+    ref = F.conv3d(torch.cat([x0, x1], 1).double(), w.to(dt).double(), b.double(), padding=1)
+    close(ncdhw(y.cpu()), ref, 1e-2, "fwd16 split")
+    mean, var = bn_moments(stats, rows, cout, nvox)
+    yref = ref.transpose(0, 1).reshape(cout, -1)
+    close(mean, yref.mean(1), 1e-3, "stats mean")
+    close(var, yref.var(1, unbiased=False), 1e-3, "stats var")
+    # dgrad: dx = conv(dy, w transposed, flipped), split into two outputs at cin / 2
+    spd = L.query("pcms_conv3_fwd16_split_ok", N, *S, cout, 0, cin)
+    if spd:
+        dy = torch.randn(N, cout, *S, generator=g).to(dt)
+        accd = torch.full((spd * nvox * cin,), float("nan"), device=DEV)
+        L.call("pcms_conv3_fwd16_split", ndhwc(dy).to(DEV), cout, None, 0, d16, accd, N, *S, cin, spd)
+        cy0 = cin // 2 if cin >= 128 else cin
+        o0 = torch.empty(N, *S, cy0, dtype=dt, device=DEV)
+        o1 = torch.empty(N, *S, max(cin - cy0, 8), dtype=dt, device=DEV)
+        L.call("pcms_split_epilogue", 1, accd, spd, None, o0, o1 if cin > cy0 else None, cy0, None, cin, nvox, 0)
+        torch.cuda.synchronize()
+        got = ncdhw(o0.cpu())
+        if cin > cy0:
+            got = torch.cat([got, ncdhw(o1.cpu())], 1)
+        close(got, F.conv_transpose3d(dy.double(), w.to(dt).double(), padding=1), 1e-2, "dgrad16 split")
+
+
 @pytest.mark.parametrize("nt8", [1, 0])
 @pytest.mark.parametrize("N,cout,cin,S,wgs", [(2, 64, 64, (16, 16, 32), 0), (1, 64, 128, (16, 16, 16), 3),
                                               (2, 128, 64, (8, 16, 32), 0), (1, 64, 256, (8, 8, 16), 0)])
