@@ -431,7 +431,10 @@ __device__ __forceinline__ f32x4_t mfma16(s16x8_t a, s16x8_t b, f32x4_t c) {
 
 constexpr int kWThreads = 512;          // 8 waves: wave = (co-tile, tap-group)
 // ablation builds only (tests/tools/wgrad_abl.py; 0 in the product): bit 1 the direct flush's
-// global stores dropped, 2 no staging after a workgroup's first box, 4 no MFMA phase
+// global stores dropped, 2 no staging after a workgroup's first box, 4 no MFMA phase, 8 no
+// wait for the next box's DMA at a box's end, 16 the spread pieces' addresses computed but
+// read nothing (zeros land in LDS), 32 the spread pieces read fixed in-range addresses (no
+// address arithmetic) -- wrong results: timing only
 #ifndef WGRAD_ABL
 #define WGRAD_ABL 0
 #endif
@@ -971,6 +974,8 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         if (gd < p.D && gh < p.H && gw < p.W)
           voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * p.Cout + co_base + ql * 8) * 2);
       }
+      if constexpr (WGRAD_ABL & 16) { asm volatile("" ::"v"(voff)); voff = kOOB; }
+      if constexpr (WGRAD_ABL & 32) voff = (uint32_t)(pc * 16);
       dma16(buffer_desc(p.dy, p.dybytes), __builtin_amdgcn_readfirstlane(lb0 + pc0 * 16), voff, 0);
       return 0u;
     }
@@ -982,6 +987,66 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
     if (hp < XP && gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && xc + q * 8 < xs)
       voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * xs + xc + q * 8) * 2);
+    if constexpr (WGRAD_ABL & 16) { asm volatile("" ::"v"(voff)); voff = kOOB; }
+    if constexpr (WGRAD_ABL & 32) voff = (uint32_t)(pc * 16);
+    dma16(buffer_desc(first ? p.x0 : p.x1, first ? p.x0bytes : p.x1bytes),
+          __builtin_amdgcn_readfirstlane(lb0 + DYBYTES + (pc0 - DYP) * 16), voff, 0);
+    return voff != kOOB ? 1u << i : 0u;
+  };
+  // compile-time boxes: each piece's source offset relative to its box origin does not depend
+  // on the box, so it is formed once (prel: elements past the box-origin voxel's first channel,
+  // pco: the halo coordinates hd | hh << 8 | hw << 16 of an x piece, -1 for padding pieces);
+  // a box then costs one add per piece, plus 3 compares on boxes that touch the volume's border.
+  // (Measured neutral here -- 819 vs 823-832 us at level 0, profiles/r5_wgrad_prel_abl.txt:
+  // with two waves per SIMD the VALU already hid under the other wave's MFMAs; what the
+  // fixed-address ablation gained, profiles/r5_wgrad_addr_abl.txt, was L2 hits, not arithmetic.)
+  int prel[kSpread ? MAXP : 1], pco[kSpread ? MAXP : 1];
+  if constexpr (kSpread) {
+    const bool first = ci_base < p.c0;
+    const int xs = first ? p.c0 : p.c1, xc = first ? ci_base : ci_base - p.c0;
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const int pc = (tid & ~63) + i * kWThreads + lane;
+      if ((tid & ~63) + i * kWThreads < DYP) {
+        const int r = pc >> 3, q = pc & 7;
+        const int ql = q ^ (((r >> 1) & 1) << 2);
+        const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+        prel[i] = ((rd * p.H + rh) * p.W + rw) * p.Cout + co_base + ql * 8;
+        pco[i] = r < boxvol ? (rd | (rh << 8) | (rw << 16)) : -1;
+      } else {
+        const int hp = pc - DYP, hv = hp >> 2, q = hp & 3;
+        const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+        prel[i] = (((hd_ - 1) * p.H + (hh_ - 1)) * p.W + (hw_ - 1)) * xs + xc + q * 8;
+        pco[i] = (hp < XP && xc + q * 8 < xs) ? (hd_ | (hh_ << 8) | (hw_ << 16)) : -1;
+      }
+    }
+  }
+  // piece i of the box at (n, d0, h0, w0): `inner` = the box and its halo lie inside the volume
+  auto stage_piece_fast = [&](char* buf, int i, int n, int d0, int h0, int w0, bool inner) -> uint32_t {
+    const int pc0 = (tid & ~63) + i * kWThreads;
+    if (pc0 >= DYP + XP) return 0u;
+    const uint32_t lb0 = lds_addr(buf);
+    const int c = pco[i];
+    const long vb = ((long)(n * p.D + d0) * p.H + h0) * p.W + w0;
+    uint32_t voff;
+    if (pc0 < DYP) {
+      voff = (uint32_t)((vb * p.Cout + prel[i]) * 2);
+      if (c < 0) voff = kOOB;
+      else if (!inner && (d0 + (c & 255) >= p.D || h0 + ((c >> 8) & 255) >= p.H || w0 + (c >> 16) >= p.W)) voff = kOOB;
+      dma16(buffer_desc(p.dy, p.dybytes), __builtin_amdgcn_readfirstlane(lb0 + pc0 * 16), voff, 0);
+      return 0u;
+    }
+    const bool first = ci_base < p.c0;
+    const int xs = first ? p.c0 : p.c1;
+    voff = (uint32_t)((vb * xs + prel[i]) * 2);
+    if (c < 0) {
+      voff = kOOB;
+    } else if (!inner) {
+      const int gd = d0 + (c & 255) - 1, gh = h0 + ((c >> 8) & 255) - 1, gw = w0 + (c >> 16) - 1;
+      if ((unsigned)gd >= (unsigned)p.D || (unsigned)gh >= (unsigned)p.H || (unsigned)gw >= (unsigned)p.W) voff = kOOB;
+    }
+    if constexpr (WGRAD_ABL & 16) { asm volatile("" ::"v"(voff)); voff = kOOB; }
+    if constexpr (WGRAD_ABL & 32) voff = (uint32_t)((pc0 + lane) * 16);
     dma16(buffer_desc(first ? p.x0 : p.x1, first ? p.x0bytes : p.x1bytes),
           __builtin_amdgcn_readfirstlane(lb0 + DYBYTES + (pc0 - DYP) * 16), voff, 0);
     return voff != kOOB ? 1u << i : 0u;
@@ -1071,8 +1136,12 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         // instead of in a block before them (where both waves of a SIMD stalled the MFMA pipe
         // together); they land long before the box-end wait (BNIN: before its apply at NK / 2)
         int n1 = 0, d1 = 0, h1 = 0, w1 = 0;
+        bool inner1 = false;
         if constexpr (kSpread && !(WGRAD_ABL & 4)) {
-          if (nxt) box_origin(b + 1, n1, d1, h1, w1);
+          if (nxt) {
+            box_origin(b + 1, n1, d1, h1, w1);
+            inner1 = d1 >= 1 && d1 + bd < p.D && h1 >= 1 && h1 + bh < p.H && w1 >= 1 && w1 + bw < p.W;
+          }
           xm = 0;
         } else if (nxt) {
           xm = stage_dma(nbuf, b + 1);
@@ -1087,7 +1156,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
               if (nxt) {
 #pragma unroll
                 for (int k = 0; k < PPS; ++k)
-                  if (st * PPS + k < MAXP) xm |= stage_piece(nbuf, st * PPS + k, n1, d1, h1, w1);
+                  if (st * PPS + k < MAXP) xm |= stage_piece_fast(nbuf, st * PPS + k, n1, d1, h1, w1, inner1);
               }
             }
           }
@@ -1102,7 +1171,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
         } else if constexpr (!(WGRAD_ABL & 4)) {
           compute_box(wlds + cur * BUFBYTES, nomid, stage);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (!(WGRAD_ABL & 8)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
     }
@@ -2126,20 +2195,37 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
   const i32x4_t xr1 = buffer_desc(p.x1 ? p.x1 : p.x0, x1bytes);
   const uint32_t lds0 = lds_addr(lds);
   // halo piece j of this thread: row pc / 2 (32 B), 16-B half pc & 1 (channels 8 half ..),
-  // no swizzle; live = false: still issued (the vmcnt arithmetic), reads out of range = zeros
-  auto stage_piece = [&](int n, int d0, int h0, int w0, int chunk, int buf, int j, bool live) {
+  // no swizzle; live = false: still issued (the vmcnt arithmetic), reads out of range = zeros.
+  // The piece's voxel (pvox, -1 outside the volume) depends on the box only: formed when a
+  // box's first chunk is staged (fresh) and reused for its other chunks (one multiply-add then);
+  // 4-deep boxes only (one wave per SIMD: registers to spare; the 8-deep kernel spills with it)
+  constexpr bool kCache = BD == 4;
+  int pvox[kCache ? G6::Pieces : 1];
+  auto stage_piece = [&](int n, int d0, int h0, int w0, int chunk, int buf, int j, bool live, bool fresh) {
     const int c = chunk * 16;
     const bool first = c < p.c0;
     const uint32_t stride = first ? p.c0 : p.c1;
     const uint32_t cofs = first ? c : c - p.c0;
     const int pc = opaque(tid) + j * G6::T;
-    const int hv = pc >> 1;
-    const int hw_ = hv % GW::HW, t_ = hv / GW::HW, hh_ = t_ % GW::HH, hd_ = t_ / GW::HH;
-    const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
     uint32_t voff = kOOB;
-    if (live && hv < G6::Halo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
-        (unsigned)gw < (unsigned)p.W)
-      voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs + (uint32_t)(pc & 1) * 8u) * 2u;
+    if constexpr (kCache) {
+      if (fresh) {
+        const int hv = pc >> 1;
+        const int hw_ = hv % GW::HW, t_ = hv / GW::HW, hh_ = t_ % GW::HH, hd_ = t_ / GW::HH;
+        const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+        pvox[j] = (hv < G6::Halo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
+                   (unsigned)gw < (unsigned)p.W) ? ((n * p.D + gd) * p.H + gh) * p.W + gw : -1;
+      }
+      if (live && pvox[j] >= 0) voff = ((uint32_t)pvox[j] * stride + cofs + (uint32_t)(pc & 1) * 8u) * 2u;
+    } else {
+      (void)fresh;
+      const int hv = pc >> 1;
+      const int hw_ = hv % GW::HW, t_ = hv / GW::HW, hh_ = t_ % GW::HH, hd_ = t_ / GW::HH;
+      const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+      if (live && hv < G6::Halo && (unsigned)gd < (unsigned)p.D && (unsigned)gh < (unsigned)p.H &&
+          (unsigned)gw < (unsigned)p.W)
+        voff = ((uint32_t)(((n * p.D + gd) * p.H + gh) * p.W + gw) * stride + cofs + (uint32_t)(pc & 1) * 8u) * 2u;
+    }
     const bool dummy = j == G6::Pieces - 1 && j * G6::T + wave * 64 >= 2 * G6::Halo;
     const uint32_t lb = __builtin_amdgcn_readfirstlane(
         dummy ? lds0 + 2 * G6::Buf : lds0 + buf * G6::Buf + (wave * 64 + j * G6::T) * 16);
@@ -2215,7 +2301,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     for (int i = 0; i < 2 * (slot & 3); ++i) __builtin_amdgcn_s_sleep(127);
   uint32_t pmask = 0;
 #pragma unroll
-  for (int j = 0; j < G6::Pieces; ++j) pmask |= stage_piece(n, d0, h0, w0, cbeg, 0, j, true);
+  for (int j = 0; j < G6::Pieces; ++j) pmask |= stage_piece(n, d0, h0, w0, cbeg, 0, j, true, true);
   {
     const uint32_t boff0 = (uint32_t)(cob * NT * 1024 + lane * 16);
 #pragma unroll
@@ -2265,7 +2351,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
         if constexpr (sn_ < kB6Steps) load_b(bset[sn_ % (kB6Dist + 1)], chunk, sn_, boff);
         else load_b(bset[sn_ % (kB6Dist + 1)], schunk, sn_ - kB6Steps, boff);
         if constexpr (st < G6::Pieces) {
-          const uint32_t bits = stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, st, live);
+          const uint32_t bits = stage_piece(sn, sd, sh, sw, schunk, buf ^ 1, st, live, last);
           if constexpr (BNIN) pmask = (st == 0 ? 0u : pmask) | bits;
         }
         s16x8_t (&b)[NT] = bset[st % (kB6Dist + 1)];
