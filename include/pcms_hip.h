@@ -312,8 +312,9 @@ int pcms_adam(float* p, float* g, float* m, float* v, long n, float step_size, f
               float eps, float wd, float bc2_sqrt, float gscale, const float* gmul, hipStream_t s);
 /* The same update split three ways so the weight packs come out of the same pass (bf16
  * build): conv weights by table rows int64[8] = {flat offset, Cout, Cin, fwd pack, dgrad
- * pack, first tile, 0, 0} (one 32 x 32 tile per block, Cout % 32 == Cin % 32 == 0) writing
- * both pcms_conv3_pack2 packs; ConvTranspose3d weights by rows {offset, Cin, Cout, fwd pack,
+ * pack, first tile, fwd16 pack, dgrad16 pack} (one 32 x 32 tile per block, Cout % 32 ==
+ * Cin % 32 == 0) writing each non-NULL pack: the pcms_conv3_pack2 pair and the
+ * pcms_conv3_pack16 pair; ConvTranspose3d weights by rows {offset, Cin, Cout, fwd pack,
  * dgrad pack, first tile, 0, 0} writing both pcms_convt_pack packs; every other parameter
  * through [begin, end) element ranges (int64 pairs).  Identical per-element arithmetic.   */
 int pcms_adam_pack_conv3(float* p, float* g, float* m, float* v, const long long* table, int ntab, int ntiles,

@@ -1526,12 +1526,17 @@ __global__ void __launch_bounds__(256) pack_conv3_bf16_both_kernel(const float* 
   }
 }
 
-// Adam + both bf16 packs in one pass over the conv weights (the flat master is read once per
+// the pack16 forms of one 32 co x 32 ci tile from its bf16 copy in LDS (defined below pack16_off)
+__device__ void pack16_tile_store(const uint16_t* tb, bf16_t* fwd16, bf16_t* dgr16, int j0, int ci0, int Cout,
+                                  int Cin);
+
+// Adam + the bf16 packs in one pass over the conv weights (the flat master is read once per
 // step instead of once for Adam and once more for the packs).  One block per (conv, 32 co x
-// 32 ci) tile of a table entry [off, Cout, Cin, fwd pack, dgrad pack, first tile, -, -]
-// (int64 each): the tile's 32 contiguous 864-float runs w[co][ci0..ci0+32][27] are updated
-// in place (p, m, v, and g when scaled), the new weights converted to bf16 into LDS, and both
-// packs written as in pack_conv3_bf16_both_kernel.
+// 32 ci) tile of a table entry [off, Cout, Cin, fwd pack, dgrad pack, first tile, fwd16 pack,
+// dgrad16 pack] (int64 each): the tile's 32 contiguous 864-float runs w[co][ci0..ci0+32][27]
+// are updated in place (p, m, v, and g when scaled), the new weights converted to bf16 into
+// LDS, and each non-null pack written: the general kernel's two as in
+// pack_conv3_bf16_both_kernel, the 16x16x32 kernel's two as in pack16_conv3_kernel.
 __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* Gr, float* Mo, float* Vo,
                                                               const long long* tab, int ntab, AdamCoef c,
                                                               const float* gmul) {
@@ -1543,6 +1548,8 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
   const int Cout = (int)e[1], Cin = (int)e[2];
   bf16_t* fwd = reinterpret_cast<bf16_t*>(e[3]);
   bf16_t* dgr = reinterpret_cast<bf16_t*>(e[4]);
+  bf16_t* fwd16 = reinterpret_cast<bf16_t*>(e[6]);
+  bf16_t* dgr16 = reinterpret_cast<bf16_t*>(e[7]);
   const int local = blockIdx.x - (int)e[5];
   const int j0 = (local % (Cout / 32)) * 32, chunk = local / (Cout / 32);
   const float s = gmul ? c.gscale * gmul[0] : c.gscale;
@@ -1587,22 +1594,25 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_kernel(float* P, float* G
     }
   }
   __syncthreads();
-  for (int g = threadIdx.x; g < 27 * 128; g += 256) {
-    const int t = g >> 7, co = (g >> 2) & 31, k8 = (g & 3) * 8;
-    u32x4_t o;
+  if (fwd)
+    for (int g = threadIdx.x; g < 27 * 128; g += 256) {
+      const int t = g >> 7, co = (g >> 2) & 31, k8 = (g & 3) * 8;
+      u32x4_t o;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      o[i] = (uint32_t)tb[co * 864 + (k8 + 2 * i) * 27 + t] | ((uint32_t)tb[co * 864 + (k8 + 2 * i + 1) * 27 + t] << 16);
-    *reinterpret_cast<u32x4_t*>(fwd + pack_bf16_off(chunk, t, j0 + co, k8, Cout)) = o;
-  }
-  for (int g = threadIdx.x; g < 27 * 128; g += 256) {
-    const int t = g >> 7, ci = (g >> 2) & 31, k8 = (g & 3) * 8, ts = 26 - t;
-    u32x4_t o;
+      for (int i = 0; i < 4; ++i)
+        o[i] = (uint32_t)tb[co * 864 + (k8 + 2 * i) * 27 + t] | ((uint32_t)tb[co * 864 + (k8 + 2 * i + 1) * 27 + t] << 16);
+      *reinterpret_cast<u32x4_t*>(fwd + pack_bf16_off(chunk, t, j0 + co, k8, Cout)) = o;
+    }
+  if (dgr)
+    for (int g = threadIdx.x; g < 27 * 128; g += 256) {
+      const int t = g >> 7, ci = (g >> 2) & 31, k8 = (g & 3) * 8, ts = 26 - t;
+      u32x4_t o;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      o[i] = (uint32_t)tb[(k8 + 2 * i) * 864 + ci * 27 + ts] | ((uint32_t)tb[(k8 + 2 * i + 1) * 864 + ci * 27 + ts] << 16);
-    *reinterpret_cast<u32x4_t*>(dgr + pack_bf16_off(j0 >> 5, t, chunk * 32 + ci, k8, Cin)) = o;
-  }
+      for (int i = 0; i < 4; ++i)
+        o[i] = (uint32_t)tb[(k8 + 2 * i) * 864 + ci * 27 + ts] | ((uint32_t)tb[(k8 + 2 * i + 1) * 864 + ci * 27 + ts] << 16);
+      *reinterpret_cast<u32x4_t*>(dgr + pack_bf16_off(j0 >> 5, t, chunk * 32 + ci, k8, Cin)) = o;
+    }
+  if (fwd16 || dgr16) pack16_tile_store(tb, fwd16, dgr16, j0, chunk * 32, Cout, Cin);
 }
 
 // fp32 build (bf16x6 packs): Adam + both three-part packs in one pass.  One block per (conv,
@@ -2535,15 +2545,26 @@ __global__ void __launch_bounds__(256) pack16_conv3_kernel(const long long* tab,
   bf16_t* dgr = reinterpret_cast<bf16_t*>(e[4]);
   const int local = blockIdx.x - (int)e[5];
   const int j0 = (local % (Cout / 32)) * 32, ci0 = (local / (Cout / 32)) * 32;
-  for (int i = threadIdx.x; i < 32 * 216; i += 256) {
-    const int run = i / 216, q = i % 216;
-    const f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(w + ((long)(j0 + run) * Cin + ci0) * 27) + q);
+  // all 27 loads of a thread in flight at once (as pack_conv3_bf16_both_kernel)
+  f32x4_t v[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+    const int q4 = threadIdx.x + i * 256, run = q4 / 216, q = q4 % 216;
+    v[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(w + ((long)(j0 + run) * Cin + ci0) * 27) + q);
+  }
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+    const int q4 = threadIdx.x + i * 256, run = q4 / 216, q = q4 % 216;
     uint2 o;
-    o.x = pack_bf16x2(v[0], v[1]);
-    o.y = pack_bf16x2(v[2], v[3]);
+    o.x = pack_bf16x2(v[i][0], v[i][1]);
+    o.y = pack_bf16x2(v[i][2], v[i][3]);
     *reinterpret_cast<uint2*>(tb + run * 864 + 4 * q) = o;
   }
   __syncthreads();
+  pack16_tile_store(tb, fwd, dgr, j0, ci0, Cout, Cin);
+}
+
+__device__ void pack16_tile_store(const uint16_t* tb, bf16_t* fwd, bf16_t* dgr, int j0, int ci0, int Cout, int Cin) {
   // 2 chunks x 14 steps x 2 row tiles x 64 lanes = 3584 16-B pieces per direction
   for (int it = threadIdx.x; it < 2 * 3584; it += 256) {
     const int dir = it / 3584, q = it % 3584;

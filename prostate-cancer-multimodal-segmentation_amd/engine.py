@@ -35,7 +35,8 @@ _DT = {"bf16": (torch.bfloat16, BF16), "fp32": (torch.float32, F32)}
 
 
 class ConvSpec:
-    __slots__ = ("mod", "cin", "cout", "cin_store", "fwd", "dgrad", "code", "fwd16", "dgrad16")
+    __slots__ = ("mod", "cin", "cout", "cin_store", "fwd", "dgrad", "code", "fwd16", "dgrad16", "old_stale",
+                 "old_used")
 
     def __init__(self, mod, cin, cout, cin_store):
         self.mod, self.cin, self.cout, self.cin_store = mod, cin, cout, cin_store
@@ -45,6 +46,11 @@ class ConvSpec:
         # UNetEngine._alloc for the convs whose forward / dgrad run on it at the allocated shape
         self.fwd16 = None
         self.dgrad16 = None
+        # fwd / dgrad (the general kernel's packs) not rewritten by the last fused Adam (it
+        # writes only the pack16 forms of a conv whose every call at the allocated shape ran
+        # on the 16x16x32 kernel); old_used: a call at this shape needed them
+        self.old_stale = False
+        self.old_used = False
         # conv-kernel dtype code: BF16, or for fp32 data F32 (bf16x6 arithmetic, fp32-grade)
         # / F32X3 (bf16x3, faster, ~10x the fp32 rounding error)
         self.code = None
@@ -346,6 +352,9 @@ class UNetEngine:
         self._dirty = True
         self._wgen += 1
         self._packs_fresh = packs_fresh and self._packed_version == self.flat_p._version
+        if self._packs_fresh and self._adam_plan is not None:
+            for cs in self._adam_plan["old_skip"]:
+                cs.old_stale = True
 
     def adam_plan(self):
         """Fused Adam + weight-pack plan (FlatAdam.step): device tables of the conv / ConvT
@@ -364,7 +373,7 @@ class UNetEngine:
 
         fused = []
         skipped = 0  # layers (besides the stem) whose packs the Adam kernels do not write
-        conv_rows, tiles = [], 0
+        conv_rows, tiles, old_skip = [], 0, []
         for i, cs in enumerate(self.convs):
             w = cs.mod.weight
             if i == 0:
@@ -372,7 +381,15 @@ class UNetEngine:
             if cs.cin % 32 or cs.cout % 32 or offset(w) % 4 or (x6 and cs.code != F32):
                 skipped += 1
                 continue
-            conv_rows.append([offset(w), cs.cout, cs.cin, cs.fwd.data_ptr(), cs.dgrad.data_ptr(), tiles, 0, 0])
+            # bf16 build: the pack16 forms too; the general kernel's packs only where a call
+            # at this shape used them (else marked stale, repacked on first use: _old_packs)
+            f16 = cs.fwd16.data_ptr() if not x6 and cs.fwd16 is not None else 0
+            d16 = cs.dgrad16.data_ptr() if not x6 and cs.dgrad16 is not None else 0
+            skip = bool(f16 and d16) and not cs.old_used
+            conv_rows.append([offset(w), cs.cout, cs.cin, 0 if skip else cs.fwd.data_ptr(),
+                              0 if skip else cs.dgrad.data_ptr(), tiles, f16, d16])
+            if skip:
+                old_skip.append(cs)
             tiles += (cs.cout // 32) * (cs.cin // (16 if x6 else 32))
             fused.append((offset(w), w.numel()))
         ct_rows, ct_tiles = [], 0
@@ -406,6 +423,8 @@ class UNetEngine:
             # must not mark the packs fresh: a skipped layer would train on stale packs)
             "complete": skipped == 0,
             "x6": x6,
+            "old_skip": old_skip,  # convs whose general-kernel packs this plan does not write
+            "p16": not x6,         # the pack16 forms come out of the Adam pass
         }
         return self._adam_plan
 
@@ -427,7 +446,8 @@ class UNetEngine:
                 call("pcms_conv3_pack2", cs.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
             self._dirty = False
             self._packs_fresh = False
-            self._pack16()
+            if self._adam_plan is None or not self._adam_plan["p16"]:
+                self._pack16()
             return
         for i, cs in enumerate(self.convs):
             w = cs.mod.weight
@@ -454,6 +474,8 @@ class UNetEngine:
             f, d = self.convt_packs[i]
             call("pcms_convt_pack", self.code, up.weight, f, cin, cout, 0)
             call("pcms_convt_pack", self.code, up.weight, d, cin, cout, 1)
+        for cs in self.convs:
+            cs.old_stale = False
         self._packed_version = self.flat_p._version
         self._dirty = False
         self._packs_fresh = False
@@ -477,6 +499,17 @@ class UNetEngine:
         tab, n, tiles = self._p16
         if n:
             call("pcms_conv3_pack16", tab, n, tiles)
+
+    def _old_packs(self, cs: ConvSpec):
+        """The general kernel's packs of ``cs`` before a call that reads them: rebuilt from the
+        master when the fused Adam skipped them, and the Adam plan redone so that it writes
+        them from the next step on."""
+        if cs.old_stale:
+            call("pcms_conv3_pack2", cs.code, cs.mod.weight, cs.fwd, cs.dgrad, cs.cout, cs.cin)
+            cs.old_stale = False
+        if not cs.old_used:
+            cs.old_used = True
+            self._adam_plan = None
 
     def _stem_conv_pack(self):
         """The stem conv's general-kernel weight pack, when the fast path skipped it."""
@@ -652,8 +685,12 @@ class UNetEngine:
                     if query("pcms_conv3_big16_ok", N, *S[l], cs.cout, 0, cs.cin) or \
                             query("pcms_conv3_fwd16_split_ok", N, *S[l], cs.cout, 0, cs.cin):
                         cs.dgrad16 = torch.empty(query("pcms_conv3_pack16_elems", cs.cin, cs.cout), dtype=T, device=dev)
+        for cs in self.convs:
+            cs.old_used = False
         self._p16 = None
         self._dirty = True  # build the new pack16 forms before the next conv
+        self._packs_fresh = False  # (those of the last fused Adam went to the old buffers)
+        self._adam_plan = None
         self.bufs = b
         self.buf_key = key
 
@@ -695,6 +732,7 @@ class UNetEngine:
                  st, 0, N, *S, cs.cout)
             rows = query("pcms_conv3_fwd16_rows", N, *S, c0, 0, cs.cout)
         elif bnin is not None:
+            self._old_packs(cs)
             call("pcms_conv3_fwd_bnin", cs.code, x0, c0, bnin.scale, bnin.shift, cs.fwd, cs.mod.bias, y, st, N,
                  *S, cs.cout)
             rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, 0, cs.cout)
@@ -712,11 +750,13 @@ class UNetEngine:
             call("pcms_split_epilogue", self.code, acc, sp16, cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox, 0)
             rows = query("pcms_split_epilogue_rows", nvox)
         elif splits == 1:
+            self._old_packs(cs)
             call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  None, st, 0, N, S[0], S[1], S[2], cs.cout, 1)
             rows = query("pcms_conv3_fwd_rows", cs.code, N, *S, c0, c1, cs.cout)
         else:
             acc = b["yacc"]
+            self._old_packs(cs)
             call("pcms_conv3_fwd", cs.code, x0, c0, x1, c1, cs.fwd, cs.mod.bias, y, None, cs.cout,
                  acc, None, 0, N, S[0], S[1], S[2], cs.cout, splits)
             call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", cs.code, c0 + c1, splits),
@@ -914,6 +954,7 @@ class UNetEngine:
             call("pcms_conv3_fwd16", gy, cs.cout, None, 0, None, None, cs.dgrad16, None, out0, out1, cy0, None, 0,
                  N, *S, cs.cin)
         elif splits == 1:
+            self._old_packs(cs)
             call("pcms_conv3_fwd", cs.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  None, None, 0, N, *S, cs.cin, 1)
         elif cs.dgrad16 is not None and (sp16 := query("pcms_conv3_fwd16_split_ok", N, *S, cs.cout, 0, cs.cin)):
@@ -922,6 +963,7 @@ class UNetEngine:
             call("pcms_split_epilogue", self.code, acc, sp16, None, out0, out1, cy0, None, cs.cin, nvox, 0)
         else:
             acc = b["yacc"]
+            self._old_packs(cs)
             call("pcms_conv3_fwd", cs.code, gy, cs.cout, None, 0, cs.dgrad, None, out0, out1, cy0,
                  acc, None, 0, N, *S, cs.cin, splits)
             call("pcms_split_epilogue", self.code, acc, query("pcms_conv3_splits", cs.code, cs.cout, splits),

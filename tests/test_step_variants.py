@@ -188,15 +188,63 @@ def test_fused_adam_packs_match_flat_adam(gscale, precision):
     assert plan["x6"] == (precision == "fp32")
     for a, b in ((e0.flat_p, e1.flat_p), (e0.flat_g, e1.flat_g), (o0._m, o1._m), (o0._v, o1._v)):
         torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-12)
-    packs = [t.clone() for cs in e1.convs for t in (cs.fwd, cs.dgrad) if t is not None]
-    packs += [t.clone() for i in range(4) for t in e1.convt_packs[i]]
+    # (the general kernel's packs of convs that run only on the 16x16x32 kernel are skipped
+    # by the fused Adam and rebuilt on use: test_fused_adam_writes_pack16)
+    packs = [(t, t.clone()) for cs in e1.convs if not cs.old_stale for t in (cs.fwd, cs.dgrad) if t is not None]
+    packs += [(t, t.clone()) for i in range(4) for t in e1.convt_packs[i]]
+    packs += [(t, t.clone()) for cs in e1.convs for t in (cs.fwd16, cs.dgrad16) if t is not None]
+    assert len(packs) >= 21
     e1.mark_dirty()
-    e1._ensure_packs()  # full repack from the fused step's master
-    fresh = [t for cs in e1.convs for t in (cs.fwd, cs.dgrad) if t is not None]
-    fresh += [t for i in range(4) for t in e1.convt_packs[i]]
+    e1._ensure_packs()  # full repack from the fused step's master (in place)
     torch.cuda.synchronize()
-    for a, b in zip(packs, fresh):
+    for t, a in packs:
+        assert torch.equal(a.view(torch.int16), t.view(torch.int16))
+
+
+@pytest.mark.gpu
+def test_fused_adam_writes_pack16():
+    """At a shape where the 16x16x32 kernel runs (1 x 5x128x128x64), the fused Adam also writes
+    the pack16 forms (no separate pcms_conv3_pack16 pass) and skips the general kernel's packs
+    of the convs no call used; both are bit-identical to the pack kernels run on the updated
+    master, and a skipped pack is rebuilt on first use (engine._old_packs), which re-plans."""
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    gen = torch.Generator().manual_seed(3)
+    x = torch.rand(1, 5, 128, 128, 64, generator=gen).cuda()
+    y = (torch.rand(1, 1, 128, 128, 64, generator=gen) < 0.5).float().cuda()
+    torch.manual_seed(0)
+    m = UNet3D(n_modalities=5, n_classes=1, precision="bf16").cuda()
+    opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
+    for _ in range(2):
+        opt.zero_grad()
+        BCEDiceLoss()(m(x), y).backward()
+        opt.step()
+    eng = m.engine()
+    plan = eng._adam_plan
+    assert plan is not None and plan["p16"] and plan["complete"]
+    with16 = [cs for cs in eng.convs if cs.fwd16 is not None or cs.dgrad16 is not None]
+    assert len(with16) >= 8
+    assert plan["old_skip"] and all(cs.old_stale for cs in plan["old_skip"])
+    p16 = [t.clone() for cs in with16 for t in (cs.fwd16, cs.dgrad16) if t is not None]
+    old = {id(cs): (cs.fwd.clone(), cs.dgrad.clone()) for cs in eng.convs[1:] if not cs.old_stale}
+    # a skipped pack, rebuilt on use
+    cs = plan["old_skip"][0]
+    eng._old_packs(cs)
+    assert not cs.old_stale and cs.old_used and eng._adam_plan is None
+    lazy = (cs.fwd.clone(), cs.dgrad.clone())
+    eng.mark_dirty()
+    eng._ensure_packs()  # full repack (general packs + pcms_conv3_pack16) from the same master
+    torch.cuda.synchronize()
+    fresh = [t for c in with16 for t in (c.fwd16, c.dgrad16) if t is not None]
+    for a, b in zip(p16, fresh):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    for c in eng.convs[1:]:
+        if id(c) in old:
+            assert torch.equal(old[id(c)][0].view(torch.int16), c.fwd.view(torch.int16))
+            assert torch.equal(old[id(c)][1].view(torch.int16), c.dgrad.view(torch.int16))
+    assert torch.equal(lazy[0].view(torch.int16), cs.fwd.view(torch.int16))
+    assert torch.equal(lazy[1].view(torch.int16), cs.dgrad.view(torch.int16))
 
 
 def _oracle_amp_clip_step(x, y, max_norm, init_scale=2.0 ** 16):
