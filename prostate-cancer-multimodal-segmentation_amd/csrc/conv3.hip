@@ -2428,6 +2428,16 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
     // 16 B per lane, each store instruction inside one 64-channel half), 16-B stores.
     // BatchNorm moments shifted by K (the running mean; the bias before the first box), per
     // channel over the wave's 128 voxels, Chan-merged per (wave, channel).
+    if constexpr ((BG_ABL & 64) != 0) {  // ablation: no epilogue at all
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) asm volatile("" ::"v"(acc[mt][j]));
+      if (!has_next) break;
+      box = nbx;
+      n = nn; d0 = nd0; h0 = nh0; w0 = nw0;
+      continue;
+    }
     const int lane_o = opaque(lane);
     const int rr = lane_o & 15, gg = lane_o >> 4;
     const long plane = (long)p.H * p.W;
@@ -2449,8 +2459,11 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v0 = acc[mt][j][i];
-          *reinterpret_cast<bf16_t*>(slice + (4 * gg + i) * G6::Row + (16 * j + rr) * 2) =
-              f2bf(relu ? fmaxf(v0 + bias_j[j], 0.f) : v0 + bias_j[j]);
+          if constexpr ((BG_ABL & 32) == 0)
+            *reinterpret_cast<bf16_t*>(slice + (4 * gg + i) * G6::Row + (16 * j + rr) * 2) =
+                f2bf(relu ? fmaxf(v0 + bias_j[j], 0.f) : v0 + bias_j[j]);
+          else
+            asm volatile("" ::"v"(v0));
           const float e0 = v0 + (bias_j[j] - K0[j]);
           S1[j] += e0;
           S2[j] = fmaf(e0, e0, S2[j]);
