@@ -2182,6 +2182,11 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
   static_assert(NT == 4 || (NT == 8 && BD == 4), "128-channel blocks: one wave per SIMD");
   static_assert(!SPLIT || (!BNIN && NT == 4), "split-K form: plain 64-channel blocks");
   constexpr int CO = G6::CO;
+  // kT (64-channel blocks): the MFMA runs weights x activations, so a lane's accumulator holds
+  // 4 consecutive output channels of one voxel (channel-major D) -- the epilogue stores them
+  // straight from registers (8 B of bf16, or 16 B of fp32 partial rows) instead of transposing
+  // through the LDS slice
+  constexpr bool kT = NT == 4;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2372,7 +2377,10 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
           constexpr int q = st * 8 + mt + 2;  // the fragment read now: position q (two ahead)
           if constexpr (q < kB6Steps * 8) ar[q % 3] = rd(q / 8, q % 8);
 #pragma unroll
-          for (int j = 0; j < NT; ++j) acc[mt][j] = mfma16(ar[(st * 8 + mt) % 3], b[j], acc[mt][j]);
+          for (int j = 0; j < NT; ++j) {
+            if constexpr (kT) acc[mt][j] = mfma16(b[j], ar[(st * 8 + mt) % 3], acc[mt][j]);
+            else acc[mt][j] = mfma16(ar[(st * 8 + mt) % 3], b[j], acc[mt][j]);
+          }
         });
         // keep the order (1 read, NT MFMAs per M-tile) and every step's work in its step
 #pragma unroll
@@ -2402,10 +2410,15 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
+        for (int j = 0; j < NT; ++j) {
+          if constexpr (kT) {  // lane (gg, rr): voxel rr, channels 16 j + 4 gg .. + 3
+            *reinterpret_cast<f32x4_t*>(slice + rr * G6::Row32 + (16 * j + 4 * gg) * 4) = acc[mt][j];
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<float*>(slice + (4 * gg + i) * G6::Row32 + (16 * j + rr) * 4) = acc[mt][j][i];
+            for (int i = 0; i < 4; ++i)
+              *reinterpret_cast<float*>(slice + (4 * gg + i) * G6::Row32 + (16 * j + rr) * 4) = acc[mt][j][i];
+          }
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int k = 0; k < CO / 16; ++k) {
@@ -2433,6 +2446,114 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
       for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
         for (int j = 0; j < NT; ++j) asm volatile("" ::"v"(acc[mt][j]));
+      if (!has_next) break;
+      box = nbx;
+      n = nn; d0 = nd0; h0 = nh0; w0 = nw0;
+      continue;
+    }
+    if constexpr (kT) {
+      // lane (gg, rr) holds, per (M-tile mt, N-tile j), voxel rr of h-row(s) mt and channels
+      // 16 j + 4 gg + i (i < 4): + bias, bf16, one 8-B store.  BatchNorm moments shifted by K
+      // (the running mean; the bias before the first box) summed over the lane's 8 M-tiles,
+      // then over the 16 lanes of its DPP row (the wave's 128 voxels), Chan-merged per (wave,
+      // channel) as below
+      const int lane_o = opaque(lane);
+      const int rr = lane_o & 15, gg = lane_o >> 4;
+      const long vbase = (((long)n * p.D + d0 + wave) * p.H + h0) * p.W + w0;
+      const bool relu = p.accumulate & PCMS_CONV_RELU;
+      const bool want_stats = p.stats != nullptr;  // (the dgrads: none)
+      long ys;
+      int yc0;
+      const auto yr = ydst(0, ys, yc0);
+      const float rn = (float)nbdone * 128.f;
+      constexpr float nb = 128.f;  // voxels per wave and box
+      const float nnew = rn + nb;
+      // statistics N-tile by N-tile (4 channels x 2 sums live), then the values M-tile by
+      // M-tile through the wave's slice: one 8-B LDS write per (M-tile, N-tile), read back as
+      // whole 128-B half rows for 16-B stores (register-direct 8-B stores touch 16 lines per
+      // instruction and ran slower)
+      float bias4[NT][4];
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bias4[j][i] = bls[16 * j + 4 * gg + i];
+      if (want_stats) {
+        // per-lane shifted sums of its 16 channels (m = 4 j + i) over its 8 voxels, then a
+        // reduce-scatter over the 16 lanes of the row (4 DPP stages, halving the values each
+        // time): lane rr ends with channel m = rr summed over the row's 128 voxels, and merges
+        // that one channel
+        float S1[4 * NT], S2[4 * NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          float K4[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            K4[i] = nbdone ? red[(wave * CO + 16 * j + 4 * gg + i) * 3] : bias4[j][i];
+            S1[4 * j + i] = 0.f;
+            S2[4 * j + i] = 0.f;
+          }
+#pragma unroll
+          for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float e0 = acc[mt][j][i] + (bias4[j][i] - K4[i]);
+              S1[4 * j + i] += e0;
+              S2[4 * j + i] = fmaf(e0, e0, S2[4 * j + i]);
+            }
+        }
+        auto stage = [&](auto nc, auto ctl, bool hi) __attribute__((always_inline)) {
+          constexpr int h = decltype(nc)::value / 2;
+          constexpr int c = decltype(ctl)::value;
+#pragma unroll
+          for (int k = 0; k < h; ++k) {
+            const float k1 = hi ? S1[h + k] : S1[k], t1 = hi ? S1[k] : S1[h + k];
+            const float k2 = hi ? S2[h + k] : S2[k], t2 = hi ? S2[k] : S2[h + k];
+            S1[k] = k1 + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t1), c, 0xf, 0xf, true));
+            S2[k] = k2 + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t2), c, 0xf, 0xf, true));
+          }
+        };
+        static_assert(NT == 4, "16 channels per lane");
+        stage(std::integral_constant<int, 16>{}, std::integral_constant<int, 0x140>{}, (rr & 8) != 0);  // 15 - r
+        stage(std::integral_constant<int, 8>{}, std::integral_constant<int, 0x141>{}, (rr & 4) != 0);   // 7 - r
+        stage(std::integral_constant<int, 4>{}, std::integral_constant<int, 0x4e>{}, (rr & 2) != 0);    // r ^ 2
+        stage(std::integral_constant<int, 2>{}, std::integral_constant<int, 0xb1>{}, (rr & 1) != 0);    // r ^ 1
+        const int ch = 16 * (rr >> 2) + 4 * gg + (rr & 3);
+        float* rme = red + (wave * CO + ch) * 3;
+        const float K = nbdone ? rme[0] : bls[ch];
+        const float s1 = S1[0], s2 = S2[0];
+        const float mbox = K + s1 / nb;
+        const float m2b = fmaxf(s2 - s1 * s1 / nb, 0.f);
+        const float rmean = nbdone ? rme[0] : 0.f, rm2 = nbdone ? rme[1] : 0.f;
+        const float delta = mbox - rmean;
+        rme[0] = rmean + delta * (nb / nnew);
+        rme[1] = rm2 + m2b + delta * delta * (rn * nb / nnew);
+        rme[2] = nnew;
+      }
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          uint32_t o[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const float a0 = acc[mt][j][2 * k] + bias4[j][2 * k], a1 = acc[mt][j][2 * k + 1] + bias4[j][2 * k + 1];
+            o[k] = (uint32_t)f2bf(relu ? fmaxf(a0, 0.f) : a0) | ((uint32_t)f2bf(relu ? fmaxf(a1, 0.f) : a1) << 16);
+          }
+          *reinterpret_cast<u32x2_t*>(slice + rr * G6::Row + (16 * j + 4 * gg) * 2) = (u32x2_t){o[0], o[1]};
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < NT / 2; ++k) {
+          const int vw = (k * 64 + lane_o) >> 3, c8 = lane_o & 7;
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(slice + vw * G6::Row + c8 * 16);
+          const long vox = vbase + (long)(mt * (16 / WB) + vw / WB) * p.W + vw % WB;
+          if constexpr ((BG_ABL & 2) == 0)
+            __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)((vox * ys + yc0 + c8 * 8) * 2), 0, 0);
+          else
+            asm volatile("" ::"v"(v), "v"((int)vox));
+        }
+      }
+      ++nbdone;
       if (!has_next) break;
       box = nbx;
       n = nn; d0 = nd0; h0 = nh0; w0 = nw0;
