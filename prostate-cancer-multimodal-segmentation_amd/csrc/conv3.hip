@@ -2482,24 +2482,28 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
         // reduce-scatter over the 16 lanes of the row (4 DPP stages, halving the values each
         // time): lane rr ends with channel m = rr summed over the row's 128 voxels, and merges
         // that one channel
+        // (channel pairs in packed fp32: v_pk_add_f32 / v_pk_fma_f32, the same IEEE results)
         float S1[4 * NT], S2[4 * NT];
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          float K4[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            K4[i] = nbdone ? red[(wave * CO + 16 * j + 4 * gg + i) * 3] : bias4[j][i];
-            S1[4 * j + i] = 0.f;
-            S2[4 * j + i] = 0.f;
-          }
+          for (int q = 0; q < 2; ++q) {
+            const int c0 = 16 * j + 4 * gg + 2 * q;
+            const float k0 = nbdone ? red[(wave * CO + c0) * 3] : bias4[j][2 * q];
+            const float k1 = nbdone ? red[(wave * CO + c0 + 1) * 3] : bias4[j][2 * q + 1];
+            const f32x2_t sh = {bias4[j][2 * q] - k0, bias4[j][2 * q + 1] - k1};
+            f32x2_t s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
 #pragma unroll
-          for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float e0 = acc[mt][j][i] + (bias4[j][i] - K4[i]);
-              S1[4 * j + i] += e0;
-              S2[4 * j + i] = fmaf(e0, e0, S2[4 * j + i]);
+            for (int mt = 0; mt < 8; ++mt) {
+              const f32x2_t e = (f32x2_t){acc[mt][j][2 * q], acc[mt][j][2 * q + 1]} + sh;
+              s1 += e;
+              s2 = __builtin_elementwise_fma(e, e, s2);
             }
+            S1[4 * j + 2 * q] = s1[0];
+            S1[4 * j + 2 * q + 1] = s1[1];
+            S2[4 * j + 2 * q] = s2[0];
+            S2[4 * j + 2 * q + 1] = s2[1];
+          }
         }
         auto stage = [&](auto nc, auto ctl, bool hi) __attribute__((always_inline)) {
           constexpr int h = decltype(nc)::value / 2;
@@ -2536,8 +2540,10 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
           uint32_t o[2];
 #pragma unroll
           for (int k = 0; k < 2; ++k) {
-            const float a0 = acc[mt][j][2 * k] + bias4[j][2 * k], a1 = acc[mt][j][2 * k + 1] + bias4[j][2 * k + 1];
-            o[k] = (uint32_t)f2bf(relu ? fmaxf(a0, 0.f) : a0) | ((uint32_t)f2bf(relu ? fmaxf(a1, 0.f) : a1) << 16);
+            f32x2_t a = (f32x2_t){acc[mt][j][2 * k], acc[mt][j][2 * k + 1]} +
+                        (f32x2_t){bias4[j][2 * k], bias4[j][2 * k + 1]};
+            if (relu) a = (f32x2_t){fmaxf(a[0], 0.f), fmaxf(a[1], 0.f)};
+            o[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(a, bf16x2_t));
           }
           *reinterpret_cast<u32x2_t*>(slice + rr * G6::Row + (16 * j + 4 * gg) * 2) = (u32x2_t){o[0], o[1]};
         }
