@@ -2392,7 +2392,7 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
       });
       if (!last) vm_wait<NT * (kB6Steps - G6::Pieces)>();
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (BNIN) bn_apply(buf ^ 1, schunk, pmask);
+      if constexpr (BNIN && (BG_ABL & 128) == 0) bn_apply(buf ^ 1, schunk, pmask);  // (128: ablation)
       __syncthreads();
       buf ^= 1;
     };

@@ -11,10 +11,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
-SHAPES = [  # (N, D, H, W, c0, c1, Cout, cy0, stats)
+SHAPES = [  # (N, D, H, W, c0, c1, Cout, cy0, stats[, bnin])
     (2, 128, 128, 64, 64, 0, 128, 64, False),   # level-0 dgrad of the decoder's first conv
     (2, 128, 128, 64, 64, 0, 64, 64, True),     # level-0 64 -> 64 forward with statistics
     (2, 128, 128, 64, 64, 64, 64, 64, True),    # level-0 decoder conv0 forward
+    (2, 128, 128, 64, 64, 0, 64, 64, True, True),  # level-0 conv1 with the BN of conv0 fused in
 ]
 
 
@@ -25,7 +26,8 @@ def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "product"
     probe = bench.ClockProbe()
     T = torch.bfloat16
-    for (N, D, H, W, c0, c1, cout, cy0, with_stats) in SHAPES:
+    for (N, D, H, W, c0, c1, cout, cy0, with_stats, *bn) in SHAPES:
+        bnin = bool(bn and bn[0])
         nvox = N * D * H * W
         cin = c0 + c1
         xs = [(torch.randn(nvox * c0, device="cuda").to(T), torch.randn(nvox * max(c1, 8), device="cuda").to(T))
@@ -40,10 +42,12 @@ def main():
         bias = torch.randn(cout, device="cuda")
         stats = torch.zeros(4096 * (2 * cout + 1) + 1024, device="cuda")
         st = stats if with_stats else None
+        isc = (torch.rand(c0, device="cuda") + 0.5) if bnin else None
+        ish = torch.randn(c0, device="cuda") if bnin else None
 
         def run(i):
             a, b = xs[i % 2]
-            L.call("pcms_conv3_fwd16", a, c0, b if c1 else None, c1, None, None, w16, bias, y0,
+            L.call("pcms_conv3_fwd16", a, c0, b if c1 else None, c1, isc, ish, w16, bias, y0,
                    y1 if cy0 < cout else None, cy0, st, 0, N, D, H, W, cout)
         for rep in range(2):
             for i in range(3):
@@ -60,7 +64,7 @@ def main():
             us = e0.elapsed_time(e1) / 20 * 1e3
             mhz = statistics.median(bench.ClockProbe.mhz(k0, k1).values())
             flop = 2.0 * nvox * cout * cin * 27
-            print(json.dumps({"lib": tag, "shape": f"{c0}+{c1}->{cout} {N}x{D}x{H}x{W} cy0 {cy0} stats {int(with_stats)}",
+            print(json.dumps({"lib": tag, "shape": f"{'bn' if bnin else ''}{c0}+{c1}->{cout} {N}x{D}x{H}x{W} cy0 {cy0} stats {int(with_stats)}",
                               "us": round(us, 1), "mhz": round(mhz), "mfma_frac": round(flop / us / 1e-6 / 2.5e15, 3),
                               "mfma_frac_at_clock": round(flop / us / 1e-6 / (2.5e15 * mhz / 2400), 3)}), flush=True)
 
