@@ -8,8 +8,9 @@ loss + backward + (all-reduce) + Adam.  The K timed steps run back to back betwe
 device synchronize on both sides; per-step times are HIP events recorded on the compute
 stream at every step boundary, max over ranks, and ``value`` uses their MEDIAN (the wall time
 of the K steps is reported beside it).  Prints ONE JSON line (rank 0) with the roofline of the stem conv
-(forward + weight-gradient kernels with the stem's BatchNorm-backward apply fused into the
-latter, HBM-bound, 847.3 MB algorithmic at N=2), their launch
+(forward + weight-gradient kernels, HBM-bound: ``frac`` on BASELINE.md's 578.9 MB at N=2,
+``frac_fused`` on the 847.3 MB the product's kernels move with the stem's BatchNorm-backward
+apply fused into the weight gradient), their launch
 durations measured with HIP events on the launch stream inside the timed steps, the fp32
 parity build's rate, and the CPU oracle timed on the host cores
 (rank 0, N=1 only: 1 warm-up + 3 timed steps at the config batch, median).
@@ -161,11 +162,13 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
     fwd_bytes = xb + 64 * 5 * 27 * es + yb
     wg_bytes = xb + (2 if fused else 1) * yb + 64 * 5 * 27 * 4
     t = res["fwd"] + res["wgrad"]
-    achieved = (fwd_bytes + wg_bytes) / t
-    # SURVEY §8(d)'s own accounting (the conv alone: X + W + Y / X + dY + dW = 578.9 MB at
-    # N=2), over the same measured time: the fused kernel reads Y as well, so this is the
-    # lower of the two fractions
+    # the headline follows BASELINE.md / SURVEY §8(d): the conv alone, X + W + Y / X + dY + dW
+    # = 578.9 MB at N=2, achieved = 578.9e6 / t / 8e12
     s8d_bytes = fwd_bytes + xb + yb + 64 * 5 * 27 * 4
+    achieved = s8d_bytes / t
+    # the bytes the product's fused kernels must move over the same t (the stem's BN-backward
+    # apply fused into its weight gradient reads dA and the pre-BN Y: 847.3 MB at N=2)
+    fused_bytes = fwd_bytes + wg_bytes
     # HBM bytes per fwd+wgrad pair from the PMC counters (FETCH_SIZE / WRITE_SIZE in separate
     # rocprofv3 passes, gfx950 FETCH correction: tests/kexp/pmc_stem_traffic.sh), committed
     # for the shape they were measured on; null for any other shape
@@ -183,8 +186,9 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
     return {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
             "kernel": kernel,
-            "algorithmic_bytes": fwd_bytes + wg_bytes,
-            "frac_s8d": round(s8d_bytes / t / HBM_PEAK, 4), "algorithmic_bytes_s8d": s8d_bytes,
+            "algorithmic_bytes": s8d_bytes,
+            "frac_fused": round(fused_bytes / t / HBM_PEAK, 4), "achieved_fused": round(fused_bytes / t / 1e9, 1),
+            "algorithmic_bytes_fused": fused_bytes,
             "t_fwd_us": round(res["fwd"] * 1e6, 1),
             "t_wgrad_us": round(res["wgrad"] * 1e6, 1),
             "timing": "HIP events around each launch inside the timed steps" if in_step else

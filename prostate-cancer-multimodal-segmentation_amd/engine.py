@@ -255,16 +255,26 @@ class UNetEngine:
         t.setdefault(name, []).append((e0, e1))
 
     def _grads_done(self, *params):
-        """The gradients of ``params`` (adjacent in the flat buffer) are final: join the
-        weight-gradient stream (its dW kernels are then ordered before any consumer), and report
-        their flat range to the data-parallel hook (dp.GradSync) -- per layer, as each
+        """The gradients of ``params`` (adjacent in the flat buffer) are final: report their
+        flat range to the data-parallel hook (dp.GradSync) -- per layer, as each
         weight-gradient / BatchNorm-backward kernel is enqueued, in descending flat order
         (dp.readiness_groups lists the sequence), so the all-reduce buckets start while the
-        backward still runs and only the last layers' bucket waits at the end."""
-        self._join_side()
-        if self.grad_ready is not None:
-            spans = [self.param_span[id(p)] for p in params]
-            self.grad_ready(min(a for a, _ in spans), max(b for _, b in spans))
+        backward still runs and only the last layers' bucket waits at the end.  With the
+        weight gradients on the side stream the report is made from that stream after it has
+        waited for the compute stream's queue, so a bucket's all-reduce is ordered after the
+        kernels of both streams that wrote it, and the compute stream itself does not wait for
+        the weight gradients (it joins them once per block: _block_bwd)."""
+        if self.grad_ready is None:
+            return
+        spans = [self.param_span[id(p)] for p in params]
+        lo, hi = min(a for a, _ in spans), max(b for _, b in spans)
+        if self._side_used:
+            side = self._side_stream
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                self.grad_ready(lo, hi)
+        else:
+            self.grad_ready(lo, hi)
 
     # weight gradients run on a side stream beside the data-gradient chain (dgrad -> BN ->
     # dgrad ...): they only read activations and the dY buffer of their layer, which the main
@@ -643,14 +653,16 @@ class UNetEngine:
         # split-K slabs [splits][nvox][Cout] for every conv (fwd and dgrad) that splits
         yacc = 1
         for blk, l in [(bk, i) for i, bk in enumerate(self.enc)] + [(bk, 3 - i) for i, bk in enumerate(self.dec)]:
-            for cs in (blk.c0, blk.c1):
-                dirs = [(cs.cin_store, cs.cout)] + ([(cs.cout, cs.cin)] if cs is not self.convs[0] else [])
-                for cin, cout in dirs:  # forward, dgrad (the stem has none)
-                    sp = self._splits(N, S[l], cin, cout, cs.code)
+            for cs, c1 in ((blk.c0, C[l] if blk in self.dec else 0), (blk.c1, 0)):
+                # forward (sources as the block feeds them: the decoder's first conv reads the
+                # skip and the upsampled halves), dgrad (the stem has none)
+                dirs = [(cs.cin_store - c1, c1, cs.cout)] + ([(cs.cout, 0, cs.cin)] if cs is not self.convs[0] else [])
+                for c0_, c1_, cout in dirs:
+                    sp = self._splits(N, S[l], c0_ + c1_, cout, cs.code)
                     if sp > 1:
-                        yacc = max(yacc, query("pcms_conv3_splits", cs.code, cin, sp) * nv[l] * cout)
+                        yacc = max(yacc, query("pcms_conv3_splits", cs.code, c0_ + c1_, sp) * nv[l] * cout)
                     if self.use_b16 and self.code == BF16:  # the level-3 16x16x32 split-K form
-                        yacc = max(yacc, query("pcms_conv3_fwd16_split_ok", N, *S[l], cin, 0, cout) * nv[l] * cout)
+                        yacc = max(yacc, query("pcms_conv3_fwd16_split_ok", N, *S[l], c0_, c1_, cout) * nv[l] * cout)
         b["yacc"] = torch.empty(yacc, dtype=torch.float32, device=dev)
         # partial rows of the head / ConvT-bias gradient reductions (summed in a fixed order)
         red = [query("pcms_head_bwd_ws_floats", D * H * W, N, self.ncls)]
@@ -746,6 +758,8 @@ class UNetEngine:
             rows = query("pcms_conv3_fwd16_rows", N, *S, c0, c1, cs.cout)
         elif cs.fwd16 is not None and (sp16 := query("pcms_conv3_fwd16_split_ok", N, *S, c0, c1, cs.cout)):
             acc = b["yacc"]
+            if sp16 * nvox * cs.cout > acc.numel():
+                raise RuntimeError("split-K workspace smaller than the 16x16x32 split form needs")
             call("pcms_conv3_fwd16_split", x0, c0, x1, c1, cs.fwd16, acc, N, *S, cs.cout, sp16)
             call("pcms_split_epilogue", self.code, acc, sp16, cs.mod.bias, y, None, cs.cout, st, cs.cout, nvox, 0)
             rows = query("pcms_split_epilogue_rows", nvox)
@@ -892,6 +906,9 @@ class UNetEngine:
         buffer (written by pcms_maxpool_bwd_bn), only its finish + apply run here."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
+        # the previous block's weight gradients (side stream) read this level's buffers until
+        # joined (a decoder and an encoder block share gY / gZ / gA at one level)
+        self._join_side()
         gY, gZ, gA = b[f"gY{lvl}"], b[f"gZ{lvl}"], b[f"gA{lvl}"]
         # BN1/ReLU backward -> dy2; its weight gradient on the side stream
         if ga2 is not None and bn1_rows:
@@ -959,6 +976,8 @@ class UNetEngine:
                  None, None, 0, N, *S, cs.cin, 1)
         elif cs.dgrad16 is not None and (sp16 := query("pcms_conv3_fwd16_split_ok", N, *S, cs.cout, 0, cs.cin)):
             acc = b["yacc"]
+            if sp16 * nvox * cs.cin > acc.numel():
+                raise RuntimeError("split-K workspace smaller than the 16x16x32 split form needs")
             call("pcms_conv3_fwd16_split", gy, cs.cout, None, 0, cs.dgrad16, acc, N, *S, cs.cin, sp16)
             call("pcms_split_epilogue", self.code, acc, sp16, None, out0, out1, cy0, None, cs.cin, nvox, 0)
         else:
@@ -1000,6 +1019,7 @@ class UNetEngine:
             l = 3 - i
             blk = self.dec[i]
             acts = self._dec_acts(l)
+            self._join_side()  # the recompute rewrites the shared set the side stream may still read
             if self.buf_key[4]:
                 self._block_fwd(blk, b[f"e{l}_x"], C[l], b[f"d{l}_u"], C[l], acts, N, S[l], True, recompute=True)
             gu = b[f"gU{l}"]
@@ -1034,4 +1054,5 @@ class UNetEngine:
                 call("pcms_maxpool_bwd_bn", self.code, b[f"e{l - 1}_y2"], bn.scale, bn.shift, bn.mean, bn.invstd, gp,
                      b[f"gx{l - 1}"], b["stats"], N, *S[l - 1], C[l - 1])
                 rows = query("pcms_maxpool_bwd_bn_rows", self.code, N, *S[l - 1], C[l - 1])
+        self._join_side()  # every weight gradient before the optimizer / all-reduce wait
         self.saved_epoch = -1

@@ -174,6 +174,7 @@ def check_step_against_fixture(params: dict, grads: dict, p0: dict, buffers: dic
     (after Adam / its gradients / before the step); ``buffers``: the GPU model's state dict."""
     nconf = ntot = 0
     worst = (0.0, "")
+    wbar = (0.0, "")
     for k in params:
         got = fixture_sampled(grads[k], fx, k)
         exp = torch.from_numpy(fx["g32__" + k]).double()
@@ -185,6 +186,7 @@ def check_step_against_fixture(params: dict, grads: dict, p0: dict, buffers: dic
             rl = float((got - t).norm()) / nrm
             rl_ref = float((exp - t).norm()) / nrm
             worst = max(worst, (rl, k))
+            wbar = max(wbar, (rl / max(grad_rl2, 10 * rl_ref), k))
             assert rl <= max(grad_rl2, 10 * rl_ref), (k, rl, rl_ref)
         pk = fixture_sampled(params[k], fx, k)
         pe = torch.from_numpy(fx["post__" + k]).double()
@@ -203,5 +205,25 @@ def check_step_against_fixture(params: dict, grads: dict, p0: dict, buffers: dic
         elif k.endswith("num_batches_tracked"):
             assert int(v) == int(fx["b__" + k]), k
     if report is not None:
-        report.update(worst_grad_rl2=worst, confident=nconf / max(ntot, 1))
+        report.update(worst_grad_rl2=worst, worst_grad_over_bar=wbar, confident=nconf / max(ntot, 1))
     assert nconf >= min_confident * ntot, (nconf, ntot)
+
+
+def record_margin(test: str, **vals):
+    """Append one JSON line {"test": ..., **vals} to the file $PCMS_MARGINS names (the parity
+    margins of the full-size tests: measured error / bar, so a green run also says how close
+    it came; profiles/r6_parity_margins.json is such a file).  No-op without the variable."""
+    path = os.environ.get("PCMS_MARGINS")
+    if not path:
+        return
+    import json
+
+    def plain(v):
+        if isinstance(v, (tuple, list)):
+            return [plain(x) for x in v]
+        if isinstance(v, (np.floating, np.integer)):
+            return v.item()
+        return v
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "a") as f:
+        f.write(json.dumps({"test": test, **{k: plain(v) for k, v in vals.items()}}) + "\n")

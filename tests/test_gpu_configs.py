@@ -19,11 +19,23 @@ on the GPU box's host.  Bars:
   2.01 lr everywhere and within 1e-5 relative on "confident" elements; BatchNorm running
   statistics within 1e-4 relative (gradients / parameters at 8192 strided positions per tensor).
 * bf16 build (bf16 storage cannot meet 1e-3): against the reference's fp32 run with
-  a bar set by the reference's OWN bf16-autocast run: max |dlogit| <= 2x the autocast run's (same
+  a bar set by the reference's bf16-autocast run: max |dlogit| <= 2x the autocast run's (same
   sampled positions), mask agreement >= the autocast run's - 0.5 % (every voxel), loss within
   2x the autocast run's loss error (floor 1e-3).  Configs 2, 4 and 5 (config 5: the
   decoder-checkpointed step, and every gradient within max(3x the autocast run's relative L2
   distance to the fp32 gradient, 2e-2)).
+* Dense windows (configs 2 and 4): besides the strided 2^18-position sample, every logit of the
+  volume faces and of the planes either side of the 8-voxel (d, h) / 16-voxel (w) box seams
+  (win_axis / win_index / w32__ / wbf__ in the fixture): fp32 within 1e-3, bf16 within 2x the
+  autocast run's largest error on the same planes.
+
+The autocast bar is not the reference's single-call arithmetic everywhere: oneDNN's CPU bf16
+conv backward faults past ~2^28 elements per call, so make_golden_full.py ran the layers the
+fixture's ``autocast_chunked`` lists (the level-0 convs at configs 2 / 4; those plus up3.conv.0
+and up4.up at config 5) over d-slabs, each slab casting its own operands (the same bf16 sums per
+output, slab partials of the weight gradients added in fp32).  Config 5's bf16 gradient bar
+comes only from such a run (no fp32 truth at that size): parity unpinned there in the strict
+sense, pinned to a slab-chunked autocast run of the reference's modules.
 """
 import pytest
 import torch
@@ -91,17 +103,47 @@ def test_fp32_build_matches_reference(fixture_run):
     mine = (lg > 0).reshape(-1)
     assert torch.equal(mine[sure], m32[sure])
     assert abs(loss - float(fx["loss32"])) <= 1e-5, (loss, float(fx["loss32"]))
+    werr = _window_errors(lg, fx)
+    if werr is not None:
+        assert werr <= 1e-3, werr
     rep = {}
     params = {k: p.detach().cpu() for k, p in m.named_parameters()}
     gu.check_step_against_fixture(params, grads, p0, m.state_dict(), fx, report=rep)
-    print(f"\n[{r['cfg']} fp32 vs reference] max|dlogit| {err:.2e}, worst grad rel-L2 "
+    print(f"\n[{r['cfg']} fp32 vs reference] max|dlogit| {err:.2e} (dense windows {werr}), worst grad rel-L2 "
           f"{rep['worst_grad_rl2'][0]:.2e} ({rep['worst_grad_rl2'][1]}), confident params {rep['confident']:.3f}")
+    gu.record_margin(f"{r['cfg']}_fp32", max_dlogit=err, logit_bar=1e-3, window_max_dlogit=werr,
+                     loss_err=abs(loss - float(fx["loss32"])), loss_bar=1e-5, worst_grad=rep["worst_grad_rl2"],
+                     worst_grad_over_bar=rep["worst_grad_over_bar"], confident=rep["confident"],
+                     masks_equal_where_sure=True)
+
+
+def _window_errors(lg, fx, tag="build"):
+    """max |logit - reference fp32 logit| over the fixture's dense planes: of the GPU logits
+    ``lg`` (tag "build") or of the reference's own autocast run (tag "bf"); None for a fixture
+    without planes."""
+    if "win_axis" not in fx:
+        return None
+    err = 0.0
+    for i, (ax, j) in enumerate(zip(fx["win_axis"], fx["win_index"])):
+        base = torch.from_numpy(fx[f"w32__{i}"]).double()
+        got = (lg.select(int(ax), int(j)).reshape(-1).double() if tag == "build"
+               else torch.from_numpy(fx[f"w{tag}__{i}"]).double())
+        err = max(err, float((got - base).abs().max()))
+    return err
 
 
 def test_bf16_build_within_bf16_bar(fixture_run):
     r = fixture_run
     _, lg, loss = _gpu_step("bf16", r["x"], r["y"])
-    _bf16_bar(lg, loss, r["fx"], r["cfg"])
+    marg = _bf16_bar(lg, loss, r["fx"], r["cfg"])
+    fx = r["fx"]
+    werr = _window_errors(lg, fx)
+    if werr is not None:
+        wauto = _window_errors(None, fx, "bf")
+        print(f"[{r['cfg']} bf16] dense windows max|dlogit| {werr:.4f} (autocast {wauto:.4f})")
+        assert werr <= 2 * wauto, (werr, wauto)
+        marg.update(window_max_dlogit=werr, window_autocast=wauto)
+    gu.record_margin(f"{r['cfg']}_bf16", **marg)
 
 
 def test_config2_full_step_deterministic():
@@ -155,22 +197,27 @@ def _bf16_bar(lg, loss, fx, tag):
     assert e <= 2 * e_auto, (e, e_auto)
     assert agree >= agree_auto - 0.005, (agree, agree_auto)
     assert abs(loss - loss32) <= max(2 * abs(lossbf - loss32), 1e-3), (loss, loss32, lossbf)
+    return {"max_dlogit": e, "autocast_max_dlogit": e_auto, "dlogit_over_bar": e / (2 * e_auto),
+            "mask_agree": agree, "autocast_mask_agree": agree_auto, "loss_err": abs(loss - loss32),
+            "loss_bar": max(2 * abs(lossbf - loss32), 1e-3),
+            "autocast_chunked": [str(v) for v in fx["autocast_chunked"]] if "autocast_chunked" in fx else None}
 
 
 def test_config5_checkpointed_bf16_vs_reference():
     """Config 5 (1 x 5x256x256x96, decoder checkpointing, bf16) against the reference's step at
     that shape (tests/golden/full_cfg5.npz) with the autocast-relative bf16 bar (train logits /
     masks / loss as at configs 2 and 4), and every gradient: its relative L2 distance to the
-    reference's fp32 gradient within max(3x the reference's own bf16-autocast run's distance,
-    2e-2), on the fixture's sample positions (pre-BN conv biases, exact gradient 0, SURVEY H5:
-    within 1e-4 absolute)."""
+    reference's fp32 gradient within max(3x the reference's bf16-autocast run's distance, 2e-2),
+    on the fixture's sample positions (pre-BN conv biases, exact gradient 0, SURVEY H5: within
+    1e-4 absolute).  Parity unpinned in the strict sense: the autocast run that sets the bar is
+    slab-chunked at the six layers ``autocast_chunked`` lists (module docstring)."""
     fx = gu.full_fixture("cfg5")
     x, y = gu.full_batch("cfg5")
     assert abs(float(x.double().sum()) - float(fx["input_sum"])) <= 1e-6 * abs(float(fx["input_sum"]))
     m, lg, loss, grads = _gpu_step("bf16", x, y, ckpt=True, keep_grad=True)
     del m
     torch.cuda.empty_cache()
-    _bf16_bar(lg, loss, fx, "cfg5 ckpt")
+    marg = _bf16_bar(lg, loss, fx, "cfg5 ckpt")
     worst = (0.0, "")
     rows = []
     for k, g in grads.items():
@@ -188,5 +235,6 @@ def test_config5_checkpointed_bf16_vs_reference():
     for k, rl, rl_auto in rows:
         print(f"  {k:48s} rel-L2 {rl:.3e} (reference autocast {rl_auto:.3e})")
     print(f"[cfg5 ckpt bf16 vs reference] worst gradient rel-L2 / bar {worst[0]:.3f} ({worst[1]})")
+    gu.record_margin("cfg5_ckpt_bf16", worst_grad_over_bar=worst, **marg)
     for k, rl, rl_auto in rows:
         assert rl <= max(3 * rl_auto, 2e-2), (k, rl, rl_auto)

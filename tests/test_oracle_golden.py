@@ -83,3 +83,32 @@ def test_full_fixtures_pinned(cfg):
     n = x.shape[0] * x.shape[2] * x.shape[3] * x.shape[4]
     assert fx["m32_bits"].size == (n + 7) // 8
     assert float(fx["e_auto"]) > 0 and 0.9 < float(fx["agree_auto"]) <= 1.0
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg4"])
+def test_full_fixture_windows_agree_with_sample(cfg):
+    """The dense logit planes (make_golden_full.py add_windows: a second run of the reference's
+    forward) hold the same numbers as the strided sample of the original step where the two
+    meet: the d = 0 plane of sample 0 is flat[0 : H W], the sample's first H W / stride
+    entries."""
+    fx = gu.full_fixture(cfg)
+    ls = int(fx["logit_stride"])
+    _, (D, H, W), _ = gu.FULL_CFGS[cfg]
+    assert int(fx["win_axis"][0]) == 2 and int(fx["win_index"][0]) == 0
+    for tag in ("32", "bf"):
+        plane = fx[f"w{tag}__0"][:H * W]          # sample 0, d = 0
+        np.testing.assert_array_equal(plane[::ls], fx[f"l{tag}_s"][:(H * W + ls - 1) // ls])
+    assert len(fx["win_axis"]) == len(fx["win_index"]) == sum(1 for k in fx if k.startswith("w32__"))
+
+
+def test_dp3_fixture_autocast_run():
+    """full_dp3.npz holds the reference's two-rank step under CPU bf16 autocast as well
+    (make_golden_full.py add_dp3_autocast): per-replica losses near the fp32 ones, the mean
+    autocast gradient at every sampled tensor, rank 0's buffers, and the slab-chunked layers."""
+    fx = gu.full_fixture("dp3")
+    assert fx["lossesbf"].shape == fx["losses32"].shape == (2,)
+    assert np.all(np.abs(fx["lossesbf"] - fx["losses32"]) < 1e-2)
+    g32 = [k[5:] for k in fx if k.startswith("g32__")]
+    assert g32 and all("gbf__" + k in fx and fx["gbf__" + k].shape == fx["g32__" + k].shape for k in g32)
+    assert all("bbf__" + k[3:] in fx for k in fx if k.startswith("b__"))
+    assert "inc.conv.0" in list(fx["autocast_chunked"])

@@ -10,6 +10,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, REPO)
 
 SPATIAL = tuple(int(v) for v in os.environ.get("PCMS_DP_SPATIAL", "32,32,16").split(","))
+# the engine build (PCMS_DP_PRECISION: "fp32" parity build, "bf16" the product build BASELINE
+# configs 3 / 5 name) and config 5's decoder activation checkpointing (PCMS_DP_CKPT=1)
+PRECISION = os.environ.get("PCMS_DP_PRECISION", "fp32")
+CKPT = os.environ.get("PCMS_DP_CKPT", "0") == "1"
 
 
 def main():
@@ -22,11 +26,13 @@ def main():
     from pcms_amd.utils.trainer import Trainer
     torch.manual_seed(0)
     cfg = {"device": "cuda:0", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1, "loss": "bce_dice",
-           "precision": "fp32", "dp_bucket_elems": 4 << 20, "max_grad_norm": float(os.environ.get("CLIP", "0")) or None}
+           "precision": PRECISION, "checkpoint_decoder": CKPT, "dp_bucket_elems": 4 << 20,
+           "max_grad_norm": float(os.environ.get("CLIP", "0")) or None}
     if os.environ.get("MODE") == "train":
         return train_mode(rank, world, out, Trainer)
     tr = Trainer(cfg)
     assert tr.distributed and tr.world_size == world
+    assert tr.model.precision == PRECISION and tr.model.checkpoint_decoder == CKPT, (tr.model.precision, CKPT)
     losses = []
     for s in range(int(os.environ.get("PCMS_DP_STEPS", "1"))):
         b = make_batch(2, SPATIAL, seed=step_seed(rank, s), label="bernoulli")
