@@ -107,6 +107,10 @@ int pcms_conv3_wgrad_tg_maxbox(int v);
  * v_mfma_f32_16x16x32_bf16 (1) or v_mfma_f32_32x32x16_bf16 (0, default); v < 0 queries;
  * returns the previous setting (A/B switch) */
 int pcms_conv3_wgrad_k16(int v);
+/* fp32 (bf16x6) weight gradient: boxes streamed by LDS-DMA into an fp32 staging buffer beside
+ * the previous box's MFMAs (1) or staged synchronously through registers (0, default: measured
+ * as fast); v < 0 queries; returns the previous setting (A/B switch) */
+int pcms_conv3_wgrad_x6_dma(int v);
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, int flags, hipStream_t s);

@@ -438,6 +438,11 @@ constexpr int kWThreads = 512;          // 8 waves: wave = (co-tile, tap-group)
 #ifndef WGRAD_ABL
 #define WGRAD_ABL 0
 #endif
+// A/B builds: bit 0 s_setprio 1 for waves 4-7 of the weight gradient, bit 1 of the 8-deep
+// 16x16x32 conv (MI355X_MICROARCH.md, two waves per SIMD item 4); 0 in the product
+#ifndef PCMS_SETPRIO
+#define PCMS_SETPRIO 0
+#endif
 constexpr int kWHaloMax = 720;          // halo rows (box <= 256 voxels)
 
 template <typename T> struct WTraits;
@@ -453,14 +458,20 @@ template <> struct WTraits<bf16_t> {
   typedef s16x8_t Frag;
 };
 template <> struct WTraits<x6_t> {
-  static constexpr int BV = 128;        // voxels per staged box (h, m, l tiles: 3 x 43 KB)
+  // boxes of <= 64 voxels (round 6): the h, m, l tiles (3 x 24 KB) plus the fp32 LDS-DMA
+  // target of the NEXT box (48 KB) fit in LDS, so the box stream no longer stops the MFMAs
+  static constexpr int BV = 64;         // voxels per staged box
   static constexpr int KV = 8;          // voxels per MFMA k-step (K halves concatenated)
   static constexpr int NBUF = 1;
   static constexpr int DYROW = 128;
   static constexpr int XROW = 64;
   static constexpr int VEC = 4;
-  static constexpr int HALO = 432;
+  static constexpr int HALO = 256;
   static constexpr int NPART = 3;
+  // the fp32 box as it arrives by LDS-DMA: dy [BV][64 co] then the x halo [HALO][32 ci] (+ one
+  // wave-instruction of slack: a halo's last DMA may run past its rows, reading zeros)
+  static constexpr int RAWDY = BV * 64 * 4;
+  static constexpr int RAWBYTES = RAWDY + (HALO * 8 + 64) * 16;
   typedef s16x8_t Frag;
 };
 template <> struct WTraits<x3_t> {
@@ -518,6 +529,10 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hsel = lane >> 5;
+#if PCMS_SETPRIO & 1
+  // static priority for the second-dispatched half (waves 4-7: each SIMD's younger wave)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   // wave w owns taps w, w + 8, w + 16 (, w + 24) for BOTH co tiles, so each B (x) fragment
   // feeds 2 MFMAs: 1.5 LDS reads per MFMA instead of 2.3 (8 accumulators)
   // fp32 data, split-bf16 products: x3 (hi, lo tiles) / x6 (h, m, l tiles), the parts
@@ -693,6 +708,71 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           *reinterpret_cast<u32x2_t*>(buf + BUFBYTES + off) = (u32x2_t){h01[1], h23[1]};
         }
       }
+    }
+  };
+
+  // fp32 build with LDS-DMA (p.dma): the box's fp32 dy tile and x halo into the raw buffer
+  // after the part tiles (16-B pieces, one wave-instruction of 64 consecutive pieces each;
+  // padding / out-of-volume pieces read zeros), and the split of the landed box into the tiles
+  auto stage_raw = [&](int b) __attribute__((always_inline)) {
+    if constexpr (kX6) {
+      int n, d0, h0, w0;
+      box_origin(b, n, d0, h0, w0);
+      const uint32_t lb0 = lds_addr(wlds + Tr::NPART * BUFBYTES);
+      const bool first = ci_base < p.c0;  // a 32-channel block lies in one source
+      const i32x4_t xr = buffer_desc(first ? p.x0 : p.x1, first ? p.x0bytes : p.x1bytes);
+      const i32x4_t dr = buffer_desc(p.dy, p.dybytes);
+      const int xs = first ? p.c0 : p.c1, xc = first ? ci_base : ci_base - p.c0;
+      constexpr int DYQ = Tr::BV * 16;  // 16 pieces of 4 fp32 per voxel (64 co)
+      constexpr int RP = (DYQ + Tr::HALO * 8 + kWThreads - 1) / kWThreads;
+      static_assert(DYQ % 64 == 0, "dy pieces in whole wave-instructions");
+      const int XQ = HV * 8;            // 8 pieces per halo voxel (32 ci)
+#pragma unroll
+      for (int i = 0; i < RP; ++i) {
+        const int pc0 = (tid & ~63) + i * kWThreads;  // wave-uniform first piece
+        if (pc0 >= DYQ + XQ) break;
+        const int pc = pc0 + lane;
+        uint32_t voff = kOOB;
+        if (pc0 < DYQ) {
+          const int r = pc >> 4, q = pc & 15;
+          if (r < boxvol) {
+            const int rd = r >> (lbh_ + lbw_), rh = (r >> lbw_) & (bh - 1), rw = r & (bw - 1);
+            const int gd = d0 + rd, gh = h0 + rh, gw = w0 + rw;
+            if (gd < p.D && gh < p.H && gw < p.W)
+              voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * p.Cout + co_base + q * 4) * 4);
+          }
+          dma16(dr, __builtin_amdgcn_readfirstlane(lb0 + pc0 * 16), voff, 0);
+        } else {
+          const int hp = pc - DYQ, hv = hp >> 3, q = hp & 7;
+          const int hw_ = hv % HW, t_ = hv / HW, hh_ = t_ % HH, hd_ = t_ / HH;
+          const int gd = d0 + hd_ - 1, gh = h0 + hh_ - 1, gw = w0 + hw_ - 1;
+          if (hp < XQ && gd >= 0 && gd < p.D && gh >= 0 && gh < p.H && gw >= 0 && gw < p.W && xc + q * 4 < xs)
+            voff = (uint32_t)(((((n * p.D + gd) * p.H + gh) * p.W + gw) * xs + xc + q * 4) * 4);
+          dma16(xr, __builtin_amdgcn_readfirstlane(lb0 + Tr::RAWDY + (pc0 - DYQ) * 16), voff, 0);
+        }
+      }
+    } else {
+      (void)b;
+    }
+  };
+  auto split_raw = [&](char* buf) __attribute__((always_inline)) {
+    if constexpr (kX6) {
+      const char* raw = wlds + Tr::NPART * BUFBYTES;
+      constexpr int DYQ = Tr::BV * 16;
+      const int XQ = HV * 8;
+      for (int pc = tid; pc < DYQ + XQ; pc += kWThreads) {
+        const bool isdy = pc < DYQ;
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(isdy ? raw + pc * 16 : raw + Tr::RAWDY + (pc - DYQ) * 16);
+        const int off = isdy ? dy_off_bf16(pc >> 4, (pc & 15) * 4) : DYBYTES + (pc - DYQ) * 8;
+        const float f[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
+        u32x4_t h, m, l;
+        split3x8(f, h, m, l);
+        *reinterpret_cast<u32x2_t*>(buf + off) = (u32x2_t){h[0], h[1]};
+        *reinterpret_cast<u32x2_t*>(buf + BUFBYTES + off) = (u32x2_t){m[0], m[1]};
+        *reinterpret_cast<u32x2_t*>(buf + 2 * BUFBYTES + off) = (u32x2_t){l[0], l[1]};
+      }
+    } else {
+      (void)buf;
     }
   };
 
@@ -1121,7 +1201,7 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
     __syncthreads();
   }
 
-  if (b_beg < b_end && p.dma) {
+  if (!kX6 && b_beg < b_end && p.dma) {
     if constexpr (Tr::NBUF == 2) {
       uint32_t xm = stage_dma(wlds, b_beg);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1172,6 +1252,23 @@ __global__ void __launch_bounds__(kWThreads, 1) conv3_wgrad_kernel(WgradParams p
           compute_box(wlds + cur * BUFBYTES, nomid, stage);
         }
         if constexpr (!(WGRAD_ABL & 8)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else if (kX6 && b_beg < b_end && p.dma) {
+    if constexpr (kX6) {
+      // fp32 build (bf16x6) with LDS-DMA: box b + 1 streams into the fp32 staging buffer while
+      // box b's MFMAs run on its split tiles; between boxes every thread splits its pieces of
+      // the landed box into the h / m / l tiles (the values stage_x3 writes)
+      stage_raw(b_beg);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int b = b_beg; b < b_end; ++b) {
+        split_raw(wlds);
+        __syncthreads();
+        if (b + 1 < b_end) stage_raw(b + 1);
+        compute(wlds);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
     }
@@ -2190,6 +2287,9 @@ __global__ void __launch_bounds__(BD * 64, 1) conv3_fwd_b16_kernel(Conv3Params p
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#if PCMS_SETPRIO & 2
+  if (BD == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);  // the younger wave of each SIMD pair
+#endif
   const int Cout = p.Cout, ncob = Cout / CO;
   const int G = gridDim.x;
   const int lg = (G & 7) == 0 ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
@@ -3117,6 +3217,11 @@ static int g_wgrad_tg_maxbox = 64;
 // compile-time-box bf16 weight gradients on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0, the
 // product: the 16x16x32 form ran at a higher clock but slower, profiles/r5_wgrad_k16_abl.txt)
 static int g_wgrad_k16 = 0;
+// the fp32 build's weight gradient streams its boxes by LDS-DMA into an fp32 staging buffer (1)
+// or stages each box synchronously through registers (0, the product): with the 64-voxel boxes
+// of round 6 both run the fp32 step in the same time (66.5 vs 66.2 ms, profiles/r6_x6_ab.txt) --
+// the kernel is bound by its LDS fragment reads, not by the box stream
+static int g_wgrad_x6_dma = 0;
 struct WgradPlan { Box b; int nbd, nbh, nbw, nbox, bps, splits, ntg; };
 static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int Cout, int target_wgs) {
   WgradPlan q;
@@ -3139,6 +3244,14 @@ static WgradPlan wgrad_plan(int dtype, int N, int D, int H, int W, int Cin, int 
 int pcms_conv3_wgrad_k16(int v) {
   const int old = g_wgrad_k16;
   if (v >= 0) g_wgrad_k16 = v;
+  return old;
+}
+
+// the fp32 (bf16x6) weight gradient's LDS-DMA box stream (1) or synchronous staging (0); v < 0
+// queries.  Returns the previous value.
+int pcms_conv3_wgrad_x6_dma(int v) {
+  const int old = g_wgrad_x6_dma;
+  if (v >= 0) g_wgrad_x6_dma = v;
   return old;
 }
 
@@ -3208,10 +3321,13 @@ static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, in
   p.nbox = q.nbox;
   p.boxes_per_split = q.bps;
   const long nvox = (long)N * D * H * W;
-  p.dma = dtype == PCMS_BF16 && (c1 == 0 || c0 % 32 == 0) && nvox * std::max(Cout, std::max(c0, c1)) * 2 < (long)kOOB;
-  p.x0bytes = (uint32_t)(nvox * c0 * 2);
-  p.x1bytes = (uint32_t)(nvox * c1 * 2);
-  p.dybytes = (uint32_t)(nvox * Cout * 2);
+  // LDS-DMA staging: bf16, and the fp32 (bf16x6) build's fp32 staging buffer (g_wgrad_x6_dma)
+  const int es = dtype == PCMS_BF16 ? 2 : 4;
+  p.dma = (dtype == PCMS_BF16 || (dtype == PCMS_F32 && g_wgrad_x6_dma)) && (c1 == 0 || c0 % 32 == 0) &&
+          nvox * std::max(Cout, std::max(c0, c1)) * es < (long)kOOB;
+  p.x0bytes = (uint32_t)(p.dma ? nvox * c0 * es : 0);
+  p.x1bytes = (uint32_t)(p.dma ? nvox * c1 * es : 0);
+  p.dybytes = (uint32_t)(p.dma ? nvox * Cout * es : 0);
   const int splits = q.splits;
   p.nco = Cout / 64;
   p.nci = cdiv(Cin, 32);
@@ -3261,7 +3377,7 @@ static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, in
     hipLaunchKernelGGL((conv3_wgrad_kernel<x3_t, -1, -1, -1>), grid, dim3(kWThreads), lds, s, p);
   } else {
     typedef WTraits<x6_t> X;
-    lds = (size_t)X::NPART * (X::BV * X::DYROW + X::HALO * X::XROW);
+    lds = (size_t)X::NPART * (X::BV * X::DYROW + X::HALO * X::XROW) + (p.dma ? X::RAWBYTES : 0);
     auto kern = Cin <= 8 ? conv3_wgrad_kernel<x6_t, -1, -1, -1, false, true> : conv3_wgrad_kernel<x6_t, -1, -1, -1>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);

@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 
 def main():
-    ks = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,8,16,32").split(",")]
+    ks = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,4,8,32").split(",")]
     import pcms_amd  # noqa: F401
     from pcms_amd.synthetic import make_batch
     from pcms_amd.utils.trainer import Trainer
@@ -34,6 +34,25 @@ def main():
     for _ in range(3):
         tr.step(batch)
     torch.cuda.synchronize()
+    # per-launch cost with a kernel resident on another queue: 400 dependent tiny launches (a
+    # 4-element fill) on the compute stream, with and without one hog workgroup beside them
+    tiny = torch.zeros(4, device="cuda")
+    for k in sorted(set([0, 1] + ks)):
+        ts = []
+        for _ in range(3):
+            side.wait_stream(torch.cuda.current_stream())
+            hog.cu_hog(k, 4000.0, sink.data_ptr(), side.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(400):
+                tiny.add_(1.0)
+            e1.record()
+            e1.synchronize()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3 / 400)
+        print(f"hog {k:3d} CUs:  {statistics.median(ts):6.2f} us per dependent tiny launch (all {[round(t, 2) for t in ts]})",
+              flush=True)
     for k in ks:
         ts = []
         for _ in range(5):

@@ -361,6 +361,26 @@ def test_conv3_wgrad_k16(k16, N, c0, c1, cout, S):
         L.query("pcms_conv3_wgrad_k16", old)
 
 
+@pytest.mark.parametrize("x6dma", [1, 0])
+@pytest.mark.parametrize("N,c0,c1,cout,S", [
+    (2, 64, 64, 64, (24, 20, 40)),     # two sources, ragged edges: ~10 boxes per workgroup
+    (2, 8, 0, 64, (32, 32, 32)),       # stem channels (4 taps x 8 channels per MFMA column)
+    (1, 256, 0, 128, (16, 16, 8)),     # deep-level channel counts
+])
+def test_conv3_wgrad_x6_box_stream(x6dma, N, c0, c1, cout, S):
+    """fp32 build (bf16x6) weight gradient over many boxes per workgroup: the round-6 box
+    stream (fp32 boxes by LDS-DMA into a staging buffer beside the previous box's MFMAs, split
+    into the h / m / l tiles between boxes) and the synchronous register staging
+    (pcms_conv3_wgrad_x6_dma(0)), both vs fp64 autograd at the fp32 build's bar."""
+    L = _lib()
+    old = L.query("pcms_conv3_wgrad_x6_dma", x6dma)
+    try:
+        for store in (1, 0):
+            _wgrad_case(L, torch.float32, 0, N, c0, c1, cout, S, store)
+    finally:
+        L.query("pcms_conv3_wgrad_x6_dma", old)
+
+
 @pytest.mark.parametrize("c0,c1,S", [(64, 0, (32, 32, 32)), (32, 32, (24, 20, 40))])
 def test_conv3_wgrad_many_boxes(c0, c1, S):
     """bf16 weight gradient over a grid of many boxes (the level-0..2 voxel-split plan, partial

@@ -5,7 +5,8 @@ variant alike; HIP events around K back-to-back steps, median over rounds.
     python tests/tools/step_ab.py [--rounds 4] [--steps 10] [--variants base,nobnin,...]
 
 Variants: base (the defaults), nobnin (engine.fuse_bnin off), densewg (stem weight gradient
-in the dense-column form), split256 / split512 (engine.split_target)."""
+in the dense-column form), split256 / split512 (engine.split_target), x6sync / x6dma (the fp32
+build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32)."""
 import argparse
 import os
 import statistics
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--variants", default="base,nobnin,densewg")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
     from pcms_amd import _lib as L
@@ -28,16 +30,18 @@ def main():
     from pcms_amd.utils.trainer import Trainer
     torch.manual_seed(0)
     tr = Trainer({"device": "cuda", "learning_rate": 1e-4, "batch_size": 2, "num_epochs": 1,
-                  "loss": "bce_dice", "precision": "bf16"})
+                  "loss": "bce_dice", "precision": a.precision})
     eng = tr.model.engine()
     b = make_batch(2, (128, 128, 64), seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
     dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target}
     dense0 = L.query("pcms_stem_wgrad_dense", -1)
+    x6dma0 = L.query("pcms_conv3_wgrad_x6_dma", -1)
 
     def setup(v):
         eng.fuse_bnin, eng.split_target = dflt["fuse_bnin"], dflt["split_target"]
         L.query("pcms_stem_wgrad_dense", dense0)
+        L.query("pcms_conv3_wgrad_x6_dma", x6dma0)
         if v == "nobnin":
             eng.fuse_bnin = False
         elif v == "bnin":
@@ -46,6 +50,8 @@ def main():
             L.query("pcms_stem_wgrad_dense", 1)
         elif v == "tapswg":
             L.query("pcms_stem_wgrad_dense", 0)
+        elif v in ("x6sync", "x6dma"):  # the fp32 build's weight-gradient box stream
+            L.query("pcms_conv3_wgrad_x6_dma", int(v == "x6dma"))
         elif v.startswith("split"):
             eng.split_target = int(v[5:])
         elif v != "base":
