@@ -76,6 +76,9 @@ def main():
     ap.add_argument("--big-min-boxes", type=int, default=0, help="pcms_conv3_big_min_boxes override")
     ap.add_argument("--fwd-box-vol", type=int, default=0, help="pcms_conv3_fwd_box_vol override (256)")
     ap.add_argument("--convt-taps", type=int, default=0, help="pcms_convt_wgrad_taps override (8 / 4 / 2)")
+    ap.add_argument("--hog", type=int, default=0,
+                    help="K spinning workgroups (tests/kexp/libcuhog.so) holding K CUs on a side stream during every "
+                         "recorded step: what an RCCL kernel beside the backward does to each launch")
     ap.add_argument("--clock", action="store_true",
                     help="bracket every launch with bench.ClockProbe stamps: the shader clock per launch and the MFMA "
                          "fraction at that clock (the stamps add a few us of launches between layers)")
@@ -134,9 +137,19 @@ def main():
         v = list(bench.ClockProbe.mhz(c0, c1).values())
         return statistics.median(v) if v else None
 
+    hog = side = sink = None
+    if a.hog:
+        import ctypes
+        hog = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kexp", "libcuhog.so"))
+        hog.cu_hog.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
+        side = torch.cuda.Stream()
+        sink = torch.zeros(64, dtype=torch.int32, device="cuda")
     per = []
     for _ in range(a.steps):
         rec.clear()
+        if hog is not None:
+            side.wait_stream(torch.cuda.current_stream())
+            hog.cu_hog(a.hog, 30000.0, sink.data_ptr(), side.cuda_stream)
         tr.step(batch)
         torch.cuda.synchronize()
         per.append([(n, ar, s.elapsed_time(e) * 1e3, clk(c0, c1)) for n, ar, s, e, c0, c1 in rec])
