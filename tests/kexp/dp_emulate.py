@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--policies", default="none,overlap,end")
+    ap.add_argument("--buckets", default="16", help="bucket sizes to compare (Mi elements, comma list): the "
+                    "overlap policy is run once per size")
     a = ap.parse_args()
     import pcms_amd  # noqa: F401
     from pcms_amd.synthetic import make_batch
@@ -85,8 +87,17 @@ def main():
     x, y = b["image"].cuda(), b["label"].cuda()
     sink = torch.zeros(64, dtype=torch.int32, device="cuda")
     n = eng.flat_g.numel()
-    syncs = {p: FakeSync(hog, n, a.k, a.world, a.busbw, a.lat, 16 << 20, 1 << 20, p == "overlap", sink)
-             for p in ("overlap", "end")}
+    syncs = {"end": FakeSync(hog, n, a.k, a.world, a.busbw, a.lat, 16 << 20, 1 << 20, False, sink)}
+    pols = []
+    for p in a.policies.split(","):
+        if p == "overlap":
+            for bm in a.buckets.split(","):
+                name = f"overlap{bm}M"
+                syncs[name] = FakeSync(hog, n, a.k, a.world, a.busbw, a.lat, int(float(bm) * (1 << 20)),
+                                       min(1 << 20, int(float(bm) * (1 << 20))), True, sink)
+                pols.append(name)
+        else:
+            pols.append(p)
 
     def step(pol):
         tr.optimizer.zero_grad()
@@ -101,7 +112,6 @@ def main():
             s.finish()
         tr.optimizer.step()
 
-    pols = a.policies.split(",")
     res = {p: [] for p in pols}
     for r in range(a.rounds):
         for p in pols:
