@@ -3378,6 +3378,8 @@ static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, in
   } else {
     typedef WTraits<x6_t> X;
     lds = (size_t)X::NPART * (X::BV * X::DYROW + X::HALO * X::XROW) + (p.dma ? X::RAWBYTES : 0);
+    // the direct (one-split) flush transposes a [32 co][32 ci][27] fp32 tile through LDS
+    if (p.direct) lds = std::max(lds, (size_t)32 * 32 * 27 * sizeof(float));
     auto kern = Cin <= 8 ? conv3_wgrad_kernel<x6_t, -1, -1, -1, false, true> : conv3_wgrad_kernel<x6_t, -1, -1, -1>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(kWThreads), lds, s, p);

@@ -366,6 +366,8 @@ def test_conv3_wgrad_k16(k16, N, c0, c1, cout, S):
     (2, 64, 64, 64, (24, 20, 40)),     # two sources, ragged edges: ~10 boxes per workgroup
     (2, 8, 0, 64, (32, 32, 32)),       # stem channels (4 taps x 8 channels per MFMA column)
     (1, 256, 0, 128, (16, 16, 8)),     # deep-level channel counts
+    (2, 512, 0, 1024, (1, 1, 1)),      # level 4 of a 16^3 volume: 256 tiles, one split (direct flush)
+    (2, 512, 512, 512, (2, 2, 2)),     # level 3 of a 16^3 volume, two sources
 ])
 def test_conv3_wgrad_x6_box_stream(x6dma, N, c0, c1, cout, S):
     """fp32 build (bf16x6) weight gradient over many boxes per workgroup: the round-6 box
