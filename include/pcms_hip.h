@@ -111,6 +111,10 @@ int pcms_conv3_wgrad_k16(int v);
  * the previous box's MFMAs (1) or staged synchronously through registers (0, default: measured
  * as fast); v < 0 queries; returns the previous setting (A/B switch) */
 int pcms_conv3_wgrad_x6_dma(int v);
+/* the weight gradient's per-split partial rows summed in one launch (1, default) or by the
+ * group-sum + reduce pair (0); the sums are bit-identical; v < 0 queries; returns the previous
+ * setting (A/B switch) */
+int pcms_conv3_wgrad_reduce_fused(int v);
 int pcms_conv3_wgrad(int dtype, const void* x0, int c0, const void* x1, int c1, const void* dy,
                      float* dw, float* dwt, int N, int D, int H, int W, int Cout, int cin_w,
                      int target_wgs, int flags, hipStream_t s);

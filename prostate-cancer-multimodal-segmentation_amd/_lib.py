@@ -37,6 +37,7 @@ SIGNATURES = {
     "pcms_conv3_wgrad_tg_maxbox": "i",
     "pcms_conv3_wgrad_k16": "i",
     "pcms_conv3_wgrad_x6_dma": "i",
+    "pcms_conv3_wgrad_reduce_fused": "i",
     "pcms_conv3_big16_ok": "iiiiiii",
     "pcms_conv3_fwd16_rows": "iiiiiii",
     "pcms_conv3_b16_nt8": "i",

@@ -1475,6 +1475,73 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, in
   for (int e = threadIdx.x; e < n; e += 256) dst[e] = store ? tile[e % 27][e / 27] : dst[e] + tile[e % 27][e / 27];
 }
 
+// Both stages in one launch, same sums bit for bit: the S split rows as G = ceil(S / 16)
+// groups of 16, each group summed in row order by one thread, the G group sums then added in
+// group order (= wgrad_group_sum_kernel + wgrad_reduce_kernel).  Block = (co, 32 channels) x
+// GL group lanes: 256 element lanes (up to 4 of the 864 [27][32] elements each) per group
+// lane, all of a group's rows for all of a thread's elements loaded before the first add
+// (the two-stage form was a 57 MB pass plus a latency-bound 3.5 MB pass per level-0/1 layer).
+// LDS: the [G][27 x 32] group sums.
+constexpr int kWredMaxGroups = 16;  // and 16 rows x E floats per group below 2 GB (host check)
+static int g_wred_fused = 1;  // 0: the two-stage reduction (A/B, bit-identity test)
+template <int GL>
+__global__ void __launch_bounds__(256 * GL) wgrad_reduce_fused_kernel(const float* part, int S, float* dw, int Cout,
+                                                                      int Cin, int Cw, int store) {
+  extern __shared__ float gsum[];  // [G][864]
+  constexpr int NE = 27 * 32;
+  const int co = blockIdx.x, ci0 = blockIdx.y * 32;
+  const long E = 27L * Cout * Cin;
+  const int G = (S + 15) / 16;
+  const int el = threadIdx.x & 255, gl = threadIdx.x >> 8;
+  // 32-bit byte offsets from the group's (uniform) first row: 16 rows x E floats < 2 GB
+  uint32_t off[4];
+  bool ok[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = el + 256 * k, t = e >> 5, c = e & 31;
+    ok[k] = e < NE && ci0 + c < Cw;
+    off[k] = ok[k] ? (uint32_t)((((long)t * Cout + co) * Cin + ci0 + c) * 4) : 0u;
+  }
+  const uint32_t rowb = (uint32_t)(E * 4);
+  for (int g = gl; g < G; g += GL) {
+    const int r0 = g * 16, n = min(16, S - r0);
+    // the group's rows through a descriptor: row offset in the SGPR soffset, element offset in
+    // one VGPR (a 64-bit address per load held 128 VGPRs of addresses)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(part + (long)r0 * E), (short)0, (int)(n * rowb), 0x00020000);
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 16; h += 8) {  // 8 rows x 4 elements in flight, added in row order
+      float v[4][8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (h + r < n && ok[k])
+            v[k][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off[k], (int)((h + r) * rowb), 0));
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (h + r < n && ok[k]) s[k] += v[k][r];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = el + 256 * k;
+      if (e < NE) gsum[g * NE + e] = s[k];
+    }
+  }
+  __syncthreads();
+  float* dst = dw + ((long)co * Cw + ci0) * 27;
+  const int n = min(32, Cw - ci0) * 27;
+  for (int o = threadIdx.x; o < n; o += 256 * GL) {
+    const int c = o / 27, t = o % 27, e = t * 32 + c;
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += gsum[g * NE + e];
+    dst[o] = store ? s : dst[o] + s;
+  }
+}
+
 // master fp32 W[Cout][Cin][27] -> packed T [chunk][27][J][CK]
 //   fwd  (flip=0): J = Cout, k-index = ci
 //   dgrad(flip=1): J = Cin,  k-index = co, tap mirrored (26 - t)
@@ -3255,6 +3322,14 @@ int pcms_conv3_wgrad_x6_dma(int v) {
   return old;
 }
 
+// the weight gradient's split rows summed by one launch (1) or by the two-stage group-sum +
+// reduce pair (0), bit-identical; v < 0 queries.  Returns the previous value.
+int pcms_conv3_wgrad_reduce_fused(int v) {
+  const int old = g_wred_fused;
+  if (v >= 0) g_wred_fused = v;
+  return old;
+}
+
 // grids of at most v boxes split the taps of the bf16 weight gradient over two workgroups
 // before splitting the voxels (0: never); v < 0 queries.  Returns the previous value.
 int pcms_conv3_wgrad_tg_maxbox(int v) {
@@ -3388,6 +3463,21 @@ static int conv3_wgrad_any(int dtype, const void* x0, int c0, const void* x1, in
   if (e != hipSuccess) return (int)e;
   if (p.direct) return 0;  // the kernel added into dw itself
   const long E = 27L * Cout * Cin;
+  const int G = cdiv(splits, 16);
+  if (g_wred_fused && G <= kWredMaxGroups && E * 16 * 4 < (1L << 31)) {
+    const dim3 grid(Cout, cdiv(cin_w, 32));
+    const size_t glds = (size_t)G * 27 * 32 * sizeof(float);
+    if (G >= 4)
+      hipLaunchKernelGGL(wgrad_reduce_fused_kernel<4>, grid, dim3(1024), glds, s, (const float*)dwt, splits, dw, Cout,
+                         Cin, cin_w, p.store);
+    else if (G >= 2)
+      hipLaunchKernelGGL(wgrad_reduce_fused_kernel<2>, grid, dim3(512), glds, s, (const float*)dwt, splits, dw, Cout,
+                         Cin, cin_w, p.store);
+    else
+      hipLaunchKernelGGL(wgrad_reduce_fused_kernel<1>, grid, dim3(256), glds, s, (const float*)dwt, splits, dw, Cout,
+                         Cin, cin_w, p.store);
+    PCMS_CHECK_LAUNCH();
+  }
   int R = splits, stride = 1;
   if (splits > 16) {
     hipLaunchKernelGGL(wgrad_group_sum_kernel, dim3((unsigned)cdiv(E, 256), cdiv(splits, 16)), dim3(256), 0, s, dwt,

@@ -383,6 +383,48 @@ def test_conv3_wgrad_x6_box_stream(x6dma, N, c0, c1, cout, S):
         L.query("pcms_conv3_wgrad_x6_dma", old)
 
 
+@pytest.mark.parametrize("code", [1, 0])
+@pytest.mark.parametrize("N,c0,c1,cout,S", [
+    (2, 8, 0, 64, (16, 16, 16)),       # 1 tile: 256 split rows, 16 groups of 16
+    (2, 64, 0, 64, (16, 32, 64)),      # 2 tiles: 128 rows, 8 groups
+    (1, 64, 64, 128, (8, 16, 16)),     # 8 tiles: 32 rows, 2 groups
+    (2, 64, 64, 64, (8, 8, 8)),        # 16 rows, one group
+    (1, 256, 0, 512, (4, 4, 8)),       # deep channel counts: 2 rows
+])
+def test_conv3_wgrad_reduce_fused_bit_identical(code, N, c0, c1, cout, S):
+    """The one-launch split-row reduction = the group-sum + reduce pair, bit for bit (fresh
+    store and accumulate), and within the wgrad bar of fp64."""
+    L = _lib()
+    g = torch.Generator().manual_seed(5)
+    dt = torch.bfloat16 if code == 1 else torch.float32
+    cin = c0 + c1
+    x = torch.randn(N, cin, *S, generator=g).to(dt)
+    dy = torch.randn(N, cout, *S, generator=g).to(dt)
+    ws = torch.empty(L.query("pcms_conv3_wgrad_ws_floats", code, N, *S, c0, c1, cout, 256), device=DEV)
+    x0 = ndhwc(x[:, :c0]).to(DEV)
+    x1 = ndhwc(x[:, c0:]).to(DEV) if c1 else None
+    dyd = ndhwc(dy).to(DEV)
+    init = torch.randn(cout * cin * 27, generator=g).to(DEV)
+    old = L.query("pcms_conv3_wgrad_reduce_fused", 1)
+    try:
+        outs = {}
+        for fused in (1, 0):
+            L.query("pcms_conv3_wgrad_reduce_fused", fused)
+            for store in (1, 0):
+                dw = init.clone()
+                L.call("pcms_conv3_wgrad", code, x0, c0, x1, c1, dyd, dw, ws, N, *S, cout, cin, 256, store)
+                torch.cuda.synchronize()
+                outs[fused, store] = dw.cpu()
+    finally:
+        L.query("pcms_conv3_wgrad_reduce_fused", old)
+    for store in (1, 0):
+        assert torch.equal(outs[1, store], outs[0, store]), f"store={store}"
+    wr = torch.zeros(cout, cin, 3, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv3d(x.double(), wr, None, padding=1).backward(dy.double())
+    close(outs[1, 1].view(cout, cin, 3, 3, 3), wr.grad, 1e-4 if code else 2e-5, "fused-reduce wgrad vs fp64")
+    close((outs[1, 0] - init.cpu()).view(cout, cin, 3, 3, 3), wr.grad, 1e-4 if code else 2e-5, "accumulate")
+
+
 @pytest.mark.parametrize("c0,c1,S", [(64, 0, (32, 32, 32)), (32, 32, (24, 20, 40))])
 def test_conv3_wgrad_many_boxes(c0, c1, S):
     """bf16 weight gradient over a grid of many boxes (the level-0..2 voxel-split plan, partial

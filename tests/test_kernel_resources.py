@@ -20,7 +20,7 @@ KERNELS = {
     "conv3.hip": ["conv3_fwd_big_kernel", "conv3_fwd_b16_kernelILb0ELi8ELi4E", "conv3_fwd_b16_kernelILb1ELi8ELi4E",
                   "conv3_fwd_b16_kernelILb0ELi4ELi4E", "conv3_fwd_b16_kernelILb1ELi4ELi4E",
                   "conv3_fwd_b16_kernelILb0ELi4ELi8E", "conv3_fwd_b16_kernelILb1ELi4ELi8E", "conv3_fwd_kernelItLi2ELi2ELi3ELi4E", "conv3_fwd_kernelItLi2ELin1ELin1ELin1E",
-                  "conv3_wgrad_kernelI4x6_t"],
+                  "conv3_wgrad_kernelI4x6_t", "wgrad_reduce_fused_kernel"],
     "stem.hip": ["stem_fwd_direct_kernelILi2ELi3E", "stem_fwd_direct_kernelILi3ELi2E", "stem_wgrad_stream_kernel"],
     "convt.hip": ["convt_lds_kernel", "convt_fwd_stream_kernel"],
     # streaming fusions: a spill there would add scratch traffic to an HBM-bound pass

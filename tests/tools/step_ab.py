@@ -6,7 +6,8 @@ variant alike; HIP events around K back-to-back steps, median over rounds.
 
 Variants: base (the defaults), nobnin (engine.fuse_bnin off), densewg (stem weight gradient
 in the dense-column form), split256 / split512 (engine.split_target), x6sync / x6dma (the fp32
-build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32)."""
+build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32),
+wred1 / wred0 (the weight gradient's split rows summed in one launch / by the two-stage pair)."""
 import argparse
 import os
 import statistics
@@ -37,11 +38,13 @@ def main():
     dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target}
     dense0 = L.query("pcms_stem_wgrad_dense", -1)
     x6dma0 = L.query("pcms_conv3_wgrad_x6_dma", -1)
+    wred0 = L.query("pcms_conv3_wgrad_reduce_fused", -1)
 
     def setup(v):
         eng.fuse_bnin, eng.split_target = dflt["fuse_bnin"], dflt["split_target"]
         L.query("pcms_stem_wgrad_dense", dense0)
         L.query("pcms_conv3_wgrad_x6_dma", x6dma0)
+        L.query("pcms_conv3_wgrad_reduce_fused", wred0)
         if v == "nobnin":
             eng.fuse_bnin = False
         elif v == "bnin":
@@ -52,6 +55,8 @@ def main():
             L.query("pcms_stem_wgrad_dense", 0)
         elif v in ("x6sync", "x6dma"):  # the fp32 build's weight-gradient box stream
             L.query("pcms_conv3_wgrad_x6_dma", int(v == "x6dma"))
+        elif v in ("wred1", "wred0"):
+            L.query("pcms_conv3_wgrad_reduce_fused", int(v == "wred1"))
         elif v.startswith("split"):
             eng.split_target = int(v[5:])
         elif v != "base":
