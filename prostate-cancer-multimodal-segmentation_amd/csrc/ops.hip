@@ -293,6 +293,12 @@ constexpr int kSmallRows = 512;
 // in flight per trip (the sums were latency-bound chains of ~rows / 32 dependent trips on 4
 // row lanes); the 16 lane sums are added in lane order
 constexpr int kCfRL = 16;
+// rows in flight per thread per trip (16: one trip for <= 256 rows, two for 512; 8 took up to
+// four dependent trips of memory latency); the row order of every sum is the same for any value
+#ifndef PCMS_CF_U
+#define PCMS_CF_U 16
+#endif
+constexpr int kCfU = PCMS_CF_U;
 template <bool BWD>
 __global__ void __launch_bounds__(64 * kCfRL) colsum_finalize_small_kernel(
     const float* part, int rows, int C, const float* cnt, double count, const float* gamma, const float* beta,
@@ -305,29 +311,25 @@ __global__ void __launch_bounds__(64 * kCfRL) colsum_finalize_small_kernel(
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     int r = rl;
-    for (; r + 7 * kCfRL < rows; r += 8 * kCfRL) {
-      float2 v[8];
+    for (; r < rows; r += kCfU * kCfRL) {  // the last trip predicated, loads still batched
+      float2 v[kCfU];
+      float nv[kCfU];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(part + ((long)(r + kCfRL * u) * C + c) * 2);
+      for (int u = 0; u < kCfU; ++u)
+        if (r + kCfRL * u < rows) {
+          v[u] = *reinterpret_cast<const float2*>(part + ((long)(r + kCfRL * u) * C + c) * 2);
+          nv[u] = cnt ? cnt[r + kCfRL * u] : 0.f;
+        }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < kCfU; ++u) {
+        if (r + kCfRL * u >= rows) break;
         s1 += (double)v[u].x;
         if (cnt) {
-          const double n = (double)cnt[r + kCfRL * u];
+          const double n = (double)nv[u];
           s2 += (double)v[u].y + (n > 0.0 ? (double)v[u].x * (double)v[u].x / n : 0.0);
         } else {
           s2 += (double)v[u].y;
         }
-      }
-    }
-    for (; r < rows; r += kCfRL) {
-      const float2 v = *reinterpret_cast<const float2*>(part + ((long)r * C + c) * 2);
-      s1 += (double)v.x;
-      if (cnt) {
-        const double n = (double)cnt[r];
-        s2 += (double)v.y + (n > 0.0 ? (double)v.x * (double)v.x / n : 0.0);
-      } else {
-        s2 += (double)v.y;
       }
     }
   }

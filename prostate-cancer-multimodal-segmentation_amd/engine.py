@@ -158,6 +158,10 @@ class UNetEngine:
         self.grad_ready = None   # callable(lo, hi) per finished module gradient (dp.GradSync.ready)
         self.kernel_timer = None  # dict name -> [(start, end) events] (bench.py roofline timing)
         self.wgrad_side_stream = False  # ablation: weight gradients on a side stream (measured 119.9 vs 121.6 vol/s: off)
+        # levels >= this run their conv weight gradients on the side stream (the deep levels'
+        # small latency-bound launches beside the dgrad chain; the big levels' persistent grids
+        # straggle when they share the chip).  99: never
+        self.wgrad_side_min_level = 99
         self._side_stream = None
         self._side_used = False
         # eval mode: every BatchNorm folded into the conv before it (pcms_bn_fold) and the ReLU
@@ -279,8 +283,11 @@ class UNetEngine:
     # weight gradients run on a side stream beside the data-gradient chain (dgrad -> BN ->
     # dgrad ...): they only read activations and the dY buffer of their layer, which the main
     # stream does not overwrite before the next _join_side()
-    def _side(self):
-        if not self.wgrad_side_stream:
+    def _side_at(self, lvl: int) -> bool:
+        return self.wgrad_side_stream or lvl >= self.wgrad_side_min_level
+
+    def _side(self, lvl: int):
+        if not self._side_at(lvl):
             return contextlib.nullcontext()
         if self._side_stream is None:
             self._side_stream = torch.cuda.Stream(device=self.device)
@@ -588,7 +595,7 @@ class UNetEngine:
         return s
 
     def _alloc(self, N, D, H, W):
-        key = (N, D, H, W, self.act_ckpt, self.wgrad_side_stream)
+        key = (N, D, H, W, self.act_ckpt, self.wgrad_side_stream, self.wgrad_side_min_level)
         if self.buf_key == key:
             return
         self.bufs = None
@@ -624,7 +631,7 @@ class UNetEngine:
             b[f"gA{l}"] = act(l, C[l])      # grad of a1 / block outputs (scratch)
             b[f"gY{l}"] = act(l, C[l])      # grad of pre-BN conv outputs (scratch)
             # second one while the side stream may still read gY; else an alias
-            b[f"gZ{l}"] = act(l, C[l]) if self.wgrad_side_stream else b[f"gY{l}"]
+            b[f"gZ{l}"] = act(l, C[l]) if self._side_at(l) else b[f"gY{l}"]
             b[f"gU{l}"] = act(l, C[l])      # grad of up output / pooled input (scratch)
         # workspaces
         rows_f = max(max(query("pcms_conv3_mblocks", N, *S[l]) for l in range(5)),
@@ -920,7 +927,7 @@ class UNetEngine:
             self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         if ga2 is not None:
             self._grads_done(blk.b1.mod.weight, blk.b1.mod.bias)
-        with self._side():
+        with self._side(lvl):
             if id(blk) in self._fwd_bnin:  # x = relu(bn0(y1)), applied in the kernel's staging (as the forward)
                 call("pcms_conv3_wgrad_bnin", blk.c1.code, acts["y1"], blk.c0.cout, blk.b0.scale, blk.b0.shift, gY,
                      blk.c1.mod.weight.grad, b["dwt"], N, *S, blk.c1.cout, blk.c1.cin, self.wgrad_target,
@@ -939,14 +946,14 @@ class UNetEngine:
             call("pcms_bn_relu_bwd", self.code, gA, acts["y1"], bn.scale, bn.shift, bn.mean, bn.invstd, m.weight,
                  b["stats"], b["coef"], m.weight.grad, m.bias.grad, None, bn.c, nvox, b["bnws"])
             self._grads_done(m.weight, m.bias)
-            with self._side(), self._timed("stem_wgrad"):
+            with self._side(lvl), self._timed("stem_wgrad"):
                 call("pcms_stem_wgrad_bn", x0, gA, acts["y1"], bn.scale, bn.shift, bn.mean, bn.invstd, b["coef"],
                      blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
             self._grads_done(blk.c0.mod.weight, blk.c0.mod.bias)
             return
         self._bn_bwd(blk.b0, gA, acts["y1"], gZ, nvox)
         self._grads_done(blk.b0.mod.weight, blk.b0.mod.bias)
-        with self._side():
+        with self._side(lvl):
             if blk is self.enc[0] and self.stem_sup & 2:
                 with self._timed("stem_wgrad"):
                     call("pcms_stem_wgrad", x0, gZ, blk.c0.mod.weight.grad, b["dwt"], blk.c0.cin, N, *S)
