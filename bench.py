@@ -177,7 +177,7 @@ def stem_roofline(tr, N, spatial, reps, in_step=None):
     kernel = (f"stem conv3d 5->64 fwd + wgrad with the BN0 backward apply fused in ({fk} + "
               "stem_wgrad_stream_kernel<BN>)" if fused else
               f"stem conv3d 5->64 fwd + wgrad ({fk} + stem_wgrad_stream_kernel)")
-    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r5_stem_traffic.json")
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r6_stem_traffic.json")
     if os.path.exists(tf):
         with open(tf) as f:
             rec = json.load(f)
