@@ -1,6 +1,7 @@
 """Weight-gradient ablation on the box (test tooling): the product kernel and WGRAD_ABL builds
 (tests/tools/ab_build.sh <suf> -DWGRAD_ABL=<bits>, see conv3.hip) timed back to back on the
 level-0..2 shapes of config 2, with the shader clock over the launches (bench.ClockProbe).
+WGRAD_ABL_SHAPES=deep: the level-3/4 shapes instead.
 Usage: python tests/tools/wgrad_abl.py [lib suffix ...]   ("" = the product library, "k32" = the
 product library with pcms_conv3_wgrad_k16(0))."""
 import json
@@ -21,6 +22,9 @@ SHAPES = [  # (N, D, H, W, c0, c1, Cout)
     (2, 64, 64, 32, 128, 128, 128),
     (2, 32, 32, 16, 256, 0, 256),
 ]
+if os.environ.get("WGRAD_ABL_SHAPES") == "deep":  # levels 3-4 of config 2
+    SHAPES = [(2, 8, 8, 4, 1024, 0, 1024), (2, 8, 8, 4, 512, 0, 1024), (2, 16, 16, 8, 512, 0, 512),
+              (2, 16, 16, 8, 512, 512, 512)]
 
 
 def worker(suf):
