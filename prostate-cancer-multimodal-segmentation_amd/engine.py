@@ -595,7 +595,10 @@ class UNetEngine:
         return s
 
     def _alloc(self, N, D, H, W):
-        key = (N, D, H, W, self.act_ckpt, self.wgrad_side_stream, self.wgrad_side_min_level)
+        # the workspaces below are sized for the current split / weight-gradient workgroup
+        # targets: a changed target re-lays them out (a larger one would otherwise overrun them)
+        key = (N, D, H, W, self.act_ckpt, self.wgrad_side_stream, self.wgrad_side_min_level, self.wgrad_target,
+               self.split_target)
         if self.buf_key == key:
             return
         self.bufs = None
@@ -999,6 +1002,9 @@ class UNetEngine:
         if self.saved_epoch != self.epoch:
             raise RuntimeError("UNet3D backward must follow its own training forward (the engine keeps "
                                "only the activations of the latest forward)")
+        if self.buf_key[7:9] != (self.wgrad_target, self.split_target):
+            raise RuntimeError("wgrad_target / split_target changed between the forward and its backward (the "
+                               "workspaces were sized for the forward's values)")
         fresh = self.sync_params(full=False, fresh_ok=True)
         self._gstore = fresh
         if fresh:

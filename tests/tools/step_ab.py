@@ -8,7 +8,8 @@ Variants: base (the defaults), nobnin (engine.fuse_bnin off), densewg (stem weig
 in the dense-column form), split256 / split512 (engine.split_target), x6sync / x6dma (the fp32
 build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32),
 wred1 / wred0 (the weight gradient's split rows summed in one launch / by the two-stage pair),
-sideK (conv weight gradients of levels >= K on the side stream; side99 = never)."""
+sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
+(engine.wgrad_target = N)."""
 import argparse
 import os
 import statistics
@@ -36,7 +37,8 @@ def main():
     eng = tr.model.engine()
     b = make_batch(2, (128, 128, 64), seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
-    dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target, "side": eng.wgrad_side_min_level}
+    dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target, "side": eng.wgrad_side_min_level,
+            "wt": eng.wgrad_target}
     dense0 = L.query("pcms_stem_wgrad_dense", -1)
     x6dma0 = L.query("pcms_conv3_wgrad_x6_dma", -1)
     wred0 = L.query("pcms_conv3_wgrad_reduce_fused", -1)
@@ -44,6 +46,7 @@ def main():
     def setup(v):
         eng.fuse_bnin, eng.split_target = dflt["fuse_bnin"], dflt["split_target"]
         eng.wgrad_side_min_level = dflt["side"]
+        eng.wgrad_target = dflt["wt"]
         L.query("pcms_stem_wgrad_dense", dense0)
         L.query("pcms_conv3_wgrad_x6_dma", x6dma0)
         L.query("pcms_conv3_wgrad_reduce_fused", wred0)
@@ -59,6 +62,8 @@ def main():
             L.query("pcms_conv3_wgrad_x6_dma", int(v == "x6dma"))
         elif v in ("wred1", "wred0"):
             L.query("pcms_conv3_wgrad_reduce_fused", int(v == "wred1"))
+        elif v.startswith("wt"):
+            eng.wgrad_target = int(v[2:])
         elif v.startswith("side"):
             eng.wgrad_side_min_level = int(v[4:])
         elif v.startswith("split"):
