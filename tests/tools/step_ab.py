@@ -9,7 +9,7 @@ in the dense-column form), split256 / split512 (engine.split_target), x6sync / x
 build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32),
 wred1 / wred0 (the weight gradient's split rows summed in one launch / by the two-stage pair),
 sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
-(engine.wgrad_target = N)."""
+(engine.wgrad_target = N), q:NAME=V (the library switch pcms_NAME set to V, restored after)."""
 import argparse
 import os
 import statistics
@@ -43,7 +43,13 @@ def main():
     x6dma0 = L.query("pcms_conv3_wgrad_x6_dma", -1)
     wred0 = L.query("pcms_conv3_wgrad_reduce_fused", -1)
 
+    qsaved = {}
+
     def setup(v):
+        for name, old in qsaved.items():
+            L.query(name, old)
+            eng.buf_key = None
+        qsaved.clear()
         eng.fuse_bnin, eng.split_target = dflt["fuse_bnin"], dflt["split_target"]
         eng.wgrad_side_min_level = dflt["side"]
         eng.wgrad_target = dflt["wt"]
@@ -62,6 +68,10 @@ def main():
             L.query("pcms_conv3_wgrad_x6_dma", int(v == "x6dma"))
         elif v in ("wred1", "wred0"):
             L.query("pcms_conv3_wgrad_reduce_fused", int(v == "wred1"))
+        elif v.startswith("q:"):
+            name, val = v[2:].split("=")
+            qsaved["pcms_" + name] = L.query("pcms_" + name, int(val))
+            eng.buf_key = None  # workspace sizes may follow the switch: re-lay out
         elif v.startswith("wt"):
             eng.wgrad_target = int(v[2:])
         elif v.startswith("side"):
