@@ -102,6 +102,11 @@ constexpr int kSDThr = 512;                                   // one 8-wave work
 #ifndef PCMS_STEM_WIDE
 #define PCMS_STEM_WIDE 0
 #endif
+// dword stores: the voxel row's constant offset in voffset (folded into the immediate offset
+// field, 1) or added to the SGPR soffset (0: an s_add per store)
+#ifndef PCMS_STEM_VOFF
+#define PCMS_STEM_VOFF 1
+#endif
 
 // DPP quad_perm controls: lane j reads lane j ^ 1 / j ^ 2 of its quad
 constexpr int kDppXor1 = 0xB1;  // quad_perm [1, 0, 3, 2]
@@ -315,6 +320,10 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         __builtin_amdgcn_raw_buffer_store_b128((u32x4_t){qd[0], qd[1], qd[2], qd[3]}, yr,
                                                ((g == 1 || g == 2) ? wB : wA) + so[mt] + 4 * g * 128, 0, 2);
       }
+    } else if constexpr (PCMS_STEM_VOFF) {
+      // the voxel's constant row offset rides in the instruction's immediate offset (no s_add
+      // per store for a soffset of its own)
+      __builtin_amdgcn_raw_buffer_store_b32(pk, yr, ((g == 1 || g == 2) ? vB : vA) + rw * 128, so[mt], 2);
     } else {
       __builtin_amdgcn_raw_buffer_store_b32(pk, yr, (g == 1 || g == 2) ? vB : vA, so[mt] + rw * 128, 2);
     }
@@ -345,11 +354,11 @@ __global__ void __launch_bounds__(kSDThr, 1) stem_fwd_direct_kernel(Conv3Params 
         const float v0 = acc[mt][0][e], v1 = acc[mt][1][e];
         const int xh = (gB ? 1 : 0) ^ hsel;
         const bool valid = (d0 + rd0 < D) & (h0 + rh0 + xh < H) & (w0 + rw < W);
-        const uint32_t voff = valid ? (gB ? vB : vA) : kOOB;
+        const uint32_t voff = valid ? (gB ? vB : vA) + (PCMS_STEM_VOFF ? rw * 128 : 0) : kOOB;
         const float e0 = valid ? v0 - K[0] : 0.f, e1 = valid ? v1 - K[1] : 0.f;
         cnt += valid ? 1.f : 0.f;
         __builtin_amdgcn_raw_buffer_store_b32(RELU ? pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f)) : pack_bf16x2(v0, v1),
-                                              yr, voff, so[mt] + rw * 128, 2);
+                                              yr, voff, so[mt] + (PCMS_STEM_VOFF ? 0 : rw * 128), 2);
         s1[0] += e0; s2[0] = fmaf(e0, e0, s2[0]);
         s1[1] += e1; s2[1] = fmaf(e1, e1, s2[1]);
       }
