@@ -557,6 +557,20 @@ __global__ void __launch_bounds__(TPB, 3) maxpool_bwd_bn_kernel(const T* y, cons
     unpack(gr, g);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; arg[j] = 0; }
+    // channel pairs in packed fp32 (the same IEEE operation per element as the scalar forms,
+    // half the VALU issue: the kernel was VALU-bound) and one v_cvt_pk_bf16_f32 per pair
+    auto round2 = [](f32x2_t v) -> f32x2_t {
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t u = pack_bf16x2(v[0], v[1]);
+        return (f32x2_t){__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+      } else {
+        return v;
+      }
+    };
+    auto z2of = [&](const float (&yv)[VEC], int q) {
+      return __builtin_elementwise_fma((f32x2_t){yv[2 * q], yv[2 * q + 1]}, (f32x2_t){sc[2 * q], sc[2 * q + 1]},
+                                       (f32x2_t){sh[2 * q], sh[2 * q + 1]});
+    };
     if (whole) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -573,7 +587,11 @@ __global__ void __launch_bounds__(TPB, 3) maxpool_bwd_bn_kernel(const T* y, cons
     for (int k = 0; k < 8; ++k) {
       if (!ink(k)) continue;
       float yv[VEC], o[VEC];
-      unpack(yr[k], yv);
+      // (an opaque copy: the compiler would otherwise keep the argmax pass's 64 BN values live
+      // for this pass, past the register budget)
+      u32x4_t yk = yr[k];
+      asm volatile("" : "+v"(yk));
+      unpack(yk, yv);
       unpack(dr[k], o);
       if (whole) {
 #pragma unroll
@@ -581,10 +599,20 @@ __global__ void __launch_bounds__(TPB, 3) maxpool_bwd_bn_kernel(const T* y, cons
         store16<T>(da + vk(k) * C + cv * VEC, o);
       }
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        const float gg = (yv[j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
-        sg[j] += gg;
-        sgx[j] += gg * ((yv[j] - mu[j]) * is[j]);
+      for (int q = 0; q < VEC / 2; ++q) {
+        const f32x2_t z2 = z2of(yv, q);
+        const f32x2_t r2 = round2((f32x2_t){o[2 * q], o[2 * q + 1]});
+        const f32x2_t g2 = {z2[0] > 0.f ? r2[0] : 0.f, z2[1] > 0.f ? r2[1] : 0.f};
+        const f32x2_t t2 = ((f32x2_t){yv[2 * q], yv[2 * q + 1]} - (f32x2_t){mu[2 * q], mu[2 * q + 1]}) *
+                           (f32x2_t){is[2 * q], is[2 * q + 1]};
+        f32x2_t sg2 = {sg[2 * q], sg[2 * q + 1]}, sgx2 = {sgx[2 * q], sgx[2 * q + 1]};
+        {
+#pragma clang fp contract(off)  // a product then a sum, as the separate reduce pass forms it
+          sgx2 = sgx2 + g2 * t2;
+          sg2 = sg2 + g2;
+        }
+        sg[2 * q] = sg2[0]; sg[2 * q + 1] = sg2[1];
+        sgx[2 * q] = sgx2[0]; sgx[2 * q + 1] = sgx2[1];
       }
     }
   }
@@ -812,33 +840,57 @@ __global__ void __launch_bounds__(TPB, (BN && NC > 2) ? 2 : 3) head_bwd_kernel(c
 #pragma unroll
     for (int k = 0; k < NC; ++k) dl[k] = dlogits[((long)p.q * NC + k) * nvox_per_n + p.r];
   };
-  auto one = [&](long v, const float (&x)[8], const float (&dl)[NC]) {
-    float o[8], av[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      o[j] = 0.f;
-      if constexpr (BN) av[j] = round_st<T>(bn_relu1(x[j], sc[j], sh[j]));
-      else av[j] = x[j];
-    }
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] += dl[k] * wk[k][j];
-        accw[k][j] += dl[k] * av[j];
-      }
-      if (sub == 0) accb[k] += dl[k];
-    }
-    if constexpr (BN) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float g = (x[j] * sc[j] + sh[j] > 0.f) ? round_st<T>(o[j]) : 0.f;
-        sg[j] += g;
-        sgx[j] += g * ((x[j] - mu[j]) * is[j]);
-      }
+  // channel pairs in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: the same IEEE
+  // operation per element as the scalar forms, half the VALU issue; the kernel was VALU-bound)
+  // and one v_cvt_pk_bf16_f32 per pair for the T rounding
+  auto round2 = [](f32x2_t v) -> f32x2_t {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t u = pack_bf16x2(v[0], v[1]);
+      return (f32x2_t){__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
     } else {
-      head_st<T, NT>(da + v * 64 + sub * 8, o);
+      return v;
     }
+  };
+  auto one = [&](long v, const float (&x)[8], const float (&dl)[NC]) {
+    float o[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x2_t x2 = {x[2 * q], x[2 * q + 1]};
+      f32x2_t z2 = {0.f, 0.f}, av2 = x2;
+      if constexpr (BN) {
+        z2 = __builtin_elementwise_fma(x2, (f32x2_t){sc[2 * q], sc[2 * q + 1]}, (f32x2_t){sh[2 * q], sh[2 * q + 1]});
+        av2 = round2((f32x2_t){fmaxf(z2[0], 0.f), fmaxf(z2[1], 0.f)});
+      }
+      f32x2_t o2 = {0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        const f32x2_t d2 = {dl[k], dl[k]};
+        o2 = __builtin_elementwise_fma(d2, (f32x2_t){wk[k][2 * q], wk[k][2 * q + 1]}, o2);
+        const f32x2_t a2 = __builtin_elementwise_fma(d2, av2, (f32x2_t){accw[k][2 * q], accw[k][2 * q + 1]});
+        accw[k][2 * q] = a2[0];
+        accw[k][2 * q + 1] = a2[1];
+      }
+      if constexpr (BN) {
+        const f32x2_t r2 = round2(o2);
+        const f32x2_t g2 = {z2[0] > 0.f ? r2[0] : 0.f, z2[1] > 0.f ? r2[1] : 0.f};
+        const f32x2_t t2 = (x2 - (f32x2_t){mu[2 * q], mu[2 * q + 1]}) * (f32x2_t){is[2 * q], is[2 * q + 1]};
+        // sum g xhat as a product then a sum (not fused), as the separate reduce pass forms it
+        f32x2_t sgx2 = {sgx[2 * q], sgx[2 * q + 1]}, sg2 = {sg[2 * q], sg[2 * q + 1]};
+        {
+#pragma clang fp contract(off)
+          sgx2 = sgx2 + g2 * t2;
+          sg2 = sg2 + g2;
+        }
+        sg[2 * q] = sg2[0]; sg[2 * q + 1] = sg2[1];
+        sgx[2 * q] = sgx2[0]; sgx[2 * q + 1] = sgx2[1];
+      }
+      o[2 * q] = o2[0];
+      o[2 * q + 1] = o2[1];
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      if (sub == 0) accb[k] += dl[k];
+    if constexpr (!BN) head_st<T, NT>(da + v * 64 + sub * 8, o);
   };
   const long stride = ((long)gridDim.x * blockDim.x) >> 3;
   long v = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 3;
