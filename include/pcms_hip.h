@@ -259,6 +259,10 @@ int pcms_convt_dgrad_ws(int dtype, const void* dout, const void* wpack_d, void* 
 int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Cout, int target_wgs);
 /* A/B switch: taps per workgroup of the bf16 Cin % 128 == 0 weight gradient (8, 4 or 2; 0 =
    chosen by shape); returns the previous setting.  Process-wide. */
+/* the ConvTranspose weight gradient's split rows and (bf16 128-channel path) bias rows summed
+ * by one launch (1, default) or by the group-sum / reduce / bias-reduce launches (0); the sums
+ * are bit-identical; v < 0 queries; returns the previous setting (A/B switch) */
+int pcms_convt_reduce_fused(int v);
 int pcms_convt_wgrad_taps(int tt);
 int pcms_convt_wgrad(int dtype, const void* x, const void* dout, float* dw, float* ws,
                      int N, int Din, int Hin, int Win, int Cin, int Cout, int Do, int Ho, int Wo,

@@ -916,6 +916,67 @@ __global__ void __launch_bounds__(256) convt_wgrad_reduce(const float* ws, int R
   dw[((long)ci * Cout + co0) * 8 + e] += tile[e & 7][e >> 3];
 }
 
+// One launch for the split reduction and the bias rows, bit-identical to convt_group_sum +
+// convt_wgrad_reduce and convt_bias_reduce: blocks [0, Cin Cout / 32) sum one (ci, 32 co) tile's
+// S partial rows -- groups of 16 rows in row order per thread (all 16 loads in flight), the
+// group sums in group order -- and add them to dw through the same LDS transpose; the blocks
+// past those (bpart != nullptr) add the RB bias rows to db with convt_bias_reduce's order (8
+// rows' loads in flight per trip instead of one).
+#ifndef PCMS_CONVT_RED_FUSED
+#define PCMS_CONVT_RED_FUSED 1
+#endif
+static int g_convt_red_fused = PCMS_CONVT_RED_FUSED;  // 0: the separate launches (A/B, bit-identity test)
+__global__ void __launch_bounds__(256) convt_reduce_fused_kernel(const float* ws, int S, float* dw, int Cin, int Cout,
+                                                                 const float* bpart, int RB, float* db) {
+  __shared__ float tile[8][33];
+  __shared__ float red[32][9];
+  const int nw = Cin * (Cout / 32);
+  if ((int)blockIdx.x < nw) {
+    const int ci = blockIdx.x / (Cout / 32), co0 = (blockIdx.x % (Cout / 32)) * 32;
+    const long E = 8L * Cin * Cout;
+    const int e = threadIdx.x, t = e >> 5, c = e & 31;
+    const float* src = ws + ((long)ci * 8 + t) * Cout + co0 + c;
+    float total = 0.f;
+    for (int r0 = 0; r0 < S; r0 += 16) {
+      const int n = min(16, S - r0);
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (r < n) v[r] = src[(long)(r0 + r) * E];
+      float gsum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (r < n) gsum += v[r];
+      total += gsum;
+    }
+    tile[t][c] = total;
+    __syncthreads();
+    dw[((long)ci * Cout + co0) * 8 + e] += tile[e & 7][e >> 3];
+    return;
+  }
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int cc = (blockIdx.x - nw) * 8 + cl;
+  float sb = 0.f;
+  if (cc < Cout) {
+    int r = rl;
+    for (; r + 7 * 32 < RB; r += 8 * 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = bpart[(long)(r + 32 * u) * Cout + cc];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sb += v[u];
+    }
+    for (; r < RB; r += 32) sb += bpart[(long)r * Cout + cc];
+  }
+  red[rl][cl] = sb;
+  __syncthreads();
+  if (rl == 0 && cc < Cout) {
+    float tt = 0.f;
+    for (int k = 0; k < 32; ++k) tt += red[k][cl];
+    db[cc] += tt;
+  }
+}
+
 // master W[Cin][Cout][8] fp32 ->  fwd pack [8][Cout][Cin]  /  dgrad pack [Cin][8][Cout]
 // (x6: element i = (row, k) of that order becomes the three B fragments of its 8-group:
 // [row][k / 8][48] bf16, see afrag_x6)
@@ -1330,6 +1391,15 @@ int pcms_convt_wgrad_ws_floats(int N, int Din, int Hin, int Win, int Cin, int Co
 
 // A/B switch: taps per workgroup of the bf16 128-ci weight gradient (8, 4, 2; 0 = by shape);
 // returns the previous value.  Set before the workspace queries.
+// the ConvTranspose weight gradient's split rows and bias rows summed by one launch (1) or by
+// the group-sum / reduce / bias-reduce launches (0), bit-identical; v < 0 queries.  Returns the
+// previous value.
+int pcms_convt_reduce_fused(int v) {
+  const int old = g_convt_red_fused;
+  if (v >= 0) g_convt_red_fused = v;
+  return old;
+}
+
 int pcms_convt_wgrad_taps(int tt) {
   const int old = g_convt_wg_tt;
   if (tt == 0 || tt == 2 || tt == 4 || tt == 8) g_convt_wg_tt = tt;
@@ -1368,13 +1438,15 @@ static int convt_wgrad_any(int dtype, const void* x, const void* dout, float* dw
     if (TT == 8) launch_wgrad128<8>(nt, direct, grid, s, (const bf16_t*)x, (const bf16_t*)dout, dst, g, Cin, Cout, vps, bpart);
     else if (TT == 4) launch_wgrad128<4>(nt, direct, grid, s, (const bf16_t*)x, (const bf16_t*)dout, dst, g, Cin, Cout, vps, bpart);
     else launch_wgrad128<2>(nt, direct, grid, s, (const bf16_t*)x, (const bf16_t*)dout, dst, g, Cin, Cout, vps, bpart);
-    if (bpart != nullptr) {
-      hipError_t eb = hipGetLastError();
-      if (eb != hipSuccess) return (int)eb;
-      hipLaunchKernelGGL(convt_bias_reduce, dim3(cdiv(Cout, 8)), dim3(256), 0, s, (const float*)bpart, splits * G,
-                         Cout, db);
+    if (direct || !g_convt_red_fused) {
+      if (bpart != nullptr) {
+        hipError_t eb = hipGetLastError();
+        if (eb != hipSuccess) return (int)eb;
+        hipLaunchKernelGGL(convt_bias_reduce, dim3(cdiv(Cout, 8)), dim3(256), 0, s, (const float*)bpart, splits * G,
+                           Cout, db);
+      }
+      if (direct) PCMS_CHECK_LAUNCH();
     }
-    if (direct) PCMS_CHECK_LAUNCH();
   }
   dim3 grid(splits, Cout / 64, Cin / 64);
   if (ci128) {
@@ -1393,6 +1465,13 @@ static int convt_wgrad_any(int dtype, const void* x, const void* dout, float* dw
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const long E = 8L * Cin * Cout;
+  if (g_convt_red_fused) {  // the split rows (and, bf16 128-ci path, the bias rows) in one launch
+    const bool bias = ci128 && bpart != nullptr;
+    const int nblk = Cin * (Cout / 32) + (bias ? cdiv(Cout, 8) : 0);
+    hipLaunchKernelGGL(convt_reduce_fused_kernel, dim3(nblk), dim3(256), 0, s, (const float*)ws, splits, dw, Cin, Cout,
+                       bias ? (const float*)bpart : nullptr, bias ? splits * G : 0, db);
+    PCMS_CHECK_LAUNCH();
+  }
   int R = splits, stride = 1;
   if (splits > 16) {
     hipLaunchKernelGGL(convt_group_sum, dim3((unsigned)cdiv(E, 256), cdiv(splits, 16)), dim3(256), 0, s, ws, splits, E);

@@ -691,6 +691,39 @@ def test_convt_wgrad_taps(tt, Sin, Sout, cin, cout, target):
     close(db.cpu() - b0, br.grad, 1e-4, f"convT bias grad TT={tt}")
 
 
+@pytest.mark.parametrize("code", [1, 0])
+@pytest.mark.parametrize("Sin,Sout,cin,cout,target", [((16, 16, 8), (32, 32, 16), 512, 256, 1024),
+                                                      ((32, 32, 16), (64, 64, 32), 128, 64, 512),   # > 16 splits
+                                                      ((5, 6, 3), (11, 12, 7), 256, 128, 2048),
+                                                      ((8, 8, 4), (16, 16, 8), 1024, 512, 256)])    # direct
+def test_convt_reduce_fused_bit_identical(code, Sin, Sout, cin, cout, target):
+    """The ConvTranspose weight + bias gradient with its split rows and bias rows summed by one
+    launch = the group-sum / reduce / bias-reduce launches, bit for bit (+= onto prior dw, db)."""
+    L = _lib()
+    g = torch.Generator().manual_seed(12)
+    N = 2
+    dt = torch.bfloat16 if code == 1 else torch.float32
+    x = ndhwc(torch.randn(N, cin, *Sin, generator=g).to(dt)).to(DEV)
+    gout = ndhwc(torch.randn(N, cout, *Sout, generator=g).to(dt)).to(DEV)
+    w0 = torch.randn(cin * cout * 8, generator=g).to(DEV)
+    b0 = torch.randn(cout, generator=g).to(DEV)
+    ws = torch.empty(L.query("pcms_convt_wgrad_ws_floats", N, *Sin, cin, cout, target), device=DEV)
+    bws = torch.empty(max(1, L.query("pcms_convt_wgrad_bias_ws_floats", code, N, *Sin, cin, cout, target)), device=DEV)
+    old = L.query("pcms_convt_reduce_fused", 1)
+    outs = {}
+    try:
+        for fused in (1, 0):
+            L.query("pcms_convt_reduce_fused", fused)
+            dw, db = w0.clone(), b0.clone()
+            L.call("pcms_convt_wgrad_bias", code, x, gout, dw, db, ws, bws, N, *Sin, cin, cout, *Sout, target)
+            torch.cuda.synchronize()
+            outs[fused] = (dw.cpu(), db.cpu())
+    finally:
+        L.query("pcms_convt_reduce_fused", old)
+    assert torch.equal(outs[1][0], outs[0][0]), "dw"
+    assert torch.equal(outs[1][1], outs[0][1]), "db"
+
+
 @pytest.mark.parametrize("Sin,Sout", [((32, 32, 24), (64, 64, 48)), ((24, 20, 12), (49, 41, 25))])
 def test_convt_fwd_stream(Sin, Sout):
     """The persistent level-0 ConvTranspose forward (Cin 128, Cout 64; several 64-voxel tiles

@@ -16,6 +16,9 @@ d, v, pats = sys.argv[1], sys.argv[2], sys.argv[3:]
 rows = [r for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True) for r in csv.DictReader(open(f))]
 for p in pats:
     ts = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if p in r["Kernel_Name"]]
+    if not ts:
+        print(f"{v:8s} {p:40s} n=   0")
+        continue
     print(f"{v:8s} {p:40s} n={len(ts):4d} median {statistics.median(ts):8.1f} us  sum/13 {sum(ts) / 13:8.1f} us")
 PY
 done
