@@ -200,6 +200,10 @@ int pcms_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmea
                         float eps, int C, float* scale, float* shift, hipStream_t s);
 int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const float* shift, int C,
                  long nvox, hipStream_t s);
+/* A/B switch: block cap of the BN-backward reduce passes (their partial rows): 512 (default,
+ * the one-launch finalize) or more (2048: the two-stage finalize); v <= 0 queries; returns the
+ * previous value; set before the workspace queries */
+int pcms_bn_bwd_rows_cap(int v);
 int pcms_bn_bwd_rows(int dtype, int C, long nvox);
 /* dy = BN+ReLU backward(da); dgamma/dbeta += ; part: rows*C*2 fp32; coef: 3*C fp32 (the
  * apply coefficients k1, k2, k3 per channel: dy = k1 g + k2 xhat + k3).  dy == NULL: no

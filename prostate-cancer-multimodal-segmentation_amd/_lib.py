@@ -82,6 +82,7 @@ SIGNATURES = {
     "pcms_convt_wgrad_ws_floats": "iiiiiii",
     "pcms_convt_wgrad_taps": "i",
     "pcms_convt_reduce_fused": "i",
+    "pcms_bn_bwd_rows_cap": "i",
     "pcms_convt_wgrad": "ippppiiiiiiiiiis",
     "pcms_convt_wgrad_bias_ws_floats": "iiiiiiii",
     "pcms_convt_wgrad_bias": "ippppppiiiiiiiiiis",

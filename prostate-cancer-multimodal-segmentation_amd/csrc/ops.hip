@@ -1404,6 +1404,20 @@ int pcms_bn_relu(int dtype, const void* y, void* a, const float* scale, const fl
   PCMS_CHECK_LAUNCH();
 }
 
+// the BN-backward reduce passes' block cap (their partial-row count): kSmallRows (512, the
+// product: the finalize is one launch; round 6 kernel trace -15 us per step vs 2048,
+// profiles/r6_bn_rows_cap_ab.txt) or more (two-stage finalize); A/B switch: v <= 0 queries,
+// returns the old value; set before the workspace queries
+#ifndef PCMS_BN_ROWS_CAP
+#define PCMS_BN_ROWS_CAP 512
+#endif
+static int g_bn_rows_cap = PCMS_BN_ROWS_CAP;
+int pcms_bn_bwd_rows_cap(int v) {
+  const int old = g_bn_rows_cap;
+  if (v > 0) g_bn_rows_cap = v;
+  return old;
+}
+
 // number of partial rows pcms_bn_relu_bwd_reduce writes (caller sizes `part`)
 int pcms_bn_bwd_rows(int dtype, int C, long nvox) {
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
@@ -1411,7 +1425,7 @@ int pcms_bn_bwd_rows(int dtype, int C, long nvox) {
   // small (deep) grids: one trip of 4 rows per thread and 4x the blocks (a block's reduction
   // is a chain of memory latencies), as long as the rows stay on the one-launch finalize
   const int small = grid_for(nvox, VL * 4, 2048);
-  return small <= kSmallRows ? small : grid_for(nvox, VL * 16, 2048);
+  return small <= kSmallRows ? small : grid_for(nvox, VL * 16, g_bn_rows_cap);
 }
 
 int pcms_bn_relu_bwd(int dtype, const void* da, const void* y, const float* scale, const float* shift,
@@ -1490,7 +1504,7 @@ int pcms_bn_relu_pool(int dtype, const void* y, void* a, void* p, const float* s
 int pcms_maxpool_bwd_bn_rows(int dtype, int N, int D, int H, int W, int C) {
   const int VEC = dtype == PCMS_BF16 ? 8 : 4;
   const long cells = (long)N * ((D + 1) / 2) * ((H + 1) / 2) * ((W + 1) / 2);
-  return cell_grid(cells * (C / VEC), C / VEC, 2048);
+  return cell_grid(cells * (C / VEC), C / VEC, g_bn_rows_cap);
 }
 
 int pcms_maxpool_bwd_bn(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
