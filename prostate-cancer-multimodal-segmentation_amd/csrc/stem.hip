@@ -1001,8 +1001,11 @@ int pcms_stem_supported(int N, int D, int H, int W) {
 
 // BatchNorm statistics rows pcms_stem_fwd writes
 int pcms_stem_fwd_rows(int N, int D, int H, int W) {
+  // one row per workgroup of the persistent grid (round 6: was one per box, the rows past the
+  // grid zero-filled by the kernel -- 2 MB of zeros and a two-launch finalize over 4096 rows at
+  // config 2 instead of one launch over 256)
   const Box b = fwd_box(D, H, W);
-  return N * cdiv(D, 1 << b.lbd) * cdiv(H, 1 << b.lbh) * cdiv(W, 1 << b.lbw);
+  return std::min(N * cdiv(D, 1 << b.lbd) * cdiv(H, 1 << b.lbh) * cdiv(W, 1 << b.lbw), device_cus());
 }
 
 // x: (N, D, H, W, 8) bf16; y: (N, D, H, W, 64) bf16; stats rows = pcms_stem_fwd_rows
@@ -1030,7 +1033,8 @@ int pcms_stem_fwd(const void* x, const void* wpack, const float* bias, void* y, 
                                   : (relu ? stem_fwd_direct_kernel<3, 2, true> : stem_fwd_direct_kernel<3, 2, false>));
   const int lds = dense ? kSD2Lds : kSDLds;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThr), lds, s, p, nbox, nbox, (uint32_t)xbytes, (uint32_t)ybytes);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kSDThr), lds, s, p, nbox, pcms_stem_fwd_rows(N, D, H, W), (uint32_t)xbytes,
+                     (uint32_t)ybytes);
   PCMS_CHECK_LAUNCH();
 }
 
