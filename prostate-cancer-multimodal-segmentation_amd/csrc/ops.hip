@@ -1047,12 +1047,23 @@ __global__ void head_bwd_finish_kernel(const float* sums, int ncls, float* dw, f
 __global__ void __launch_bounds__(TPB) loss_partial_kernel(const float* x, const float* t, long M, float* part) {
   __shared__ float red[4][TPB / 64];
   float a = 0.f, b = 0.f, c = 0.f, d = 0.f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < M; i += (long)gridDim.x * blockDim.x) {
-    const float xv = x[i], tv = t[i];
+  auto one = [&](float xv, float tv) {
     const float p = 1.f / (1.f + expf(-xv));
     a += p * tv; b += p; c += tv;
     d += fmaxf(xv, 0.f) - xv * tv + log1pf(expf(-fabsf(xv)));
+  };
+  // 8 elements' loads in flight per trip, accumulated in the same element order as one at a
+  // time (identical sums; one element per trip was a chain of 8 memory latencies per thread)
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  for (; i + 7 * stride < M; i += 8 * stride) {
+    float xv[8], tv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { xv[u] = x[i + u * stride]; tv[u] = t[i + u * stride]; }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) one(xv[u], tv[u]);
   }
+  for (; i < M; i += stride) one(x[i], t[i]);
   a = wave_sum(a); b = wave_sum(b); c = wave_sum(c); d = wave_sum(d);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) { red[0][wave] = a; red[1][wave] = b; red[2][wave] = c; red[3][wave] = d; }
