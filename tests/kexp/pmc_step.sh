@@ -9,7 +9,7 @@ TAG=$1; shift
 O=$R/gpurun_out/pmc_$TAG
 rm -rf $O; mkdir -p $O
 export TMPDIR=/tmp
-B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --fp32-steps 0 --kernel-reps 1"
+B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --fp32-steps 0 --kernel-reps 1 ${BENCH_ARGS:-}"
 (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d $O/g1 -o run --output-format csv -- $B > $O/g1.log 2>&1) || exit $?
 (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d $O/g2 -o run --output-format csv -- $B > $O/g2.log 2>&1) || exit $?
 python3 - "$O" "$@" <<'PY'
