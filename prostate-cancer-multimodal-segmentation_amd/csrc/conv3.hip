@@ -31,6 +31,11 @@ namespace {
 // offsets become constant arithmetic); -1: runtime geometry from p.
 // MTW: M-tiles per wave (4: 512-voxel boxes; 2: boxes of <= 256 voxels -- level 4's 8x8x4 --
 // on all four waves instead of two)
+// ablation builds of the general forward / dgrad (0 in the product): bit 1 the fp32 (split)
+// chunks after a workgroup's first are not staged, 2 no MFMA phase for them
+#ifndef CONV_ABL
+#define CONV_ABL 0
+#endif
 template <typename T, int MINW, int LBD, int LBH, int LBW, int MTW = 4>
 __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p) {
   const int lbd_ = LBW >= 0 ? LBD : p.lbd, lbh_ = LBW >= 0 ? LBH : p.lbh, lbw_ = LBW >= 0 ? LBW : p.lbw;
@@ -95,6 +100,9 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
   const long plane = (long)p.H * p.W;
 
   for (int chunk = cbeg; chunk < cend; ++chunk) {
+#if CONV_ABL & 1  // ablation builds only (wrong results, timing): fp32 chunks after the first not staged
+    if (kSplit && chunk > cbeg) goto compute_chunk;
+#endif
     __syncthreads();
     // ---- stage the halo tile of this chunk by LDS-DMA: piece p (16 B) -> LDS [16p, 16p+16).
     // The LDS image is lane-linear, so the slot swizzle is applied to the SOURCE address
@@ -158,7 +166,13 @@ __global__ void __launch_bounds__(kThreads, MINW) conv3_fwd_kernel(Conv3Params p
       }
       __syncthreads();
     }
+#if CONV_ABL & 1
+  compute_chunk:
+#endif
     if (!wave_active) continue;
+#if CONV_ABL & 2  // ablation builds only: no MFMA phase for the fp32 data
+    if (kSplit) continue;
+#endif
 
     const bf16_t* wchunk = wp + (long)chunk * 27 * p.Cout * Tr::WK;
     Frag bset[2][2][Tr::KS];
