@@ -1815,24 +1815,42 @@ __global__ void __launch_bounds__(256) adam_pack_conv3_x6_kernel(float* P, float
   const int local = blockIdx.x - (int)e[5];
   const int j0 = (local % (Cout / 32)) * 32, ci0 = (local / (Cout / 32)) * 16;
   const float s = gmul ? c.gscale * gmul[0] : c.gscale;
-  for (int q4 = threadIdx.x; q4 < 32 * 108; q4 += 256) {  // 32 runs of 108 f32x4
-    const int run = q4 / 108, q = q4 % 108;
-    const long idx = off + ((long)(j0 + run) * Cin + ci0) * 27 + 4 * q;
-    f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(P + idx));
-    f32x4_t gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Gr + idx));
-    f32x4_t mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Mo + idx));
-    f32x4_t vv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Vo + idx));
+  // 32 runs of 108 f32x4 = 13.5 per thread: ADAM_X6_U iterations' four streams loaded before
+  // any is used (adam_pack_conv3_kernel's batching; one iteration in flight per thread left
+  // this kernel latency-bound at two 54-KiB blocks per CU)
+#ifndef ADAM_X6_U
+#define ADAM_X6_U 4
+#endif
+  for (int i0 = 0; i0 < 14; i0 += ADAM_X6_U) {
+    f32x4_t pv[ADAM_X6_U], gv[ADAM_X6_U], mv[ADAM_X6_U], vv[ADAM_X6_U];
+    long idx[ADAM_X6_U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float pk = pv[k], gk = gv[k], mk = mv[k], vk = vv[k];
-      adam_update(pk, gk, mk, vk, c, s);
-      pv[k] = pk; gv[k] = gk; mv[k] = mk; vv[k] = vk;
-      tf[run][4 * q + k] = pk;
+    for (int u = 0; u < ADAM_X6_U; ++u) {
+      const int q4 = threadIdx.x + (i0 + u) * 256, run = q4 / 108, q = q4 % 108;
+      idx[u] = off + ((long)(j0 + run) * Cin + ci0) * 27 + 4 * q;
+      if (i0 + u < 14 && q4 < 32 * 108) {
+        pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(P + idx[u]));
+        gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Gr + idx[u]));
+        mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Mo + idx[u]));
+        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(Vo + idx[u]));
+      }
     }
-    __builtin_nontemporal_store(pv, reinterpret_cast<f32x4_t*>(P + idx));
-    __builtin_nontemporal_store(mv, reinterpret_cast<f32x4_t*>(Mo + idx));
-    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4_t*>(Vo + idx));
-    if (s != 1.f) __builtin_nontemporal_store(gv, reinterpret_cast<f32x4_t*>(Gr + idx));
+#pragma unroll
+    for (int u = 0; u < ADAM_X6_U; ++u) {
+      const int q4 = threadIdx.x + (i0 + u) * 256, run = q4 / 108, q = q4 % 108;
+      if (i0 + u >= 14 || q4 >= 32 * 108) break;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float pk = pv[u][k], gk = gv[u][k], mk = mv[u][k], vk = vv[u][k];
+        adam_update(pk, gk, mk, vk, c, s);
+        pv[u][k] = pk; gv[u][k] = gk; mv[u][k] = mk; vv[u][k] = vk;
+        tf[run][4 * q + k] = pk;
+      }
+      __builtin_nontemporal_store(pv[u], reinterpret_cast<f32x4_t*>(P + idx[u]));
+      __builtin_nontemporal_store(mv[u], reinterpret_cast<f32x4_t*>(Mo + idx[u]));
+      __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4_t*>(Vo + idx[u]));
+      if (s != 1.f) __builtin_nontemporal_store(gv[u], reinterpret_cast<f32x4_t*>(Gr + idx[u]));
+    }
   }
   __syncthreads();
   auto put = [](bf16_t* row, const float (&f)[8]) {

@@ -162,6 +162,10 @@ class UNetEngine:
         # small latency-bound launches beside the dgrad chain; the big levels' persistent grids
         # straggle when they share the chip).  99: never
         self.wgrad_side_min_level = 99
+        # ablation only (tests/tools/step_ab.py nopack): skip the input pack, so the stem reads
+        # the previous step's packed input -- bounds what folding pack_input into the stem
+        # kernels could save; never set in the product (the forward is wrong with it)
+        self.ablate_skip_pack_input = False
         self._side_stream = None
         self._side_used = False
         # eval mode: every BatchNorm folded into the conv before it (pcms_bn_fold) and the ReLU
@@ -871,7 +875,8 @@ class UNetEngine:
             self._bn_epoch += training
         b = self.bufs
         S, C = b["S"], b["C"]
-        call("pcms_pack_input", self.code, x, b["xin"], N, self.nmod, D * H * W, self.cp)
+        if not self.ablate_skip_pack_input:
+            call("pcms_pack_input", self.code, x, b["xin"], N, self.nmod, D * H * W, self.cp)
         # encoder
         inp, cin = b["xin"], self.cp
         for l in range(5):

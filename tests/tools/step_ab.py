@@ -1,6 +1,6 @@
 """In-step A/B of engine knobs on ONE box (test tooling): the bench workload (2 x 5x128x128x64,
-BCEDice, Adam) stepped with each variant in turn, rounds interleaved so box drift hits every
-variant alike; HIP events around K back-to-back steps, median over rounds.
+BCEDice, Adam) stepped with each variant in turn, rounds interleaved in ABBA order so box
+drift hits every variant alike; HIP events around K back-to-back steps, median over rounds.
 
     python tests/tools/step_ab.py [--rounds 4] [--steps 10] [--variants base,nobnin,...]
 
@@ -8,7 +8,7 @@ Variants: base (the defaults), nobnin (engine.fuse_bnin off), densewg (stem weig
 in the dense-column form), split256 / split512 (engine.split_target), x6sync / x6dma (the fp32
 build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32),
 wred1 / wred0 (the weight gradient's split rows summed in one launch / by the two-stage pair),
-sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
+nopack (the input pack skipped: the upper bound of folding it into the stem kernels), sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
 (engine.wgrad_target = N), q:NAME=V (the library switch pcms_NAME set to V, restored after)."""
 import argparse
 import os
@@ -38,7 +38,7 @@ def main():
     b = make_batch(2, (128, 128, 64), seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
     dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target, "side": eng.wgrad_side_min_level,
-            "wt": eng.wgrad_target}
+            "wt": eng.wgrad_target, "nopack": eng.ablate_skip_pack_input}
     dense0 = L.query("pcms_stem_wgrad_dense", -1)
     x6dma0 = L.query("pcms_conv3_wgrad_x6_dma", -1)
     wred0 = L.query("pcms_conv3_wgrad_reduce_fused", -1)
@@ -53,6 +53,7 @@ def main():
         eng.fuse_bnin, eng.split_target = dflt["fuse_bnin"], dflt["split_target"]
         eng.wgrad_side_min_level = dflt["side"]
         eng.wgrad_target = dflt["wt"]
+        eng.ablate_skip_pack_input = dflt["nopack"]
         L.query("pcms_stem_wgrad_dense", dense0)
         L.query("pcms_conv3_wgrad_x6_dma", x6dma0)
         L.query("pcms_conv3_wgrad_reduce_fused", wred0)
@@ -60,6 +61,8 @@ def main():
             eng.fuse_bnin = False
         elif v == "bnin":
             eng.fuse_bnin = True
+        elif v == "nopack":
+            eng.ablate_skip_pack_input = True
         elif v == "densewg":
             L.query("pcms_stem_wgrad_dense", 1)
         elif v == "tapswg":
@@ -84,7 +87,9 @@ def main():
     names = a.variants.split(",")
     res = {v: [] for v in names}
     for r in range(a.rounds):
-        for v in names:
+        # ABBA order (odd rounds reversed): a box whose clock drifts over the run moves every
+        # variant alike instead of favouring the one that always runs later in a round
+        for v in (names if r % 2 == 0 else names[::-1]):
             setup(v)
             for _ in range(2):
                 tr.step(batch)
