@@ -162,6 +162,11 @@ class UNetEngine:
         # small latency-bound launches beside the dgrad chain; the big levels' persistent grids
         # straggle when they share the chip).  99: never
         self.wgrad_side_min_level = 99
+        # the ConvTranspose weight + bias gradient (HBM-bound: it streams the up-path gradient,
+        # 268 MB at level 0) on the side stream beside the same layer's ConvT dgrad (also
+        # HBM-bound, reading the same tensor); joined before the next block's backward.  Its
+        # partial rows then get their own workspace (ctws_w) instead of sharing ctws.
+        self.convt_wgrad_side = False
         # ablation only (tests/tools/step_ab.py nopack): skip the input pack, so the stem reads
         # the previous step's packed input -- bounds what folding pack_input into the stem
         # kernels could save; never set in the product (the forward is wrong with it)
@@ -290,8 +295,8 @@ class UNetEngine:
     def _side_at(self, lvl: int) -> bool:
         return self.wgrad_side_stream or lvl >= self.wgrad_side_min_level
 
-    def _side(self, lvl: int):
-        if not self._side_at(lvl):
+    def _side(self, lvl: int, on: Optional[bool] = None):
+        if not (self._side_at(lvl) if on is None else on):
             return contextlib.nullcontext()
         if self._side_stream is None:
             self._side_stream = torch.cuda.Stream(device=self.device)
@@ -602,7 +607,7 @@ class UNetEngine:
         # the workspaces below are sized for the current split / weight-gradient workgroup
         # targets: a changed target re-lays them out (a larger one would otherwise overrun them)
         key = (N, D, H, W, self.act_ckpt, self.wgrad_side_stream, self.wgrad_side_min_level, self.wgrad_target,
-               self.split_target)
+               self.split_target, self.convt_wgrad_side)
         if self.buf_key == key:
             return
         self.bufs = None
@@ -689,6 +694,9 @@ class UNetEngine:
         self.stem_sup = query("pcms_stem_supported", N, D, H, W) if self.stem_fast else 0
         ctws = [query("pcms_convt_wgrad_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels, 512)
                 for i, up in enumerate(self.ups)]
+        if self.convt_wgrad_side:  # the weight gradient's rows apart: the dgrad runs beside it
+            b["ctws_w"] = torch.empty(max(ctws), dtype=torch.float32, device=dev)
+            ctws = []
         # the ConvT dgrad's K slabs share it (the weight gradient has reduced it by then)
         ctws += [query("pcms_convt_dgrad_ws_floats", N, *S[4 - i], up.in_channels, up.out_channels)
                  for i, up in enumerate(self.ups)]
@@ -1048,8 +1056,10 @@ class UNetEngine:
             hin = b["e4_x"] if i == 0 else b[f"d{l + 1}_a2"]
             # weight and bias gradients in one pass over gu (the bias sum over the ConvT output
             # box, F.pad's front offsets floor((S[l] - 2 S[l + 1]) / 2))
-            call("pcms_convt_wgrad_bias", self.code, hin, gu, up.weight.grad, up.bias.grad, b["ctws"], b["redws"], N,
-                 *S[l + 1], up.in_channels, up.out_channels, *S[l], 512)
+            with self._side(l, self.convt_wgrad_side):
+                call("pcms_convt_wgrad_bias", self.code, hin, gu, up.weight.grad, up.bias.grad,
+                     b["ctws_w"] if self.convt_wgrad_side else b["ctws"], b["redws"], N, *S[l + 1], up.in_channels,
+                     up.out_channels, *S[l], 512)
             self._grads_done(up.weight, up.bias)
             gnext = b["gx4"] if i == 0 else b[f"gA{l + 1}"]
             call("pcms_convt_dgrad_ws", self.code, gu, dpack, gnext, b["ctws"], N, *S[l + 1], up.in_channels,

@@ -408,3 +408,40 @@ def test_bnin_fusion_step_bit_identical():
         assert torch.equal(b0, b1)
     finally:
         L.query("pcms_conv3_big_min_boxes", old)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ckpt", [False, True])
+def test_convt_wgrad_side_step_bit_identical(ckpt):
+    """The ConvTranspose weight + bias gradients on the side stream beside the ConvT dgrad
+    (engine.convt_wgrad_side, their own partial-row workspace) give the same two bf16 training
+    steps bit for bit as the serial order: logits, losses, every gradient, the Adam updates and
+    the BatchNorm buffers (2 x 64x64x32; with and without decoder checkpointing, whose recompute
+    joins the side stream first)."""
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    gen = torch.Generator().manual_seed(9)
+    x = torch.rand(2, 5, 64, 64, 32, generator=gen).cuda()
+    y = (torch.rand(2, 1, 64, 64, 32, generator=gen) < 0.4).float().cuda()
+    runs = []
+    for side in (False, True):
+        torch.manual_seed(0)
+        m = UNet3D(n_modalities=5, n_classes=1, checkpoint_decoder=ckpt).cuda()
+        eng = m.engine()
+        eng.convt_wgrad_side = side
+        opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
+        out = []
+        for _ in range(2):
+            opt.zero_grad()
+            lg = m(x)
+            loss = BCEDiceLoss()(lg, y)
+            loss.backward()
+            g = eng.flat_g.clone()
+            opt.step()
+            out += [lg.detach().clone(), loss.detach().clone(), g]
+        torch.cuda.synchronize()
+        assert ("ctws_w" in eng.bufs) == side
+        runs.append(out + [eng.flat_p.clone(), eng.flat_bn.clone()])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)

@@ -8,7 +8,7 @@ Variants: base (the defaults), nobnin (engine.fuse_bnin off), densewg (stem weig
 in the dense-column form), split256 / split512 (engine.split_target), x6sync / x6dma (the fp32
 build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32),
 wred1 / wred0 (the weight gradient's split rows summed in one launch / by the two-stage pair),
-nopack (the input pack skipped: the upper bound of folding it into the stem kernels), sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
+ctside (ConvT weight gradient on the side stream), nopack (the input pack skipped: the upper bound of folding it into the stem kernels), sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
 (engine.wgrad_target = N), q:NAME=V (the library switch pcms_NAME set to V, restored after)."""
 import argparse
 import os
@@ -38,7 +38,7 @@ def main():
     b = make_batch(2, (128, 128, 64), seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
     dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target, "side": eng.wgrad_side_min_level,
-            "wt": eng.wgrad_target, "nopack": eng.ablate_skip_pack_input}
+            "wt": eng.wgrad_target, "nopack": eng.ablate_skip_pack_input, "ctside": eng.convt_wgrad_side}
     dense0 = L.query("pcms_stem_wgrad_dense", -1)
     x6dma0 = L.query("pcms_conv3_wgrad_x6_dma", -1)
     wred0 = L.query("pcms_conv3_wgrad_reduce_fused", -1)
@@ -54,6 +54,7 @@ def main():
         eng.wgrad_side_min_level = dflt["side"]
         eng.wgrad_target = dflt["wt"]
         eng.ablate_skip_pack_input = dflt["nopack"]
+        eng.convt_wgrad_side = dflt["ctside"]
         L.query("pcms_stem_wgrad_dense", dense0)
         L.query("pcms_conv3_wgrad_x6_dma", x6dma0)
         L.query("pcms_conv3_wgrad_reduce_fused", wred0)
@@ -61,6 +62,8 @@ def main():
             eng.fuse_bnin = False
         elif v == "bnin":
             eng.fuse_bnin = True
+        elif v in ("ctside", "ctmain"):
+            eng.convt_wgrad_side = v == "ctside"
         elif v == "nopack":
             eng.ablate_skip_pack_input = True
         elif v == "densewg":
