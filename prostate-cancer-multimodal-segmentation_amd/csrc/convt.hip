@@ -731,6 +731,9 @@ __global__ void __launch_bounds__(512, 1) convt_wgrad_kernel(const T* x, const T
 #ifndef CTW_PF
 #define CTW_PF 1
 #endif
+#ifndef CTW_OMAP
+#define CTW_OMAP 0
+#endif
 template <bool NT, int TT, bool DIRECT>
 __global__ void __launch_bounds__(512, (TT <= 4 && !CTW_PF) ? 2 : 1) convt_wgrad128_kernel(const bf16_t* x, const bf16_t* dout,
                                                                              float* ws, UpGeom g, int Cin, int Cout,
@@ -765,6 +768,21 @@ __global__ void __launch_bounds__(512, (TT <= 4 && !CTW_PF) ? 2 : 1) convt_wgrad
   // written to LDS, so their latency runs under this block's MFMAs (without it each block's
   // loads -> LDS -> MFMAs run in series)
   u32x4_t stg[PT];
+  // dout piece r (0 .. TT VB PPR) -> (tap t of the group, block voxel v, 16-B piece q).
+  // CTW_OMAP 0: tap-major (a wave-instruction reads 8 child rows 256 B apart: every other
+  // voxel of an output row).  1: the two k taps of each (i, j) interleaved in output-voxel
+  // order, so a wave-instruction reads 1 KiB of contiguous output rows (child (2w + k))
+  auto dout_piece = [&](int r, int& t, int& v, int& q) {
+    q = r % PPR;
+    if constexpr (CTW_OMAP && TT >= 2) {
+      const int pair = r / (2 * VB * PPR), ow = (r % (2 * VB * PPR)) / PPR;
+      t = 2 * pair + (ow & 1);
+      v = ow >> 1;
+    } else {
+      t = r / (VB * PPR);
+      v = (r % (VB * PPR)) / PPR;
+    }
+  };
   auto load_block = [&](long vb) {
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
@@ -777,10 +795,10 @@ __global__ void __launch_bounds__(512, (TT <= 4 && !CTW_PF) ? 2 : 1) convt_wgrad
         const long m = std::min<long>(vb + v, vend - 1);
         src = x + m * Cin + p0 + hf * 64 + (rem % PPR) * 8;
       } else {                                   // dout tap tb + t
-        const int t = (pc - XP) / (VB * PPR), rem = (pc - XP) % (VB * PPR);
-        v = rem / PPR;
+        int t, q;
+        dout_piece(pc - XP, t, v, q);
         const long m = std::min<long>(vb + v, vend - 1);
-        src = dout + child_vox(g, m, tb + t) * Cout + co0 + (rem % PPR) * 8;
+        src = dout + child_vox(g, m, tb + t) * Cout + co0 + q * 8;
       }
       stg[i] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src))
                   : *reinterpret_cast<const u32x4_t*>(src);
@@ -807,8 +825,13 @@ __global__ void __launch_bounds__(512, (TT <= 4 && !CTW_PF) ? 2 : 1) convt_wgrad
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const int pc = tid + i * 512;
-      const int tile = pc / (VB * PPR), rem = pc % (VB * PPR);  // tiles 0-1: x halves, 2..: taps
-      const int v = rem / PPR, q = rem % PPR;
+      int tile = pc / (VB * PPR), rem = pc % (VB * PPR);  // tiles 0-1: x halves, 2..: taps
+      int v = rem / PPR, q = rem % PPR;
+      if (pc >= XP) {
+        int t;
+        dout_piece(pc - XP, t, v, q);
+        tile = 2 + t;
+      }
       *reinterpret_cast<u32x4_t*>(lds + tile * VB * ROW + half_swz(v, q * 8)) = stg[i];
     }
     __syncthreads();
