@@ -343,6 +343,9 @@ __global__ void __launch_bounds__(64 * kCfRL) colsum_finalize_small_kernel(
   }
 }
 
+#ifndef BNA_REV
+#define BNA_REV 0
+#endif
 // NT: as bn_relu_kernel (level-0 apply: 805 MB in 118 us = 6.8 TB/s)
 template <typename T, bool NT>
 __global__ void __launch_bounds__(TPB) bn_relu_bwd_apply_kernel(
@@ -359,7 +362,11 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_apply_kernel(
     sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
     k1[j] = coef[c * 3]; k2[j] = coef[c * 3 + 1]; k3[j] = coef[c * 3 + 2];
   }
-  for (long v = (long)blockIdx.x * VL + vl; v < nvox; v += (long)gridDim.x * VL) {
+  for (long v0 = (long)blockIdx.x * VL + vl; v0 < nvox; v0 += (long)gridDim.x * VL) {
+    // BNA_REV: walk the voxels from the end -- the reduce pass before this one finishes at the
+    // high voxels, so what it left in the Infinity Cache is read first (elementwise: any order
+    // gives the same bits)
+    const long v = BNA_REV ? nvox - 1 - v0 : v0;
     float dv[VEC], yv[VEC], o[VEC];
     ld16<NT>(da + v * C + c0, dv);
     ld16<NT>(y + v * C + c0, yv);
