@@ -1217,6 +1217,9 @@ constexpr int kMaxSplitSlabs = 16;  // slabs loaded together (more: summed one b
 // row is 4 rounds of slab loads instead of 16 (deep levels have few rows: level 4 is 8 rows x
 // 16 channel blocks, and each round is a full memory latency)
 constexpr int kSeThreads = 1024;
+#ifndef SE_BATCH
+#define SE_BATCH 0
+#endif
 template <typename T>
 __global__ void __launch_bounds__(kSeThreads) split_epilogue_kernel(const float* acc, int splits, const float* bias,
                                                                     T* y0, T* y1, int cy0, float* stats, int C,
@@ -1231,11 +1234,30 @@ __global__ void __launch_bounds__(kSeThreads) split_epilogue_kernel(const float*
   float xs[KPT];
   float s1 = 0.f, s2 = 0.f;
   int cntv = 0;
+#if SE_BATCH
+  // every slab load of the thread's KPT voxels issued before the first add: the store of a
+  // voxel may alias the next voxel's slabs for the compiler, so the per-voxel loop below ran
+  // KPT rounds of memory latency (same summation order either way)
+  float part[KPT][kMaxSplitSlabs];
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    const long v = v0 + vl + i * NV;
+#pragma unroll
+    for (int sp = 0; sp < kMaxSplitSlabs; ++sp)
+      if (sp < splits && v < nvox) part[i][sp] = acc[((long)sp * nvox + v) * C + c];
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < KPT; ++i) {
     const long v = v0 + vl + i * NV;
     xs[i] = 0.f;
     if (v >= nvox) continue;
+#if SE_BATCH
+    float x = part[i][0];
+#pragma unroll
+    for (int sp = 1; sp < kMaxSplitSlabs; ++sp)
+      if (sp < splits) x += part[i][sp];
+#else
     // the split slabs in split order (a fixed summation order); all of a voxel's slab loads
     // are issued before the first add (a load -> add chain per slab was latency-bound)
     float part[kMaxSplitSlabs];
@@ -1246,6 +1268,7 @@ __global__ void __launch_bounds__(kSeThreads) split_epilogue_kernel(const float*
 #pragma unroll
     for (int sp = 1; sp < kMaxSplitSlabs; ++sp)
       if (sp < splits) x += part[sp];
+#endif
     for (int sp = kMaxSplitSlabs; sp < splits; ++sp) x += acc[((long)sp * nvox + v) * C + c];
     x += bc;
     if (relu) x = fmaxf(x, 0.f);
