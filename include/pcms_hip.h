@@ -235,6 +235,19 @@ int pcms_maxpool_bwd_bn_rows(int dtype, int N, int D, int H, int W, int C);
 int pcms_maxpool_bwd_bn(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
                         const float* invstd, const void* dp, void* da, float* part, int N, int D, int H, int W,
                         int C, hipStream_t s);
+/* The same pair with da never written: pcms_maxpool_bwd_bn_sums writes only the partial rows
+ * (da, holding the skip part, is read); after pcms_bn_relu_bwd_finish(..., dy = NULL) has
+ * formed coef, pcms_maxpool_bn_apply forms da = da_skip + dp at the argmax again per 2x2x2 cell
+ * (rounded as pcms_maxpool_bwd_bn stores it) and writes dy = k1 g + k2 xhat + k3 -- the same
+ * dy bits as pcms_maxpool_bwd_bn + pcms_bn_relu_bwd_finish(dy), one tensor write and read
+ * fewer (engine.pool_bn_apply_fused; measured +0.19 % per step, so the engine keeps the pair
+ * above by default).                                                                      */
+int pcms_maxpool_bwd_bn_sums(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                             const float* invstd, const void* dp, const void* da, float* part, int N, int D, int H,
+                             int W, int C, hipStream_t s);
+int pcms_maxpool_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                          const float* invstd, const float* coef, const void* dp, const void* da, void* dy, int N,
+                          int D, int H, int W, int C, hipStream_t s);
 
 /* ---- ConvTranspose3d(k=2, s=2) + F.pad: models/unet3d.py:120,139-151 --------------- */
 /* the persistent bf16 forward used at Cin 128 / Cout 64 (level-0 Up3D): on (1) / off (0),

@@ -69,6 +69,8 @@ SIGNATURES = {
     "pcms_bn_relu_pool": "ipppppiiiiis",
     "pcms_maxpool_bwd_bn_rows": "iiiiii",
     "pcms_maxpool_bwd_bn": "ippppppppiiiiis",
+    "pcms_maxpool_bwd_bn_sums": "ippppppppiiiiis",
+    "pcms_maxpool_bn_apply": "ipppppppppiiiiis",
     "pcms_bn_relu_bwd_finish": "i" + "p" * 8 + "ippppilps",
     "pcms_convt_pack": "ippiiis",
     "pcms_convt_pack_elems": "iii",

@@ -346,6 +346,17 @@ __global__ void __launch_bounds__(64 * kCfRL) colsum_finalize_small_kernel(
 #ifndef BNA_REV
 #define BNA_REV 0
 #endif
+// BatchNorm + ReLU backward of one element, dy = k1 g + k2 xhat + k3 with g = da [y sc + sh > 0]:
+// the operations written out (fma(y, sc, sh) for the mask, fma(k2, xhat, k1 g) + k3) so that
+// every kernel applying it rounds the same way -- the compiler's own contraction of the plain
+// expression picked fma(k1, g, k2 xhat) in one kernel and fma(k2, xhat, k1 g) in another
+__device__ __forceinline__ float bn_bwd_dy(float da, float y, float sc, float sh, float mu, float is, float k1,
+                                           float k2, float k3) {
+#pragma clang fp contract(off)
+  const float g = __builtin_fmaf(y, sc, sh) > 0.f ? da : 0.f;
+  const float xhat = (y - mu) * is;
+  return __builtin_fmaf(k2, xhat, k1 * g) + k3;
+}
 // NT: as bn_relu_kernel (level-0 apply: 805 MB in 118 us = 6.8 TB/s)
 template <typename T, bool NT>
 __global__ void __launch_bounds__(TPB) bn_relu_bwd_apply_kernel(
@@ -371,10 +382,7 @@ __global__ void __launch_bounds__(TPB) bn_relu_bwd_apply_kernel(
     ld16<NT>(da + v * C + c0, dv);
     ld16<NT>(y + v * C + c0, yv);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      const float g = (yv[j] * sc[j] + sh[j] > 0.f) ? dv[j] : 0.f;
-      o[j] = k1[j] * g + k2[j] * ((yv[j] - mu[j]) * is[j]) + k3[j];
-    }
+    for (int j = 0; j < VEC; ++j) o[j] = bn_bwd_dy(dv[j], yv[j], sc[j], sh[j], mu[j], is[j], k1[j], k2[j], k3[j]);
     st16<NT>(dy + v * C + c0, o);
   }
 }
@@ -506,7 +514,9 @@ __global__ void __launch_bounds__(TPB) bn_relu_pool_kernel(const T* y, T* a, T* 
 // voxel (the floor-mode leftovers too), the partial sums of g = da [y sc + sh > 0] and g xhat
 // per channel: one [C][2] row per block (bn_relu_bwd_reduce_kernel's quantities), so the
 // BatchNorm backward needs no reduction pass over da and y of its own.
-template <typename T>
+// STORE false (pcms_maxpool_bwd_bn_sums): the same sums, da left as it was (the skip-path part
+// only) -- maxpool_bn_apply_kernel forms the pooled-path sum again where it applies the BN.
+template <typename T, bool STORE = true>
 __global__ void __launch_bounds__(TPB, 3) maxpool_bwd_bn_kernel(const T* y, const float* scale, const float* shift,
                                                              const float* mean, const float* invstd, const T* dp,
                                                              T* da, float* part, int N, int D, int H, int W,
@@ -603,7 +613,7 @@ __global__ void __launch_bounds__(TPB, 3) maxpool_bwd_bn_kernel(const T* y, cons
       if (whole) {
 #pragma unroll
         for (int j = 0; j < VEC; ++j) o[j] += (arg[j] == k) ? g[j] : 0.f;
-        store16<T>(da + vk(k) * C + cv * VEC, o);
+        if constexpr (STORE) store16<T>(da + vk(k) * C + cv * VEC, o);
       }
 #pragma unroll
       for (int q = 0; q < VEC / 2; ++q) {
@@ -634,6 +644,104 @@ __global__ void __launch_bounds__(TPB, 3) maxpool_bwd_bn_kernel(const T* y, cons
     float acc = 0.f;
     for (int t = t0; t < TPB; t += CV) acc += red[t][j][q];
     part[((long)blockIdx.x * C + c) * 2 + q] = acc;
+  }
+}
+
+// The consumer half of the pair above (pcms_maxpool_bn_apply): per 2x2x2 cell, the block
+// output's gradient da = gx + dp at the argmax -- recomputed from y exactly as
+// maxpool_bwd_bn_kernel forms it, rounded to T as that kernel stores it -- and then
+// bn_relu_bwd_apply_kernel's dy = k1 g + k2 xhat + k3 (its arithmetic, expression for
+// expression).  With pcms_maxpool_bwd_bn_sums before it, da is never written to HBM: this
+// pass reads gx + dp (+ 1/8 of a tensor) where the stored form wrote da and read it back.
+template <typename T, bool NT>
+// (two blocks per CU: its 7 x VEC per-channel coefficients do not fit the three-block budget)
+__global__ void __launch_bounds__(TPB, 2) maxpool_bn_apply_kernel(const T* y, const float* scale, const float* shift,
+                                                               const float* mean, const float* invstd,
+                                                               const float* coef, const T* dp, const T* gx, T* dy,
+                                                               int N, int D, int H, int W, int C) {
+  constexpr int VEC = Elem<T>::kVec;
+  const int Dc = (D + 1) / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2, CV = C / VEC;
+  const int Do = D / 2, Ho = H / 2, Wo = W / 2;
+  const long total = (long)N * Dc * Hc * Wc * CV;
+  const long stride = (long)gridDim.x * blockDim.x;  // multiple of CV (host)
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int cv = (int)(i % CV);
+  float sc[VEC], sh[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], k3[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    const int c = cv * VEC + j;
+    sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
+    k1[j] = coef[c * 3]; k2[j] = coef[c * 3 + 1]; k3[j] = coef[c * 3 + 2];
+  }
+  for (; i < total; i += stride) {
+    uint32_t r = (uint32_t)(i / CV);
+    const int wc = r % Wc; r /= Wc;
+    const int hc = r % Hc; r /= Hc;
+    const int dc = r % Dc; const long n = r / Dc;
+    const bool whole = dc < Do && hc < Ho && wc < Wo;
+    const long v0 = ((n * D + 2 * dc) * H + 2 * hc) * W + 2 * wc;
+    const bool ind = 2 * dc + 1 < D, inh = 2 * hc + 1 < H, inw = 2 * wc + 1 < W;
+    auto vk = [&](int k) { return v0 + (long)(k >> 2) * H * W + ((k >> 1) & 1) * W + (k & 1); };
+    auto ink = [&](int k) { return (!(k & 4) || ind) && (!(k & 2) || inh) && (!(k & 1) || inw); };
+    // raw 16-B vectors (4 registers each), unpacked where used: the cell's 16 loads and its
+    // dp load all in flight before the first use, in maxpool_bwd_bn_kernel's register budget
+    auto unpack = [](const u32x4_t r, float (&o)[VEC]) {
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { o[2 * q] = __uint_as_float(r[q] << 16); o[2 * q + 1] = __uint_as_float(r[q] & 0xffff0000u); }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = __uint_as_float(r[q]);
+      }
+    };
+    auto ldraw = [](const T* p) -> u32x4_t {
+      if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+      else return *reinterpret_cast<const u32x4_t*>(p);
+    };
+    u32x4_t yr[8], dr[8], gr = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      yr[k] = (u32x4_t){0u, 0u, 0u, 0u};
+      dr[k] = yr[k];
+      if (ink(k)) {
+        yr[k] = ldraw(y + vk(k) * C + cv * VEC);
+        dr[k] = ldraw(gx + vk(k) * C + cv * VEC);
+      }
+    }
+    if (whole) gr = *reinterpret_cast<const u32x4_t*>(dp + (((n * Do + dc) * Ho + hc) * Wo + wc) * C + cv * VEC);
+    float g[VEC], m[VEC];
+    int arg[VEC];
+    unpack(gr, g);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; arg[j] = 0; }
+    if (whole) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float yv[VEC];
+        unpack(yr[k], yv);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float av = round_st<T>(bn_relu1(yv[j], sc[j], sh[j]));
+          if (av > m[j] || (av != av && m[j] == m[j])) { m[j] = av; arg[j] = k; }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (!ink(k)) continue;
+      float yv[VEC], o[VEC], out[VEC];
+      u32x4_t yk = yr[k];
+      asm volatile("" : "+v"(yk));  // (as maxpool_bwd_bn_kernel: keep the argmax pass's values dead)
+      unpack(yk, yv);
+      unpack(dr[k], o);
+      if (whole) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o[j] = round_st<T>(o[j] + ((arg[j] == k) ? g[j] : 0.f));
+      }
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) out[j] = bn_bwd_dy(o[j], yv[j], sc[j], sh[j], mu[j], is[j], k1[j], k2[j], k3[j]);
+      st16<NT>(dy + vk(k) * C + cv * VEC, out);
+    }
   }
 }
 
@@ -1562,6 +1670,44 @@ int pcms_maxpool_bwd_bn(int dtype, const void* y, const float* scale, const floa
   else
     hipLaunchKernelGGL(maxpool_bwd_bn_kernel<float>, dim3(grid), dim3(TPB), 0, s, (const float*)y, scale, shift,
                        mean, invstd, (const float*)dp, (float*)da, part, N, D, H, W, C);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_maxpool_bwd_bn_sums(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                             const float* invstd, const void* dp, const void* da, float* part, int N, int D, int H,
+                             int W, int C, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC || TPB % (C / VEC)) return -1;
+  const long cells = (long)N * ((D + 1) / 2) * ((H + 1) / 2) * ((W + 1) / 2);
+  if (cells * 8 >= (1L << 31)) return -7;
+  const int grid = pcms_maxpool_bwd_bn_rows(dtype, N, D, H, W, C);
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((maxpool_bwd_bn_kernel<bf16_t, false>), dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, scale,
+                       shift, mean, invstd, (const bf16_t*)dp, (bf16_t*)const_cast<void*>(da), part, N, D, H, W, C);
+  else
+    hipLaunchKernelGGL((maxpool_bwd_bn_kernel<float, false>), dim3(grid), dim3(TPB), 0, s, (const float*)y, scale,
+                       shift, mean, invstd, (const float*)dp, (float*)const_cast<void*>(da), part, N, D, H, W, C);
+  PCMS_CHECK_LAUNCH();
+}
+
+int pcms_maxpool_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const float* mean,
+                          const float* invstd, const float* coef, const void* dp, const void* da, void* dy, int N,
+                          int D, int H, int W, int C, hipStream_t s) {
+  const int VEC = dtype == PCMS_BF16 ? 8 : 4;
+  if (C % VEC || TPB % (C / VEC)) return -1;
+  const long cells = (long)N * ((D + 1) / 2) * ((H + 1) / 2) * ((W + 1) / 2);
+  if (cells * 8 >= (1L << 31)) return -7;
+  const int CV = C / VEC;
+  const int grid = cell_grid(cells * CV, CV, 8192);
+  const bool nt = (long)N * D * H * W * C * (dtype == PCMS_BF16 ? 2 : 4) >= kNtBytesBn;
+  if (dtype == PCMS_BF16)
+    hipLaunchKernelGGL((nt ? maxpool_bn_apply_kernel<bf16_t, true> : maxpool_bn_apply_kernel<bf16_t, false>),
+                       dim3(grid), dim3(TPB), 0, s, (const bf16_t*)y, scale, shift, mean, invstd, coef,
+                       (const bf16_t*)dp, (const bf16_t*)da, (bf16_t*)dy, N, D, H, W, C);
+  else
+    hipLaunchKernelGGL((nt ? maxpool_bn_apply_kernel<float, true> : maxpool_bn_apply_kernel<float, false>),
+                       dim3(grid), dim3(TPB), 0, s, (const float*)y, scale, shift, mean, invstd, coef,
+                       (const float*)dp, (const float*)da, (float*)dy, N, D, H, W, C);
   PCMS_CHECK_LAUNCH();
 }
 

@@ -167,6 +167,13 @@ class UNetEngine:
         # HBM-bound, reading the same tensor); joined before the next block's backward.  Its
         # partial rows then get their own workspace (ctws_w) instead of sharing ctws.
         self.convt_wgrad_side = False
+        # the encoder's MaxPool3d backward + BN-backward reduction without rewriting the block
+        # output's gradient (pcms_maxpool_bwd_bn_sums), the pooled part added again in that
+        # BatchNorm's apply (pcms_maxpool_bn_apply): the same dy bits, one write + read of the
+        # level's tensor fewer.  Measured +0.19 % per step (the per-cell apply streams at ~5.3 TB/s
+        # where the per-voxel apply it replaces runs at ~6.2; profiles/r6_pool_bn_apply_fused_ab.txt):
+        # off, i.e. pcms_maxpool_bwd_bn + pcms_bn_relu_bwd_finish
+        self.pool_bn_apply_fused = False
         # ablation only (tests/tools/step_ab.py nopack): skip the input pack, so the stem reads
         # the previous step's packed input -- bounds what folding pack_input into the stem
         # kernels could save; never set in the product (the forward is wrong with it)
@@ -921,12 +928,14 @@ class UNetEngine:
 
     # ------------------------------------------------------------------ backward
     def _block_bwd(self, blk: BlockSpec, ga2, acts, x0, c0, x1, c1, gx_out0, gx_out1, cy0, N, S, lvl,
-                   bn1_rows: int = 0):
+                   bn1_rows: int = 0, pool_dp=None):
         """Backward of one DoubleConv block. ga2: grad of block output (None: the second
         BN + ReLU backward was already done by its consumer, gY{lvl} holds dy2).  Writes the
         grad of the block input into gx_out0 (channels [0, cy0)) / gx_out1 (rest); None = skip.
         ``bn1_rows``: the second BatchNorm's backward partial rows are already in the stats
-        buffer (written by pcms_maxpool_bwd_bn), only its finish + apply run here."""
+        buffer (written by pcms_maxpool_bwd_bn), only its finish + apply run here.  ``pool_dp``:
+        they came from pcms_maxpool_bwd_bn_sums (ga2 holds the skip part only) and the apply
+        adds the pooled gradient ``pool_dp`` itself (pcms_maxpool_bn_apply)."""
         b = self.bufs
         nvox = N * S[0] * S[1] * S[2]
         # the previous block's weight gradients (side stream) read this level's buffers until
@@ -937,8 +946,11 @@ class UNetEngine:
         if ga2 is not None and bn1_rows:
             m = blk.b1.mod
             call("pcms_bn_relu_bwd_finish", self.code, ga2, acts["y2"], blk.b1.scale, blk.b1.shift, blk.b1.mean,
-                 blk.b1.invstd, m.weight, b["stats"], bn1_rows, b["coef"], m.weight.grad, m.bias.grad, gY, blk.b1.c,
-                 nvox, b["bnws"])
+                 blk.b1.invstd, m.weight, b["stats"], bn1_rows, b["coef"], m.weight.grad, m.bias.grad,
+                 gY if pool_dp is None else None, blk.b1.c, nvox, b["bnws"])
+            if pool_dp is not None:
+                call("pcms_maxpool_bn_apply", self.code, acts["y2"], blk.b1.scale, blk.b1.shift, blk.b1.mean,
+                     blk.b1.invstd, b["coef"], pool_dp, ga2, gY, N, *S, blk.b1.c)
         elif ga2 is not None:
             self._bn_bwd(blk.b1, ga2, acts["y2"], gY, nvox)
         if ga2 is not None:
@@ -1066,21 +1078,25 @@ class UNetEngine:
                  up.out_channels, *S[l])
             g = gnext
         # encoder, deepest first; gx{l} holds the skip gradient already (l < 4)
-        rows = 0
+        rows, pool_dp = 0, None
         for l in reversed(range(5)):
             blk = self.enc[l]
             acts = {"y1": b[f"e{l}_y1"], "a1": b[f"e{l}_a1"], "y2": b[f"e{l}_y2"]}
             if l == 0:
                 self._block_bwd(blk, b["gx0"], acts, b["xin"], self.cp, None, 0, None, None, 0, N, S[0], 0,
-                                bn1_rows=rows)
+                                bn1_rows=rows, pool_dp=pool_dp)
             else:
                 gp = b[f"gU{l}"]
                 self._block_bwd(blk, b[f"gx{l}"], acts, b[f"pool{l}"], C[l - 1], None, 0, gp, None, C[l - 1], N,
-                                S[l], l, bn1_rows=rows)
+                                S[l], l, bn1_rows=rows, pool_dp=pool_dp)
                 # MaxPool3d backward + the next block's second BN-backward reduction, one pass
+                # (fused form: the pooled gradient is added again by that block's BN apply, so
+                # the block output's gradient gx{l-1} is not rewritten)
                 bn = self.enc[l - 1].b1
-                call("pcms_maxpool_bwd_bn", self.code, b[f"e{l - 1}_y2"], bn.scale, bn.shift, bn.mean, bn.invstd, gp,
-                     b[f"gx{l - 1}"], b["stats"], N, *S[l - 1], C[l - 1])
+                call("pcms_maxpool_bwd_bn_sums" if self.pool_bn_apply_fused else "pcms_maxpool_bwd_bn", self.code,
+                     b[f"e{l - 1}_y2"], bn.scale, bn.shift, bn.mean, bn.invstd, gp, b[f"gx{l - 1}"], b["stats"], N,
+                     *S[l - 1], C[l - 1])
+                pool_dp = gp if self.pool_bn_apply_fused else None
                 rows = query("pcms_maxpool_bwd_bn_rows", self.code, N, *S[l - 1], C[l - 1])
         self._join_side()  # every weight gradient before the optimizer / all-reduce wait
         self.saved_epoch = -1

@@ -572,7 +572,23 @@ def test_bn_relu_pool_and_maxpool_bwd_bn(dt, code, tol, S, C):
     dg1, db1, dy1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.full_like(yd, float("nan"))
     L.call("pcms_bn_relu_bwd_finish", code, da1, yd, sc, sh, mean, invstd, gd, part, r1, coef, dg1, db1, dy1, C, nvox,
            bnws)
+    part1 = part[: r1 * C * 2].clone()
+    # the consumer form (engine.pool_bn_apply_fused): the same rows without rewriting da, then
+    # the pooled part added again inside the apply -- the same dy bits
+    da2 = ndhwc(skip).to(DEV)
+    part.fill_(float("nan"))
+    L.call("pcms_maxpool_bwd_bn_sums", code, yd, sc, sh, mean, invstd, dpd, da2, part, N, *S, C)
+    part2 = part[: r1 * C * 2].clone()
+    dg2, db2, dy2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.full_like(yd, float("nan"))
+    L.call("pcms_bn_relu_bwd_finish", code, da2, yd, sc, sh, mean, invstd, gd, part, r1, coef, dg2, db2, None, C, nvox,
+           bnws)
+    L.call("pcms_maxpool_bn_apply", code, yd, sc, sh, mean, invstd, coef, dpd, da2, dy2, N, *S, C)
     torch.cuda.synchronize()
+    assert torch.equal(da2, ndhwc(skip).to(DEV)), "pcms_maxpool_bwd_bn_sums wrote da"
+    assert torch.equal(part1, part2), "partial rows differ"
+    assert torch.equal(dg1, dg2) and torch.equal(db1, db2)
+    bad = (dy1 != dy2).nonzero()
+    assert bad.numel() == 0, (bad[:8].tolist(), dy1[dy1 != dy2][:8].tolist(), dy2[dy1 != dy2][:8].tolist())
     assert torch.equal(a0, a1) and torch.equal(p0, p1)
     assert torch.equal(da0, da1)
     close(dg1.cpu(), dg0.cpu(), 1e-5, "dgamma fused vs unfused")

@@ -445,3 +445,40 @@ def test_convt_wgrad_side_step_bit_identical(ckpt):
         runs.append(out + [eng.flat_p.clone(), eng.flat_bn.clone()])
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("S", [(64, 64, 32), (20, 18, 24)])
+def test_pool_bn_apply_fused_step_bit_identical(precision, S):
+    """The encoder's MaxPool3d backward writing only the BN-backward partial rows
+    (pcms_maxpool_bwd_bn_sums) with the pooled gradient added again inside that BatchNorm's
+    apply (pcms_maxpool_bn_apply, engine.pool_bn_apply_fused) gives the same two training steps
+    bit for bit as pcms_maxpool_bwd_bn + pcms_bn_relu_bwd_finish: logits, losses, every
+    gradient, the Adam updates and the BatchNorm buffers -- at an even size and at one whose
+    odd levels leave floor-mode leftovers (partial 2x2x2 cells)."""
+    from pcms_amd.models.unet3d import UNet3D
+    from pcms_amd.optim import FlatAdam
+    from pcms_amd.utils.losses import BCEDiceLoss
+    gen = torch.Generator().manual_seed(10)
+    x = torch.rand(2, 5, *S, generator=gen).cuda()
+    y = (torch.rand(2, 1, *S, generator=gen) < 0.4).float().cuda()
+    runs = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        m = UNet3D(n_modalities=5, n_classes=1, precision=precision).cuda()
+        eng = m.engine()
+        eng.pool_bn_apply_fused = fused
+        opt = FlatAdam(m, lr=1e-3, weight_decay=1e-5)
+        out = []
+        for _ in range(2):
+            opt.zero_grad()
+            lg = m(x)
+            loss = BCEDiceLoss()(lg, y)
+            loss.backward()
+            out += [lg.detach().clone(), loss.detach().clone(), eng.flat_g.clone()]
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append(out + [eng.flat_p.clone(), eng.flat_bn.clone()])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)

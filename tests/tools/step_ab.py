@@ -8,7 +8,7 @@ Variants: base (the defaults), nobnin (engine.fuse_bnin off), densewg (stem weig
 in the dense-column form), split256 / split512 (engine.split_target), x6sync / x6dma (the fp32
 build's weight gradient staged synchronously / streamed by LDS-DMA; with --precision fp32),
 wred1 / wred0 (the weight gradient's split rows summed in one launch / by the two-stage pair),
-ctside (ConvT weight gradient on the side stream), nopack (the input pack skipped: the upper bound of folding it into the stem kernels), sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
+ctside (ConvT weight gradient on the side stream), poolsep / poolfused (engine.pool_bn_apply_fused off / on), nopack (the input pack skipped: the upper bound of folding it into the stem kernels), sideK (conv weight gradients of levels >= K on the side stream; side99 = never), wtN
 (engine.wgrad_target = N), q:NAME=V (the library switch pcms_NAME set to V, restored after)."""
 import argparse
 import os
@@ -38,7 +38,8 @@ def main():
     b = make_batch(2, (128, 128, 64), seed=1)
     batch = {"image": b["image"].cuda(), "label": b["label"].cuda()}
     dflt = {"fuse_bnin": eng.fuse_bnin, "split_target": eng.split_target, "side": eng.wgrad_side_min_level,
-            "wt": eng.wgrad_target, "nopack": eng.ablate_skip_pack_input, "ctside": eng.convt_wgrad_side}
+            "wt": eng.wgrad_target, "nopack": eng.ablate_skip_pack_input, "ctside": eng.convt_wgrad_side,
+            "pool": eng.pool_bn_apply_fused}
     dense0 = L.query("pcms_stem_wgrad_dense", -1)
     x6dma0 = L.query("pcms_conv3_wgrad_x6_dma", -1)
     wred0 = L.query("pcms_conv3_wgrad_reduce_fused", -1)
@@ -55,6 +56,7 @@ def main():
         eng.wgrad_target = dflt["wt"]
         eng.ablate_skip_pack_input = dflt["nopack"]
         eng.convt_wgrad_side = dflt["ctside"]
+        eng.pool_bn_apply_fused = dflt["pool"]
         L.query("pcms_stem_wgrad_dense", dense0)
         L.query("pcms_conv3_wgrad_x6_dma", x6dma0)
         L.query("pcms_conv3_wgrad_reduce_fused", wred0)
@@ -62,6 +64,8 @@ def main():
             eng.fuse_bnin = False
         elif v == "bnin":
             eng.fuse_bnin = True
+        elif v in ("poolsep", "poolfused"):
+            eng.pool_bn_apply_fused = v == "poolfused"
         elif v in ("ctside", "ctmain"):
             eng.convt_wgrad_side = v == "ctside"
         elif v == "nopack":
